@@ -1,0 +1,181 @@
+/*
+ * libstx — MI355X (gfx950 / CDNA4) kernels for the tupini07/StyleTransfer hot
+ * path, behind a plain C ABI.  All pointers are DEVICE pointers to fp32 NCHW
+ * contiguous tensors unless stated; `stream` is a hipStream_t (NULL = legacy
+ * default stream).  Every entry point is asynchronous on `stream`, performs no
+ * allocation and no host synchronisation, and returns 0 on success or a
+ * non-zero STX_E_* / hipError_t code (message via stx_last_error_string()).
+ * Kernels are graph-capturable.
+ *
+ * Reference interfaces replaced (all in /root/reference, tupini07/StyleTransfer):
+ *   conv2d fwd/dgrad/wgrad  <- torchvision vgg19 `.features` Conv2d layers sliced in
+ *                              stransfer/network.py:246-314 and the ImageTransformNet
+ *                              Conv2d layers stransfer/network.py:468-481,525-609
+ *   gram / style loss       <- StyleLoss.gram_matrix / forward  stransfer/network.py:92-123
+ *   mse losses              <- ContentLoss.forward :155-164, FeatureReconstructionLoss.forward :186-201
+ *   maxpool / relu          <- VGG MaxPool2d / ReLU(inplace=False) stransfer/network.py:270-271
+ *   adam                    <- torch.optim.Adam via get_content_optimizer :403-409, get_optimizer :643-649
+ *   instance norm           <- nn.InstanceNorm2d(affine=True) stransfer/network.py:474,483,531,...,600
+ *   residual add            <- ResidualBlock.forward `out += residual` :502
+ *   upsample nearest x2     <- nn.Upsample(mode='nearest', scale_factor=2) :580-581,592-593
+ *   total variation         <- get_total_variation_regularization_loss :621-641
+ */
+#ifndef STX_H_
+#define STX_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STX_OK 0
+#define STX_E_INVALID 1001   /* bad argument / unsupported shape */
+#define STX_E_WORKSPACE 1002 /* workspace too small */
+
+/* input-loader modes for stx_conv2d: how the virtual conv input is formed
+ * from the physical tensor x (fused into the LDS halo load) */
+#define STX_IN_RAW 0        /* v = x                                            */
+#define STX_IN_RELU 1       /* v = max(x, 0)              (VGG ReLU, not in-place) */
+#define STX_IN_RELU_POOL2 2 /* v = maxpool2x2(max(x,0))   (VGG ReLU + MaxPool2d) */
+#define STX_IN_UPSAMPLE2 3  /* v = x[y/2][x/2]            (nn.Upsample nearest x2) */
+#define STX_IN_DILATE2 4    /* v = x[y/2][x/2] at even y,x else 0 (stride-2 dgrad) */
+
+typedef struct stx_conv_params {
+  const float* x;     /* physical input [n][cin][h][w] */
+  const float* wt;    /* prepped weights [cin_pad*ks*ks][cout_pad] (stx_conv_weight_prep) */
+  const float* bias;  /* [cout] or NULL */
+  float* y;           /* output [n][cout][ho][wo] */
+  const float* mask;  /* NULL or [n][cout][ho][wo]: value *= (mask > 0)   (ReLU backward) */
+  const float* aux;   /* NULL or [n][cout][ho][wo]: value += aux_scale*aux */
+  float aux_scale;
+  const float* acc_scale; /* NULL or device scalar: value = acc * (*acc_scale) first */
+  int accumulate;     /* value += old y */
+  int relu_out;       /* y = max(value, 0) */
+  int n, cin, h, w;   /* physical input dims */
+  int cout, ks, stride, pad;
+  int in_mode;        /* STX_IN_* */
+  int hv, wv;         /* virtual input dims (after the in_mode transform) */
+  int ho, wo;         /* output dims */
+  int cin_pad, cout_pad;
+  long long wt_batch_stride; /* floats between per-image weight matrices (0 = shared) */
+} stx_conv_params;
+
+int stx_version(void);
+const char* stx_last_error_string(void);
+
+/* Padded GEMM dims the conv kernels expect for a (cin, cout, ks) conv. */
+int stx_conv_weight_dims(int cin, int cout, int ks, int* cin_pad, int* cout_pad);
+
+/* w [cout][cin][ks][ks] -> wt [cin_pad*ks*ks][cout_pad] (zero padded).
+ * transpose=1 builds the data-gradient weights of the same layer instead:
+ * wt'[co*ks*ks + kh*ks + kw][ci] = w[co][ci][ks-1-kh][ks-1-kw] with dims
+ * (cin'=cout, cout'=cin) padded by stx_conv_weight_dims(cout, cin, ks). */
+int stx_conv_weight_prep(const float* w, float* wt, int cout, int cin, int ks, int transpose,
+                         void* stream);
+
+/* Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32), fused input
+ * transform (in_mode) and epilogue (bias, mask, aux, accumulate, relu). */
+int stx_conv2d(const stx_conv_params* p, void* stream);
+
+/* Weight gradient: dw[cout][cin][ks][ks] (+)= sum_{n,oy,ox} dy * xv  (xv = in_mode(x)).
+ * Split-K partial slabs in ws (fp32), reduced in fixed order (deterministic).
+ * Supported: ks=3 stride 1/2, ks=9 stride 1.  Workspace: stx_conv2d_wgrad_ws(). */
+size_t stx_conv2d_wgrad_ws(int n, int cin, int cout, int ks, int stride, int ho, int wo);
+int stx_conv2d_wgrad(const float* x, const float* dy, float* dw, int accumulate,
+                     int n, int cin, int h, int w, int cout, int ks, int stride, int pad,
+                     int in_mode, int hv, int wv, int ho, int wo,
+                     void* ws, size_t ws_bytes, void* stream);
+/* db[c] (+)= sum_{n,p} dy[n][c][p]  (conv bias gradient) */
+size_t stx_bias_grad_ws(int n, int c);
+int stx_bias_grad(const float* dy, float* db, int n, int c, int hw, int accumulate,
+                  void* ws, size_t ws_bytes, void* stream);
+
+/* Gram: G[b] = F_b F_b^T * scale, F_b = z[b] viewed [c][hw].  Split-K MFMA +
+ * deterministic reduction. */
+size_t stx_gram_ws(int b, int c, int hw);
+int stx_gram(const float* z, float* g, int b, int c, int hw, float scale,
+             void* ws, size_t ws_bytes, void* stream);
+
+/* Style loss forward + backward coefficients (StyleLoss.forward):
+ *   G = gram(z)/(c*hw);  loss = mean((G - T)^2) over b*c*c  -> *loss (device scalar)
+ *   A[b] = weight*4/(b*c*c*c*hw) * (G[b]-T) + diag_alpha*I     (A is [b][cpad][cpad])
+ * so that dz = A·z (+ aux) is d(weight*loss)/dz; g_out (optional) receives G.
+ * cpad = stx_gram_coef_pitch(c).  ws: stx_gram_ws(b, c, hw). */
+int stx_gram_coef_pitch(int c);
+int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
+                   float* loss, int b, int c, int hw, float weight, float diag_alpha,
+                   void* ws, size_t ws_bytes, void* stream);
+/* dz (+)= s * A[b]·z[b] (+ aux_scale*aux) — Gram backward as a 1x1 MFMA conv with
+ * per-image weights; z viewed [b][c][h][w]; s = *acc_scale_dev (or 1 if NULL) */
+int stx_gram_bwd(const float* coef, const float* z, float* dz, int b, int c, int h, int w,
+                 const float* acc_scale_dev, const float* mask, const float* aux,
+                 float aux_scale, int accumulate, void* stream);
+
+/* Sum-of-squared-difference reductions (ContentLoss / FeatureReconstructionLoss):
+ *   s = sum((f(a) - f(b))^2), f = relu if relu_inputs else identity
+ *   mode 0: *out = s / n                        (F.mse_loss, mean)
+ *   mode 1: out[0] = (s / n)^2 / n, out[1] = s / n   (FeatureReconstructionLoss)
+ * grad (optional, mode 0): grad = gscale * 2*(a-b)/n. */
+size_t stx_mse_ws(long long n);
+int stx_mse(const float* a, const float* b, long long n, int relu_inputs, int mode,
+            float* out, float* grad, float gscale, void* ws, size_t ws_bytes, void* stream);
+/* grad (+)= s0 * (*s1) * (*s2) * (f(a) - f(b)) [* (a>0) if relu]; s1/s2 device scalars or NULL */
+int stx_diff_scale(const float* a, const float* b, float* grad, long long n, float s0,
+                   const float* s1_dev, const float* s2_dev, int relu, int accumulate,
+                   void* stream);
+/* *out = sum_i w_host[i] * s[i]   (k <= 16 device scalars, fixed order) */
+int stx_loss_combine(const float* s, int k, const float* w_host, float* out, void* stream);
+
+/* MaxPool2d(2,2) on (optionally relu'd) input; idx = flat y*w+x argmax per plane,
+ * torch CPU semantics (first max in row-major window order; NaN propagates). idx may be NULL. */
+int stx_maxpool2x2_fwd(const float* x, float* y, long long* idx, int nc, int h, int w,
+                       int relu_input, void* stream);
+/* dx = scatter(dy at idx)  (dx fully written, gather form) */
+int stx_maxpool2x2_bwd(const float* dy, const long long* idx, float* dx, int nc, int h, int w,
+                       void* stream);
+/* dz = unpool(dp) * (z > 0): backward of ReLU + MaxPool2d(2,2) with the argmax
+ * recomputed from z (dz fully written; z is the pre-ReLU tensor [nc][h][w]) */
+int stx_relupool_bwd(const float* dp, const float* z, float* dz, int nc, int h, int w,
+                     void* stream);
+int stx_relu_fwd(const float* x, float* y, long long n, void* stream);
+/* dx = dy * (y > 0) */
+int stx_relu_bwd(const float* dy, const float* y, float* dx, long long n, void* stream);
+
+/* Adam (torch.optim.Adam semantics, in place; 16-byte aligned buffers).
+ * step_dev: device int32 step counter, incremented on the device by every call so
+ * a captured graph replays correctly.  ws: stx_adam_ws() bytes of device scratch. */
+size_t stx_adam_ws(void);
+int stx_adam_step(float* p, const float* g, float* m, float* v, long long n, float lr,
+                  float beta1, float beta2, float eps, int* step_dev, void* ws, void* stream);
+
+/* InstanceNorm2d(affine) forward, per (n,c) plane over hw (biased var, eps):
+ *   u = x (+ res);  y = (u-mean)*rstd*gamma + beta;  y = max(y,0) if relu.
+ * mean/rstd [n*c] saved for the backward (may be NULL). */
+int stx_instnorm_fwd(const float* x, const float* res, const float* gamma, const float* beta,
+                     float* y, float* mean, float* rstd, int n, int c, int hw, float eps,
+                     int relu, void* stream);
+/* backward: dy = grad wrt y; y needed when relu (mask).  du = grad wrt u (= grad of x
+ * and of res).  dgamma/dbeta (may be NULL) (+)= sums over n (fixed order). */
+size_t stx_instnorm_bwd_ws(int n, int c);
+int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
+                     const float* gamma, const float* mean, const float* rstd, float* du,
+                     float* dgamma, float* dbeta, int n, int c, int hw, int relu,
+                     int accumulate_params, void* ws, size_t ws_bytes, void* stream);
+
+/* nearest x2 upsample: y [nc][2h][2w];  backward dx[y][x] = sum of dy's 2x2 block */
+int stx_upsample2x_fwd(const float* x, float* y, int nc, int h, int w, void* stream);
+int stx_upsample2x_bwd(const float* dy, float* dx, int nc, int h, int w, void* stream);
+
+/* Total variation, batch SUM (stransfer/network.py:621-641):
+ *   *loss = factor*(sum|y[..,x]-y[..,x+1]| + sum|y[..,y,:]-y[..,y+1,:]|)
+ *   grad (optional) = gscale * (*gscale_dev or 1) * d loss / dy */
+size_t stx_tv_ws(int n, int c, int h, int w);
+int stx_tv_loss(const float* y, float* loss, float* grad, float gscale, const float* gscale_dev,
+                int n, int c, int h, int w, float factor, void* ws, size_t ws_bytes,
+                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STX_H_ */

@@ -1,0 +1,276 @@
+"""ORACLE — test infrastructure only.  Never imported by the product path.
+
+CPU (torch fp32) restatement of the reference's hot path, tupini07/StyleTransfer
+`stransfer/network.py`.  Only `tests/`, `__graft_entry__.smoke()` and
+`bench.py`'s `cpu_baseline` leg may import this module, and only as the checker
+or as the CPU baseline — it is never the thing measured or shipped.
+
+It reproduces the reference's *execution schedule* (per-loss VGG prefix re-runs,
+content re-targeting on every forward, VGG parameters left with
+`requires_grad=True` so their weight-gradients are computed) so that timing it
+on the host cores is a faithful CPU baseline.
+
+Pinning: `oracle/gen_golden.py` imports the real reference from
+`/root/reference` (offline stubs for torchvision/tensorboardX/imageio, which are
+absent from the image; the stubs only supply the VGG-19 architecture with the
+synthetic weights and image transforms) and asserts this restatement matches it
+to fp32 rounding; the reference outputs are committed as `tests/golden/*.npz`.
+
+Version notes: `padding_mode='reflection'` fell through to
+zero padding at the pinned torch==1.1.0, so ITN convs use zero padding here.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(_HERE))
+from styletransfer_amd import weights as W  # noqa: E402  (data generation only)
+
+
+# --------------------------------------------------------------------------- losses
+def gram_matrix(x: torch.Tensor) -> torch.Tensor:
+    """`StyleLoss.gram_matrix` — stransfer/network.py:92-108 (divides by C·H·W, not B)."""
+    bs, d, h, w = x.size()
+    f = x.view(bs, d, h * w)
+    return torch.bmm(f, f.transpose(1, 2)).div(d * h * w)
+
+
+class StyleLoss(nn.Module):
+    """stransfer/network.py:79-131."""
+
+    def __init__(self, target):
+        super().__init__()
+        self.set_target(target)
+
+    def forward(self, x):
+        g = gram_matrix(x)
+        self.loss = F.mse_loss(g, self.target.expand_as(g))  # :117-121
+        return x
+
+    def set_target(self, target):
+        self.target = gram_matrix(target).detach()  # :125-131
+
+
+class ContentLoss(nn.Module):
+    """stransfer/network.py:134-164."""
+
+    def __init__(self, target):
+        super().__init__()
+        self.set_target(target)
+
+    def set_target(self, target):
+        self.target = target.detach()
+
+    def forward(self, x):
+        self.loss = F.mse_loss(x, self.target)
+        return x
+
+
+class FeatureReconstructionLoss(nn.Module):
+    """stransfer/network.py:167-201: mse² / (B·C·H·W)."""
+
+    def __init__(self, target):
+        super().__init__()
+        self.set_target(target)
+
+    def set_target(self, target):
+        self.target = target.detach()
+
+    def forward(self, x):
+        l2 = F.mse_loss(x, self.target)
+        bs, d, h, w = x.size()
+        self.loss = l2.pow(2).div(bs * d * h * w)
+        return x
+
+
+# ----------------------------------------------------------------------- VGG pieces
+def vgg19_features(seed: int = 1234) -> nn.Sequential:
+    """torchvision vgg19 `.features` (cfg E) with hash-PRNG weights."""
+    layers, cin, it = [], 3, iter(W.vgg19_synthetic(seed))
+    for v in W.VGG19_CFG:
+        if v == "M":
+            layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+        else:
+            conv = nn.Conv2d(cin, v, kernel_size=3, padding=1)
+            w, b = next(it)
+            with torch.no_grad():
+                conv.weight.copy_(torch.from_numpy(w))
+                conv.bias.copy_(torch.from_numpy(b))
+            layers += [conv, nn.ReLU(inplace=True)]
+            cin = v
+    return nn.Sequential(*layers)
+
+
+class StyleNetwork(nn.Module):
+    """Restatement of `StyleNetwork` (stransfer/network.py:204-458), same schedule."""
+
+    content_layers = ["Conv2d_4"]
+    style_layers = ["Conv2d_1", "Conv2d_2", "Conv2d_3", "Conv2d_4", "Conv2d_5"]
+    feature_loss_layers = ["ReLU_4"]
+
+    def __init__(self, style_image, content_image=None, vgg_seed: int = 1234, vgg=None):
+        super().__init__()
+        self.content_losses, self.style_losses, self.feature_losses = [], [], []
+        if content_image is None:
+            content_image = torch.zeros([1, 3, 256, 256])  # :241-243
+        vgg = (vgg if vgg is not None else vgg19_features(vgg_seed)).eval()
+        self.net_pieces = [nn.Sequential()]
+        loss_added, cur, i = False, 0, 0
+        for layer in vgg:  # :264-314
+            if isinstance(layer, nn.Conv2d):
+                i += 1
+            if isinstance(layer, nn.ReLU):
+                layer.inplace = False
+            name = type(layer).__name__ + f"_{i}"
+            self.net_pieces[cur].add_module(name, layer)
+            if name in self.content_layers:
+                self.content_losses.append([ContentLoss(self.run_through_pieces(content_image)), cur])
+                loss_added = True
+            if name in self.style_layers:
+                self.style_losses.append([StyleLoss(self.run_through_pieces(style_image)), cur])
+                loss_added = True
+            if name in self.feature_loss_layers:
+                self.feature_losses.append(
+                    [FeatureReconstructionLoss(self.run_through_pieces(content_image)), cur])
+                loss_added = True
+            if loss_added:
+                self.net_pieces.append(nn.Sequential())
+                cur += 1
+                loss_added = False
+        # keep the pieces as registered submodules so .to()/parameters() see them
+        self._pieces = nn.ModuleList(self.net_pieces)
+
+    def run_through_pieces(self, x, until=-1):  # :316-340
+        pieces = self.net_pieces if until == -1 else self.net_pieces[:until + 1]
+        for p in pieces:
+            x = p(x)
+        return x
+
+    def get_total_current_content_loss(self, weight=1):  # :342-348
+        return weight * torch.stack([x[0].loss for x in self.content_losses]).sum()
+
+    def get_total_current_feature_loss(self, weight=1):  # :350-356
+        return weight * torch.stack([x[0].loss for x in self.feature_losses]).sum()
+
+    def get_total_current_style_loss(self, weight=1):  # :358-364
+        return weight * torch.stack([x[0].loss for x in self.style_losses]).sum()
+
+    def forward(self, input_image, content_image=None, style_image=None):  # :366-401
+        for (loss, idx) in self.content_losses + self.feature_losses:
+            if content_image is not None:
+                loss.set_target(self.run_through_pieces(content_image, idx))
+            loss(self.run_through_pieces(input_image, idx))
+        for (loss, idx) in self.style_losses:
+            if style_image is not None:
+                # reference bug kept: re-targets style from content_image (:391-394)
+                loss.set_target(self.run_through_pieces(content_image, idx))
+            loss(self.run_through_pieces(input_image, idx))
+
+    def get_content_optimizer(self, input_img, optt=torch.optim.Adam):  # :403-409
+        return optt([input_img.requires_grad_()])
+
+
+# ------------------------------------------------------------ ImageTransformNet
+class ResidualBlock(nn.Module):
+    """stransfer/network.py:461-506 (zero padding: torch 1.1.0 semantics)."""
+
+    def __init__(self, c=128, k=3):
+        super().__init__()
+        self.conv1 = nn.Conv2d(c, c, k, 1, k // 2)
+        self.insn1 = nn.InstanceNorm2d(c, affine=True)
+        self.relu = nn.ReLU()
+        self.conv2 = nn.Conv2d(c, c, k, 1, k // 2)
+        self.insn2 = nn.InstanceNorm2d(c, affine=True)
+
+    def forward(self, x):
+        out = self.relu(self.insn1(self.conv1(x)))
+        out = self.conv2(out)
+        out = out + x  # :502 (in-place add in the reference; same value)
+        return self.insn2(out)
+
+
+def image_transform_net(seed: int = 4321, in_channels: int = 3) -> nn.Sequential:
+    """stransfer/network.py:520-611 with hash-PRNG parameters."""
+    net = nn.Sequential(
+        nn.Conv2d(in_channels, 32, 9, 1, 4), nn.InstanceNorm2d(32, affine=True), nn.ReLU(),
+        nn.Conv2d(32, 64, 3, 2, 1), nn.InstanceNorm2d(64, affine=True), nn.ReLU(),
+        nn.Conv2d(64, 128, 3, 2, 1), nn.InstanceNorm2d(128, affine=True), nn.ReLU(),
+        ResidualBlock(), ResidualBlock(), ResidualBlock(), ResidualBlock(), ResidualBlock(),
+        nn.Upsample(mode="nearest", scale_factor=2),
+        nn.Conv2d(128, 64, 3, 1, 1), nn.InstanceNorm2d(64, affine=True), nn.ReLU(),
+        nn.Upsample(mode="nearest", scale_factor=2),
+        nn.Conv2d(64, 32, 3, 1, 1), nn.InstanceNorm2d(32, affine=True), nn.ReLU(),
+        nn.Conv2d(32, 3, 9, 1, 4),
+    )
+    sd = {k: torch.from_numpy(v) for k, v in W.itn_synthetic(seed, in_channels)}
+    net.load_state_dict(sd)
+    return net
+
+
+def total_variation(y, factor=1e-6):
+    """`get_total_variation_regularization_loss` — stransfer/network.py:621-641 (batch SUM)."""
+    return factor * (torch.sum(torch.abs(y[:, :, :, :-1] - y[:, :, :, 1:]))
+                     + torch.sum(torch.abs(y[:, :, :-1, :] - y[:, :, 1:, :])))
+
+
+# ------------------------------------------------------------------- workloads
+def gatys_adam_iter(net: StyleNetwork, x, content, opt, style_weight=100_000, content_weight=1):
+    """One Gatys iteration as BASELINE.json defines it:
+    zero_grad → forward(x, content) → style·w + content·w → backward → Adam step."""
+    opt.zero_grad()
+    net(x, content)
+    total = (net.get_total_current_style_loss(style_weight)
+             + net.get_total_current_content_loss(content_weight))
+    total.backward()
+    opt.step()
+    return total
+
+
+def fast_st_closure(itn, loss_net, batch, style_weight=100_000, content_weight=1):
+    """`static_train` closure body — stransfer/network.py:690-731 (logging syncs dropped)."""
+    y = itn(batch)
+    loss_net(y, content_image=batch)
+    total = (loss_net.get_total_current_style_loss(style_weight)
+             + loss_net.get_total_current_content_loss(content_weight)
+             + total_variation(y))
+    total.backward()
+    return total, y
+
+
+def adam_reference_step(p, g, m, v, step, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
+    """Single-tensor Adam exactly as torch.optim.Adam (the in-container oracle,
+    torch 2.10; `stransfer/network.py:403-409`, `:643-649` use its defaults)."""
+    m.lerp_(g, 1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1 = 1 - b1 ** step
+    bc2 = 1 - b2 ** step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
+    return p
+
+
+def maxpool2x2_with_indices(x):
+    """MaxPool2d(2,2) with flat h·W+w argmax, ties → first in window (row-major)."""
+    return F.max_pool2d(x, 2, 2, return_indices=True)
+
+
+def to_np(t):
+    return t.detach().cpu().numpy()
+
+
+if __name__ == "__main__":  # tiny self-check
+    torch.manual_seed(0)
+    s = torch.from_numpy(W.synthetic_image(1, (1, 3, 64, 64)))
+    c = torch.from_numpy(W.synthetic_image(2, (1, 3, 64, 64)))
+    net = StyleNetwork(s, c)
+    x = c.clone()
+    opt = net.get_content_optimizer(x)
+    print(float(gatys_adam_iter(net, x, c, opt)))

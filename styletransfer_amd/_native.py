@@ -1,0 +1,111 @@
+"""ctypes binding of libstx.so (the C-ABI declared in include/stx.h).
+
+The product path has no fallback: if the library is missing or fails to load,
+`lib()` raises, and every op that needs it fails loudly.  `lib()` is lazy so
+that host-only code (argument checking, state_dict handling) imports on a
+machine without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("STX_LIB", os.path.join(_HERE, "libstx.so"))
+
+STX_IN_RAW, STX_IN_RELU, STX_IN_RELU_POOL2, STX_IN_UPSAMPLE2, STX_IN_DILATE2 = range(5)
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_longlong
+f32 = C.c_float
+sz = C.c_size_t
+
+
+class ConvParams(C.Structure):
+    """Mirror of `stx_conv_params` (include/stx.h)."""
+    _fields_ = [
+        ("x", vp), ("wt", vp), ("bias", vp), ("y", vp), ("mask", vp), ("aux", vp),
+        ("aux_scale", f32), ("acc_scale", vp), ("accumulate", i32), ("relu_out", i32),
+        ("n", i32), ("cin", i32), ("h", i32), ("w", i32),
+        ("cout", i32), ("ks", i32), ("stride", i32), ("pad", i32),
+        ("in_mode", i32), ("hv", i32), ("wv", i32), ("ho", i32), ("wo", i32),
+        ("cin_pad", i32), ("cout_pad", i32), ("wt_batch_stride", i64),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/stx.h declares
+SIGNATURES = {
+    "stx_version": (i32, []),
+    "stx_last_error_string": (C.c_char_p, []),
+    "stx_conv_weight_dims": (i32, [i32, i32, i32, C.POINTER(i32), C.POINTER(i32)]),
+    "stx_conv_weight_prep": (i32, [vp, vp, i32, i32, i32, i32, vp]),
+    "stx_conv2d": (i32, [C.POINTER(ConvParams), vp]),
+    "stx_conv2d_wgrad_ws": (sz, [i32, i32, i32, i32, i32, i32, i32]),
+    "stx_conv2d_wgrad": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
+                               i32, i32, i32, i32, vp, sz, vp]),
+    "stx_bias_grad_ws": (sz, [i32, i32]),
+    "stx_bias_grad": (i32, [vp, vp, i32, i32, i32, i32, vp, sz, vp]),
+    "stx_gram_ws": (sz, [i32, i32, i32]),
+    "stx_gram": (i32, [vp, vp, i32, i32, i32, f32, vp, sz, vp]),
+    "stx_gram_coef_pitch": (i32, [i32]),
+    "stx_style_loss": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, vp, sz, vp]),
+    "stx_gram_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, f32, i32, vp]),
+    "stx_mse_ws": (sz, [i64]),
+    "stx_mse": (i32, [vp, vp, i64, i32, i32, vp, vp, f32, vp, sz, vp]),
+    "stx_diff_scale": (i32, [vp, vp, vp, i64, f32, vp, vp, i32, i32, vp]),
+    "stx_loss_combine": (i32, [vp, i32, C.POINTER(f32), vp, vp]),
+    "stx_maxpool2x2_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
+    "stx_maxpool2x2_bwd": (i32, [vp, vp, vp, i32, i32, i32, vp]),
+    "stx_relupool_bwd": (i32, [vp, vp, vp, i32, i32, i32, vp]),
+    "stx_relu_fwd": (i32, [vp, vp, i64, vp]),
+    "stx_relu_bwd": (i32, [vp, vp, vp, i64, vp]),
+    "stx_adam_ws": (sz, []),
+    "stx_adam_step": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp, vp]),
+    "stx_instnorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp]),
+    "stx_instnorm_bwd_ws": (sz, [i32, i32]),
+    "stx_instnorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32,
+                               i32, vp, sz, vp]),
+    "stx_upsample2x_fwd": (i32, [vp, vp, i32, i32, i32, vp]),
+    "stx_upsample2x_bwd": (i32, [vp, vp, i32, i32, i32, vp]),
+    "stx_tv_ws": (sz, [i32, i32, i32, i32]),
+    "stx_tv_loss": (i32, [vp, vp, vp, f32, vp, i32, i32, i32, i32, f32, vp, sz, vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libstx.so (raises NativeError if absent — there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeError(
+                    f"libstx.so not found at {LIB_PATH}; build it with "
+                    f"`python -c 'import __graft_entry__ as g; g.build()'` "
+                    f"(make -C styletransfer_amd/csrc)")
+            try:
+                L = C.CDLL(LIB_PATH)
+            except OSError as e:  # pragma: no cover
+                raise NativeError(f"failed to load {LIB_PATH}: {e}") from e
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().stx_last_error_string().decode(errors="replace")
+        raise NativeError(f"{what or 'libstx'} failed (code {rc}): {msg}")

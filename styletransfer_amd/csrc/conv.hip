@@ -1,0 +1,327 @@
+// Implicit-GEMM convolution for gfx950 on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+//   out[n][co][oy][ox] = sum_{ci,kh,kw} W[co][ci][kh][kw] * V[n][ci][oy*S-P+kh][ox*S-P+kw]
+//
+// GEMM view: M = cout, N = output pixels of one image, K = cin*KS*KS.
+// A block owns BM output channels x a TH x TW output-pixel tile of one image and
+// walks K in chunks of CIS input channels.  Per chunk it stages
+//   * the input HALO  [CIS][RH][RW]  (the virtual input V, formed on the fly from
+//     x by the loader: relu / relu+maxpool / nearest-upsample / zero-dilation),
+//     so each input element is read from L2 once per chunk and re-used KS*KS times
+//     out of LDS ("LDS-staged 3x3 conv tiles");
+//   * the weight slab [CIS*KS*KS][BM] (prepped k-major layout, coalesced rows).
+// MFMA operand mapping (32x32x2, lane l, half h = l>>5): lane supplies
+// A[i = l&31][k_h] and B[k_h][j = l&31].  The two k slots of each MFMA are
+// assigned to the two lane halves as two different input channels
+// (k = s + h*KC/2), so every LDS address is (lane base) + compile-time offset.
+//
+// Reference: torchvision vgg19 Conv2d(3x3,p1) used by StyleNetwork
+// (stransfer/network.py:246-314) and the ImageTransformNet convs
+// (stransfer/network.py:468-481, 525-609; zero padding = torch 1.1.0 semantics
+// of padding_mode='reflection').
+#include "common.h"
+#include "../../include/stx.h"
+
+namespace stx {
+
+__device__ __forceinline__ float load_virtual(const float* __restrict__ xp, int mode, int cin,
+                                              int h, int w, int hv, int wv, int ci, int vy,
+                                              int vx) {
+  if (ci >= cin || vy < 0 || vx < 0 || vy >= hv || vx >= wv) return 0.f;
+  const float* plane = xp + (size_t)ci * h * w;
+  switch (mode) {
+    case STX_IN_RAW:
+      return plane[vy * w + vx];
+    case STX_IN_RELU:
+      return fmaxf(plane[vy * w + vx], 0.f);
+    case STX_IN_RELU_POOL2: {
+      const float* q = plane + (2 * vy) * w + 2 * vx;
+      // relu then max: every relu'd value is >= 0, start from 0
+      float m = fmaxf(fmaxf(q[0], q[1]), fmaxf(q[w], q[w + 1]));
+      return fmaxf(m, 0.f);
+    }
+    case STX_IN_UPSAMPLE2:
+      return plane[(vy >> 1) * w + (vx >> 1)];
+    default: {  // STX_IN_DILATE2
+      if ((vy | vx) & 1) return 0.f;
+      const int sy = vy >> 1, sx = vx >> 1;
+      if (sy >= h || sx >= w) return 0.f;
+      return plane[sy * w + sx];
+    }
+  }
+}
+
+template <int KS, int S, int CIS, int BM, int TW>
+struct ConvCfg {
+  static constexpr int WM = BM / 64;          // waves along M (each 64 rows = 2 MFMA tiles)
+  static constexpr int WN = 4 / WM;           // waves along N
+  static constexpr int MI = 2, NI = 2;        // MFMA tiles per wave
+  static constexpr int NPIX = WN * NI * 32;   // output pixels per block
+  static constexpr int TH = NPIX / TW;
+  static constexpr int RH = (TH - 1) * S + KS;
+  static constexpr int RW = (TW - 1) * S + KS;
+  static constexpr int RWP = RW;
+  static constexpr int CH = RH * RWP;
+  static constexpr int KK = KS * KS;
+  static constexpr int KC = CIS * KK;          // K per chunk
+  static constexpr int HALO = CIS * RH * RW;
+  static constexpr int NH = (HALO + 255) / 256;
+  static constexpr int WQ = KC * BM / 4;       // float4 per weight slab
+  static constexpr int NW = (WQ + 255) / 256;
+  static constexpr int LDS_IN = CIS * CH;
+  static constexpr int LDS_FLOATS = LDS_IN + KC * BM;
+  static_assert(CIS % 2 == 0, "CIS must be even (two lane halves)");
+  static_assert(NPIX % TW == 0, "tile");
+};
+
+template <int KS, int S, int CIS, int BM, int TW>
+__global__ void __launch_bounds__(256)
+conv_fwd_kernel(stx_conv_params p, int tiles_x) {
+  using C = ConvCfg<KS, S, CIS, BM, TW>;
+  __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
+  float* lds_in = smem;
+  float* lds_w = smem + C::LDS_IN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int wm = wave / C::WN, wn = wave % C::WN;
+
+  const int tile = blockIdx.x;
+  const int ty0 = (tile / tiles_x) * C::TH, tx0 = (tile % tiles_x) * TW;
+  const int co0 = blockIdx.y * BM;
+  const int n = blockIdx.z;
+
+  const float* __restrict__ xn = p.x + (size_t)n * p.cin * p.h * p.w;
+  const float* __restrict__ wt = p.wt + (size_t)n * p.wt_batch_stride;
+  const int vy0 = ty0 * S - p.pad, vx0 = tx0 * S - p.pad;
+  const int mode = p.in_mode;
+
+  f32x16 acc[C::MI][C::NI];
+#pragma unroll
+  for (int i = 0; i < C::MI; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // per-lane LDS bases
+  int b_base[C::NI];
+#pragma unroll
+  for (int j = 0; j < C::NI; ++j) {
+    const int pix = (wn * C::NI + j) * 32 + l32;
+    const int ty = pix / TW, tx = pix % TW;
+    b_base[j] = h * (CIS / 2) * C::CH + ty * S * C::RWP + tx * S;
+  }
+  const int a_base = h * (CIS / 2) * C::KK * BM + wm * 64 + l32;
+
+  float hreg[C::NH];
+  f32x4 wreg[C::NW];
+  const int nchunks = p.cin_pad / CIS;
+
+  auto fetch = [&](int chunk) {
+    const int c0 = chunk * CIS;
+#pragma unroll
+    for (int i = 0; i < C::NH; ++i) {
+      const int idx = tid + i * 256;
+      float v = 0.f;
+      if (idx < C::HALO) {
+        const int ci = idx / (C::RH * C::RW);
+        const int rem = idx - ci * (C::RH * C::RW);
+        const int r = rem / C::RW, c = rem - r * C::RW;
+        v = load_virtual(xn, mode, p.cin, p.h, p.w, p.hv, p.wv, c0 + ci, vy0 + r, vx0 + c);
+      }
+      hreg[i] = v;
+    }
+    const float* wsrc = wt + (size_t)c0 * C::KK * p.cout_pad + co0;
+#pragma unroll
+    for (int i = 0; i < C::NW; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < C::WQ) {
+        const int kr = idx / (BM / 4), c4 = idx - kr * (BM / 4);
+        wreg[i] = *reinterpret_cast<const f32x4*>(wsrc + (size_t)kr * p.cout_pad + c4 * 4);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < C::NH; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < C::HALO) {
+        const int ci = idx / (C::RH * C::RW);
+        const int rem = idx - ci * (C::RH * C::RW);
+        const int r = rem / C::RW, c = rem - r * C::RW;
+        lds_in[ci * C::CH + r * C::RWP + c] = hreg[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < C::NW; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < C::WQ) *reinterpret_cast<f32x4*>(lds_w + idx * 4) = wreg[i];
+    }
+  };
+
+  fetch(0);
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    __syncthreads();  // previous chunk's reads done
+    store();
+    __syncthreads();
+    if (chunk + 1 < nchunks) fetch(chunk + 1);  // overlaps the MFMA loop below
+#pragma unroll
+    for (int s = 0; s < (CIS / 2) * C::KK; ++s) {
+      const int cil = s / C::KK, r = s % C::KK, kh = r / KS, kw = r % KS;
+      float a[C::MI], b[C::NI];
+#pragma unroll
+      for (int i = 0; i < C::MI; ++i) a[i] = lds_w[a_base + s * BM + i * 32];
+#pragma unroll
+      for (int j = 0; j < C::NI; ++j) b[j] = lds_in[b_base[j] + cil * C::CH + kh * C::RWP + kw];
+#pragma unroll
+      for (int i = 0; i < C::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < C::NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // epilogue
+  const size_t plane = (size_t)p.ho * p.wo;
+#pragma unroll
+  for (int j = 0; j < C::NI; ++j) {
+    const int pix = (wn * C::NI + j) * 32 + l32;
+    const int oy = ty0 + pix / TW, ox = tx0 + pix % TW;
+    if (oy >= p.ho || ox >= p.wo) continue;
+    const size_t pofs = (size_t)oy * p.wo + ox;
+#pragma unroll
+    for (int i = 0; i < C::MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co >= p.cout) continue;
+        const size_t o = ((size_t)n * p.cout + co) * plane + pofs;
+        float v = acc[i][j][r];
+        if (p.acc_scale) v *= *p.acc_scale;
+        if (p.bias) v += p.bias[co];
+        if (p.mask) v = p.mask[o] > 0.f ? v : 0.f;
+        if (p.aux) v += p.aux_scale * p.aux[o];
+        if (p.accumulate) v += p.y[o];
+        if (p.relu_out) v = fmaxf(v, 0.f);
+        p.y[o] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- weight prep
+__global__ void weight_prep_kernel(const float* __restrict__ w, float* __restrict__ wt, int cout,
+                                   int cin, int ks, int transpose, int rows_pad, int cols_pad) {
+  const long long total = (long long)rows_pad * cols_pad;
+  const int kk = ks * ks;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int col = (int)(i % cols_pad);
+    const int row = (int)(i / cols_pad);
+    const int c_in = row / kk, r = row % kk, kh = r / ks, kw = r % ks;
+    float v = 0.f;
+    if (!transpose) {
+      // row = ci*kk + kh*ks + kw, col = co
+      if (c_in < cin && col < cout) v = w[(((size_t)col * cin + c_in) * ks + kh) * ks + kw];
+    } else {
+      // dgrad weights: row = co*kk + kh*ks + kw, col = ci; flipped taps
+      if (c_in < cout && col < cin)
+        v = w[(((size_t)c_in * cin + col) * ks + (ks - 1 - kh)) * ks + (ks - 1 - kw)];
+    }
+    wt[i] = v;
+  }
+}
+
+static int cis_for(int ks) { return ks == 9 ? 2 : (ks == 1 ? 16 : 8); }
+
+template <int KS, int S, int CIS, int BM, int TW>
+static int launch_fwd(const stx_conv_params& p, hipStream_t st) {
+  using C = ConvCfg<KS, S, CIS, BM, TW>;
+  const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
+  dim3 grid(tiles_x * tiles_y, cdiv(p.cout, BM), p.n);
+  hipLaunchKernelGGL((conv_fwd_kernel<KS, S, CIS, BM, TW>), grid, dim3(256), 0, st, p, tiles_x);
+  return check_launch("stx_conv2d");
+}
+
+template <int KS, int S, int BM>
+static int dispatch_tw(const stx_conv_params& p, hipStream_t st) {
+  constexpr int CIS = KS == 9 ? 2 : (KS == 1 ? 16 : 8);
+  if (p.wo > 32) return launch_fwd<KS, S, CIS, BM, 64>(p, st);
+  if (p.wo > 16) return launch_fwd<KS, S, CIS, BM, 32>(p, st);
+  return launch_fwd<KS, S, CIS, BM, 16>(p, st);
+}
+
+}  // namespace stx
+
+using namespace stx;
+
+extern "C" int stx_conv_weight_dims(int cin, int cout, int ks, int* cin_pad, int* cout_pad) {
+  if (ks != 1 && ks != 3 && ks != 9) {
+    set_error("stx_conv_weight_dims: unsupported kernel size %d", ks);
+    return STX_E_INVALID;
+  }
+  if (cin_pad) *cin_pad = rup(cin, cis_for(ks));
+  if (cout_pad) *cout_pad = rup(cout, 128);
+  return STX_OK;
+}
+
+extern "C" int stx_conv_weight_prep(const float* w, float* wt, int cout, int cin, int ks,
+                                    int transpose, void* stream) {
+  int rp, cp;
+  // GEMM dims of the conv this slab feeds
+  const int gin = transpose ? cout : cin, gout = transpose ? cin : cout;
+  int rc = stx_conv_weight_dims(gin, gout, ks, &rp, &cp);
+  if (rc) return rc;
+  const long long total = (long long)rp * ks * ks * cp;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(weight_prep_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, wt,
+                     cout, cin, ks, transpose, rp * ks * ks, cp);
+  return check_launch("stx_conv_weight_prep");
+}
+
+extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
+  if (!pp) {
+    set_error("stx_conv2d: null params");
+    return STX_E_INVALID;
+  }
+  const stx_conv_params& p = *pp;
+  hipStream_t st = (hipStream_t)stream;
+  int cinp, coutp;
+  if (stx_conv_weight_dims(p.cin, p.cout, p.ks, &cinp, &coutp)) return STX_E_INVALID;
+  if (p.cin_pad != cinp || p.cout_pad != coutp || p.n <= 0 || p.ho <= 0 || p.wo <= 0 ||
+      p.pad < 0 || p.in_mode < 0 || p.in_mode > 4 || !p.x || !p.wt || !p.y) {
+    set_error("stx_conv2d: invalid params (cin_pad %d/%d cout_pad %d/%d n %d ho %d wo %d)",
+              p.cin_pad, cinp, p.cout_pad, coutp, p.n, p.ho, p.wo);
+    return STX_E_INVALID;
+  }
+  // geometry consistency: ho = (hv + 2p - ks)/s + 1
+  if ((p.hv + 2 * p.pad - p.ks) / p.stride + 1 != p.ho ||
+      (p.wv + 2 * p.pad - p.ks) / p.stride + 1 != p.wo) {
+    set_error("stx_conv2d: inconsistent output dims");
+    return STX_E_INVALID;
+  }
+  if (p.in_mode == STX_IN_RELU_POOL2 && (p.hv * 2 > p.h || p.wv * 2 > p.w)) {
+    set_error("stx_conv2d: pool dims");
+    return STX_E_INVALID;
+  }
+  if (p.in_mode == STX_IN_UPSAMPLE2 && (p.hv > 2 * p.h || p.wv > 2 * p.w)) {
+    set_error("stx_conv2d: upsample dims");
+    return STX_E_INVALID;
+  }
+  if (p.in_mode <= STX_IN_RELU && (p.hv != p.h || p.wv != p.w)) {
+    set_error("stx_conv2d: raw dims");
+    return STX_E_INVALID;
+  }
+  const bool big = p.cout > 64;
+  if (p.ks == 3 && p.stride == 1)
+    return big ? dispatch_tw<3, 1, 128>(p, st) : dispatch_tw<3, 1, 64>(p, st);
+  if (p.ks == 3 && p.stride == 2)
+    return big ? dispatch_tw<3, 2, 128>(p, st) : dispatch_tw<3, 2, 64>(p, st);
+  if (p.ks == 9 && p.stride == 1) return dispatch_tw<9, 1, 64>(p, st);
+  if (p.ks == 1 && p.stride == 1)
+    return big ? dispatch_tw<1, 1, 128>(p, st) : dispatch_tw<1, 1, 64>(p, st);
+  set_error("stx_conv2d: unsupported ks=%d stride=%d", p.ks, p.stride);
+  return STX_E_INVALID;
+}

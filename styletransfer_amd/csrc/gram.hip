@@ -1,0 +1,277 @@
+// Gram matrix + style loss for gfx950 (fp32 MFMA 32x32x2, split-K, deterministic).
+//
+//   G[b] = F_b F_b^T / (C*H*W),  F_b = z[b].view(C, H*W)
+//   loss = mean((G - T)^2)  over B*C*C       (T broadcast over the batch)
+//
+// Reference: StyleLoss.gram_matrix / forward / set_target,
+// stransfer/network.py:92-131 (torch.bmm(features, features_t).div(d*h*w);
+// F.mse_loss(G, target.expand_as(G))).
+//
+// Kernel 1 (gram_partial): one block = one 64x64 tile (I<=J, symmetry) of one
+// image over one K-split of the H*W pixels.  The block stages 64 rows x 64 pixels
+// of F for tile-rows I and J in LDS (pitch 65: conflict-free column reads), each
+// of the 4 waves owns a 32x32 quadrant.  Partials go to a workspace slab.
+// Kernel 2 (gram_finalize): sums the splits in fixed order (bit-reproducible),
+// scales, mirrors, and for the style loss also forms (G-T), the per-tile squared
+// sum, and the backward coefficient matrix A = cA*(G-T) + alpha*I used by the
+// Gram backward dF = A F (a 1x1 MFMA conv, see stx_gram_bwd).
+#include "common.h"
+#include "../../include/stx.h"
+
+namespace stx {
+
+constexpr int GT = 64;    // tile
+constexpr int GKC = 64;   // pixels per LDS stage
+constexpr int GP = GKC + 1;
+
+__device__ __forceinline__ void tile_ij(int t, int nt, int& I, int& J) {
+  // enumerate upper triangle row-major: (0,0),(0,1)..(0,nt-1),(1,1)...
+  int i = 0;
+  while (t >= nt - i) {
+    t -= nt - i;
+    ++i;
+  }
+  I = i;
+  J = i + t;
+}
+
+__global__ void __launch_bounds__(256)
+gram_partial_kernel(const float* __restrict__ z, float* __restrict__ ws, int c, int hw,
+                    int nsplit, int split_len) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * GT * GP];
+  float* rI = smem;
+  float* rJ = smem + GT * GP;
+  const int nt = cdiv(c, GT);
+  const int ntu = nt * (nt + 1) / 2;
+  int I, J;
+  tile_ij(blockIdx.y, nt, I, J);
+  const bool diag = I == J;
+  const int split = blockIdx.x, b = blockIdx.z;
+  const int p_begin = split * split_len;
+  const int p_end = min(hw, p_begin + split_len);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int qi = wave >> 1, qj = wave & 1;
+  const float* zb = z + (size_t)b * c * hw;
+
+  // loader: thread -> (row = tid/4, 16 consecutive pixels at (tid%4)*16)
+  const int lrow = tid >> 2, lseg = (tid & 3) * 16;
+  float regI[16], regJ[16];
+  auto fetch = [&](int p0) {
+    const int gi = I * GT + lrow, gj = J * GT + lrow;
+    const float* srcI = zb + (size_t)gi * hw + p0 + lseg;
+    const float* srcJ = zb + (size_t)gj * hw + p0 + lseg;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int pp = p0 + lseg + e;
+      const bool ok = pp < p_end;
+      regI[e] = (ok && gi < c) ? srcI[e] : 0.f;
+      if (!diag) regJ[e] = (ok && gj < c) ? srcJ[e] : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      rI[lrow * GP + lseg + e] = regI[e];
+      if (!diag) rJ[lrow * GP + lseg + e] = regJ[e];
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const float* Bsrc = diag ? rI : rJ;
+  const int a_off = (qi * 32 + l32) * GP + h * 32;
+  const int b_off = (qj * 32 + l32) * GP + h * 32;
+
+  if (p_begin < p_end) fetch(p_begin);
+  for (int p0 = p_begin; p0 < p_end; p0 += GKC) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (p0 + GKC < p_end) fetch(p0 + GKC);
+#pragma unroll
+    for (int s = 0; s < 32; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(rI[a_off + s], Bsrc[b_off + s], acc, 0, 0, 0);
+  }
+  float* out = ws + (((size_t)b * ntu + blockIdx.y) * nsplit + split) * (GT * GT);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = qi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    out[row * GT + qj * 32 + l32] = acc[r];
+  }
+}
+
+// grid (ntu, B); 256 threads, 16 elements per thread
+__global__ void __launch_bounds__(256)
+gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scale,
+                     float* __restrict__ g_out, const float* __restrict__ target,
+                     float* __restrict__ coef, int cpad, float cA, float alpha,
+                     float* __restrict__ loss_parts) {
+  __shared__ float red[4];
+  const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
+  int I, J;
+  tile_ij(blockIdx.x, nt, I, J);
+  const int b = blockIdx.y;
+  const float* src = ws + ((size_t)b * ntu + blockIdx.x) * nsplit * (GT * GT);
+  float sq = 0.f;
+  for (int e = threadIdx.x; e < GT * GT; e += 256) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += src[(size_t)k * GT * GT + e];
+    const int gi = I * GT + e / GT, gj = J * GT + e % GT;
+    if (gi >= c || gj >= c) continue;
+    const float g = s * scale;
+    if (g_out) {
+      g_out[((size_t)b * c + gi) * c + gj] = g;
+      if (I != J) g_out[((size_t)b * c + gj) * c + gi] = g;
+    }
+    if (target) {
+      const float d = g - target[(size_t)gi * c + gj];
+      sq += (I != J ? 2.f : 1.f) * d * d;
+      if (coef) {
+        const float a = cA * d;
+        float* cb = coef + (size_t)b * cpad * cpad;
+        cb[(size_t)gi * cpad + gj] = a + (gi == gj ? alpha : 0.f);
+        if (I != J) cb[(size_t)gj * cpad + gi] = a;
+      }
+    }
+  }
+  if (target) {
+    const float t = block_sum<256>(sq, red);
+    if (threadIdx.x == 0) loss_parts[b * ntu + blockIdx.x] = t;
+  }
+}
+
+// single block: sum parts (fixed order) -> loss = sum * inv
+__global__ void sum_parts_kernel(const float* __restrict__ parts, int n, float inv,
+                                 float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += parts[i];
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) *out = s * inv;
+}
+
+__global__ void zero_kernel(float* p, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    p[i] = 0.f;
+}
+
+static void gram_geometry(int c, int hw, int b, int& nsplit, int& split_len, int& ntu) {
+  const int nt = cdiv(c, GT);
+  ntu = nt * (nt + 1) / 2;
+  const int chunks = cdiv(hw, GKC);
+  // aim for ~1024 blocks in flight, at least 4 chunks per split
+  int want = cdiv(1024, ntu * b);
+  want = std::max(1, std::min(want, cdiv(chunks, 4)));
+  const int per = cdiv(chunks, want);
+  split_len = per * GKC;
+  nsplit = cdiv(hw, split_len);
+}
+
+static size_t gram_ws_bytes(int b, int c, int hw) {
+  int nsplit, split_len, ntu;
+  gram_geometry(c, hw, b, nsplit, split_len, ntu);
+  // partial slabs + loss parts
+  return ((size_t)b * ntu * nsplit * GT * GT + (size_t)b * ntu + 64) * sizeof(float);
+}
+
+static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_out,
+                    const float* target, float* coef, float cA, float alpha, float* loss,
+                    float loss_inv, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (b <= 0 || c <= 0 || hw <= 0 || !z) {
+    set_error("gram: invalid dims");
+    return STX_E_INVALID;
+  }
+  int nsplit, split_len, ntu;
+  gram_geometry(c, hw, b, nsplit, split_len, ntu);
+  const size_t need = gram_ws_bytes(b, c, hw);
+  if (!ws || ws_bytes < need) {
+    set_error("gram: workspace %zu < %zu", ws_bytes, need);
+    return STX_E_WORKSPACE;
+  }
+  float* slabs = (float*)ws;
+  float* parts = slabs + (size_t)b * ntu * nsplit * GT * GT;
+  hipLaunchKernelGGL(gram_partial_kernel, dim3(nsplit, ntu, b), dim3(256), 0, st, z, slabs, c,
+                     hw, nsplit, split_len);
+  const int cpad = stx_gram_coef_pitch(c);
+  hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu, b), dim3(256), 0, st, slabs, c, nsplit,
+                     scale, g_out, target, coef, cpad, cA, alpha, parts);
+  if (target && loss)
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, st, parts, b * ntu, loss_inv,
+                       loss);
+  return check_launch("gram");
+}
+
+}  // namespace stx
+
+using namespace stx;
+
+extern "C" size_t stx_gram_ws(int b, int c, int hw) { return gram_ws_bytes(b, c, hw); }
+
+extern "C" int stx_gram_coef_pitch(int c) { return rup(c, 128); }
+
+extern "C" int stx_gram(const float* z, float* g, int b, int c, int hw, float scale, void* ws,
+                        size_t ws_bytes, void* stream) {
+  return gram_run(z, b, c, hw, scale, g, nullptr, nullptr, 0.f, 0.f, nullptr, 0.f, ws, ws_bytes,
+                  (hipStream_t)stream);
+}
+
+extern "C" int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
+                              float* loss, int b, int c, int hw, float weight, float diag_alpha,
+                              void* ws, size_t ws_bytes, void* stream) {
+  if (!target || !loss) {
+    set_error("stx_style_loss: target and loss are required");
+    return STX_E_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const double n = (double)c * hw;
+  const float scale = (float)(1.0 / n);
+  // d(weight*mean((G-T)^2))/dF_b = weight * 2(G-T)/(B C^2) * 2 F_b / N   (G symmetric)
+  const float cA = (float)(weight * 4.0 / ((double)b * c * c * n));
+  if (coef) {
+    const int cpad = stx_gram_coef_pitch(c);
+    const long long cnt = (long long)b * cpad * cpad;
+    hipLaunchKernelGGL(zero_kernel, dim3((int)std::min<long long>((cnt + 255) / 256, 2048)),
+                       dim3(256), 0, st, coef, cnt);
+  }
+  return gram_run(z, b, c, hw, scale, g_out, target, coef, cA, diag_alpha, loss,
+                  (float)(1.0 / ((double)b * c * c)), ws, ws_bytes, st);
+}
+
+extern "C" int stx_gram_bwd(const float* coef, const float* z, float* dz, int b, int c, int h,
+                            int w, const float* acc_scale_dev, const float* mask,
+                            const float* aux, float aux_scale, int accumulate, void* stream) {
+  stx_conv_params p = {};
+  p.x = z;
+  p.wt = coef;
+  p.y = dz;
+  p.mask = mask;
+  p.aux = aux;
+  p.aux_scale = aux_scale;
+  p.acc_scale = acc_scale_dev;
+  p.accumulate = accumulate;
+  p.n = b;
+  p.cin = c;
+  p.h = h;
+  p.w = w;
+  p.cout = c;
+  p.ks = 1;
+  p.stride = 1;
+  p.pad = 0;
+  p.in_mode = STX_IN_RAW;
+  p.hv = h;
+  p.wv = w;
+  p.ho = h;
+  p.wo = w;
+  stx_conv_weight_dims(c, c, 1, &p.cin_pad, &p.cout_pad);
+  const int cpad = stx_gram_coef_pitch(c);
+  if (p.cout_pad != cpad || p.cin_pad > cpad) {
+    set_error("stx_gram_bwd: pitch mismatch");
+    return STX_E_INVALID;
+  }
+  p.wt_batch_stride = (long long)cpad * cpad;
+  return stx_conv2d(&p, stream);
+}

@@ -1,0 +1,185 @@
+// InstanceNorm2d(affine=True) forward/backward for gfx950, with the ResidualBlock
+// add and the following ReLU fused.
+//
+// Reference: nn.InstanceNorm2d(num_features, affine=True) in ImageTransformNet /
+// ResidualBlock (stransfer/network.py:474,483,531,541,551,588,600; eps 1e-5,
+// biased variance, per-instance statistics in train and eval, no running stats),
+// residual `out += residual` (stransfer/network.py:502) and nn.ReLU.
+//
+// One 256-thread block per (n, c) plane.  Forward: u = x (+ res); two passes
+// over u (mean, then sum of squared deviations: numerically like torch's
+// two-pass CPU kernel), then y = (u-mean)*rstd*gamma + beta (relu).  The plane
+// (<= 256 KB at 256x256) stays L2-resident between the passes.
+#include "common.h"
+#include "../../include/stx.h"
+
+namespace stx {
+
+constexpr int NB = 256;
+
+__global__ void __launch_bounds__(NB)
+instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
+                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                    float* __restrict__ y, float* __restrict__ mean_out,
+                    float* __restrict__ rstd_out, int c, int hw, float eps, int relu) {
+  __shared__ float red[NB / 64];
+  const size_t base = (size_t)blockIdx.x * hw;
+  const int ch = blockIdx.x % c;
+  const float* xp = x + base;
+  const float* rp = res ? res + base : nullptr;
+  const bool vec = ((hw & 3) == 0);
+  float s = 0.f;
+  if (vec) {
+    for (int i = threadIdx.x * 4; i < hw; i += NB * 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(xp + i);
+      if (rp) v += *reinterpret_cast<const f32x4*>(rp + i);
+      s += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+  } else {
+    for (int i = threadIdx.x; i < hw; i += NB) s += xp[i] + (rp ? rp[i] : 0.f);
+  }
+  const float mean = block_sum<NB>(s, red) / (float)hw;
+  float q = 0.f;
+  if (vec) {
+    for (int i = threadIdx.x * 4; i < hw; i += NB * 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(xp + i);
+      if (rp) v += *reinterpret_cast<const f32x4*>(rp + i);
+      v -= mean;
+      q += (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+    }
+  } else {
+    for (int i = threadIdx.x; i < hw; i += NB) {
+      const float d = xp[i] + (rp ? rp[i] : 0.f) - mean;
+      q += d * d;
+    }
+  }
+  const float var = block_sum<NB>(q, red) / (float)hw;
+  const float rstd = 1.f / sqrtf(var + eps);
+  const float gsc = gamma ? gamma[ch] * rstd : rstd;
+  const float sh = (beta ? beta[ch] : 0.f) - mean * gsc;
+  float* yp = y + base;
+  if (vec) {
+    for (int i = threadIdx.x * 4; i < hw; i += NB * 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(xp + i);
+      if (rp) v += *reinterpret_cast<const f32x4*>(rp + i);
+      f32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[k] = v[k] * gsc + sh;
+        if (relu) o[k] = fmaxf(o[k], 0.f);
+      }
+      *reinterpret_cast<f32x4*>(yp + i) = o;
+    }
+  } else {
+    for (int i = threadIdx.x; i < hw; i += NB) {
+      float o = (xp[i] + (rp ? rp[i] : 0.f)) * gsc + sh;
+      yp[i] = relu ? fmaxf(o, 0.f) : o;
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (mean_out) mean_out[blockIdx.x] = mean;
+    if (rstd_out) rstd_out[blockIdx.x] = rstd;
+  }
+}
+
+// Backward.  g = dy * (y > 0 if relu);  xh = (u-mean)*rstd
+//   dgamma_nc = sum g*xh ; dbeta_nc = sum g
+//   du = gamma*rstd/HW * (HW*g - dbeta_nc - xh*dgamma_nc)
+__global__ void __launch_bounds__(NB)
+instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                    const float* __restrict__ x, const float* __restrict__ res,
+                    const float* __restrict__ gamma, const float* __restrict__ mean,
+                    const float* __restrict__ rstd, float* __restrict__ du,
+                    float* __restrict__ parts, int c, int hw, int relu) {
+  __shared__ float red[NB / 64];
+  const size_t base = (size_t)blockIdx.x * hw;
+  const int ch = blockIdx.x % c;
+  const float mu = mean[blockIdx.x], rs = rstd[blockIdx.x];
+  const float* dyp = dy + base;
+  const float* yp = y ? y + base : nullptr;
+  const float* xp = x + base;
+  const float* rp = res ? res + base : nullptr;
+  float sg = 0.f, sgx = 0.f;
+  for (int i = threadIdx.x; i < hw; i += NB) {
+    float g = dyp[i];
+    if (relu && !(yp[i] > 0.f)) g = 0.f;
+    const float xh = (xp[i] + (rp ? rp[i] : 0.f) - mu) * rs;
+    sg += g;
+    sgx += g * xh;
+  }
+  sg = block_sum<NB>(sg, red);
+  sgx = block_sum<NB>(sgx, red);
+  const float gm = gamma ? gamma[ch] : 1.f;
+  const float k = gm * rs / (float)hw;
+  float* dup = du + base;
+  for (int i = threadIdx.x; i < hw; i += NB) {
+    float g = dyp[i];
+    if (relu && !(yp[i] > 0.f)) g = 0.f;
+    const float xh = (xp[i] + (rp ? rp[i] : 0.f) - mu) * rs;
+    dup[i] = k * ((float)hw * g - sg - xh * sgx);
+  }
+  if (threadIdx.x == 0) {
+    parts[2 * blockIdx.x] = sgx;
+    parts[2 * blockIdx.x + 1] = sg;
+  }
+}
+
+__global__ void instnorm_param_grad_kernel(const float* __restrict__ parts, int n, int c,
+                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                           int accumulate) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < n; ++k) {
+    a += parts[2 * ((size_t)k * c + ch)];
+    b += parts[2 * ((size_t)k * c + ch) + 1];
+  }
+  if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + a : a;
+  if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + b : b;
+}
+
+}  // namespace stx
+
+using namespace stx;
+
+extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* gamma,
+                                const float* beta, float* y, float* mean, float* rstd, int n,
+                                int c, int hw, float eps, int relu, void* stream) {
+  if (n <= 0 || c <= 0 || hw <= 0 || !x || !y) {
+    set_error("stx_instnorm_fwd: invalid args");
+    return STX_E_INVALID;
+  }
+  if ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)res)) & 15) {
+    set_error("stx_instnorm_fwd: 16-byte alignment required");
+    return STX_E_INVALID;
+  }
+  hipLaunchKernelGGL(instnorm_fwd_kernel, dim3(n * c), dim3(NB), 0, (hipStream_t)stream, x, res,
+                     gamma, beta, y, mean, rstd, c, hw, eps, relu);
+  return check_launch("stx_instnorm_fwd");
+}
+
+extern "C" size_t stx_instnorm_bwd_ws(int n, int c) {
+  return (size_t)2 * n * c * sizeof(float) + 64;
+}
+
+extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
+                                const float* gamma, const float* mean, const float* rstd,
+                                float* du, float* dgamma, float* dbeta, int n, int c, int hw,
+                                int relu, int accumulate_params, void* ws, size_t ws_bytes,
+                                void* stream) {
+  if (n <= 0 || c <= 0 || hw <= 0 || !dy || !x || !du || !mean || !rstd || (relu && !y)) {
+    set_error("stx_instnorm_bwd: invalid args");
+    return STX_E_INVALID;
+  }
+  if (!ws || ws_bytes < stx_instnorm_bwd_ws(n, c)) {
+    set_error("stx_instnorm_bwd: workspace too small");
+    return STX_E_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(instnorm_bwd_kernel, dim3(n * c), dim3(NB), 0, st, dy, y, x, res, gamma, mean,
+                     rstd, du, (float*)ws, c, hw, relu);
+  if (dgamma || dbeta)
+    hipLaunchKernelGGL(instnorm_param_grad_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st,
+                       (const float*)ws, n, c, dgamma, dbeta, accumulate_params);
+  return check_launch("stx_instnorm_bwd");
+}

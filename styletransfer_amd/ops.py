@@ -1,0 +1,346 @@
+"""Functional wrappers over libstx (include/stx.h) for torch tensors.
+
+PyTorch supplies device memory, the current HIP stream and autograd plumbing;
+every arithmetic op here is a hand-written HIP kernel in libstx.so.  Nothing in
+this module falls back to a torch/CPU implementation: a non-CUDA tensor or a
+missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _native as N
+from ._native import ConvParams, check, lib
+
+__all__ = [
+    "conv_weight_dims", "conv_weight_prep", "conv2d", "conv_out_hw", "conv2d_wgrad",
+    "bias_grad", "gram", "style_loss", "gram_bwd", "mse", "diff_scale", "loss_combine",
+    "maxpool2x2", "maxpool2x2_bwd", "relupool_bwd", "relu", "relu_bwd", "adam_step",
+    "instnorm_fwd", "instnorm_bwd", "upsample2x", "upsample2x_bwd", "tv_loss",
+]
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _req(t: torch.Tensor, name: str = "tensor"):
+    if not t.is_cuda:
+        raise N.NativeError(f"{name}: the HIP path needs a device tensor (got {t.device}); "
+                            "there is no CPU fallback")
+    if t.dtype != torch.float32:
+        raise N.NativeError(f"{name}: fp32 required (got {t.dtype})")
+    if not t.is_contiguous():
+        raise N.NativeError(f"{name}: contiguous NCHW required")
+    return t
+
+
+class _Workspace:
+    """Per-device scratch buffer, grown on demand.  All users are stream-ordered
+    on the same stream and finish with the scratch inside one C call."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, nbytes: int, device) -> tuple:
+        nbytes = max(int(nbytes), 256)
+        key = (device.index if isinstance(device, torch.device) else device)
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b.data_ptr(), b.numel()
+
+
+WS = _Workspace()
+
+
+# ----------------------------------------------------------------------- conv
+def conv_weight_dims(cin, cout, ks):
+    a, b = C.c_int(), C.c_int()
+    check(lib().stx_conv_weight_dims(cin, cout, ks, C.byref(a), C.byref(b)), "weight_dims")
+    return a.value, b.value
+
+
+def conv_weight_prep(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
+    """[cout][cin][k][k] -> k-major GEMM slab (transpose=True: data-gradient slab)."""
+    _req(w, "weight")
+    cout, cin, ks, _ = w.shape
+    gin, gout = (cout, cin) if transpose else (cin, cout)
+    cp, op = conv_weight_dims(gin, gout, ks)
+    wt = torch.empty((cp * ks * ks, op), device=w.device, dtype=torch.float32)
+    check(lib().stx_conv_weight_prep(w.data_ptr(), wt.data_ptr(), cout, cin, ks, int(transpose),
+                                     _stream()), "conv_weight_prep")
+    return wt
+
+
+def virtual_hw(h, w, in_mode, hv=None, wv=None):
+    if in_mode in (N.STX_IN_RAW, N.STX_IN_RELU):
+        return h, w
+    if in_mode == N.STX_IN_RELU_POOL2:
+        return h // 2, w // 2
+    if in_mode == N.STX_IN_UPSAMPLE2:
+        return 2 * h, 2 * w
+    return hv, wv  # DILATE2: explicit
+
+
+def conv_out_hw(hv, wv, ks, stride, pad):
+    return (hv + 2 * pad - ks) // stride + 1, (wv + 2 * pad - ks) // stride + 1
+
+
+def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=None,
+           out=None, mask=None, aux=None, aux_scale=0.0, acc_scale=None, accumulate=False,
+           relu_out=False, wt_batch_stride=0, hv=None, wv=None):
+    """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`."""
+    _req(x, "x")
+    n, c, h, w = x.shape
+    assert c == cin, (c, cin)
+    if pad is None:
+        pad = ks // 2
+    hv, wv = virtual_hw(h, w, in_mode, hv, wv)
+    ho, wo = conv_out_hw(hv, wv, ks, stride, pad)
+    if out is None:
+        out = torch.empty((n, cout, ho, wo), device=x.device, dtype=torch.float32)
+    else:
+        _req(out, "out")
+        assert out.shape == (n, cout, ho, wo), (out.shape, (n, cout, ho, wo))
+    cp, op = conv_weight_dims(cin, cout, ks)
+    p = ConvParams(x=x.data_ptr(), wt=wt.data_ptr(), bias=_p(bias), y=out.data_ptr(),
+                   mask=_p(mask), aux=_p(aux), aux_scale=float(aux_scale),
+                   acc_scale=_p(acc_scale), accumulate=int(accumulate), relu_out=int(relu_out),
+                   n=n, cin=cin, h=h, w=w, cout=cout, ks=ks, stride=stride, pad=pad,
+                   in_mode=in_mode, hv=hv, wv=wv, ho=ho, wo=wo, cin_pad=cp, cout_pad=op,
+                   wt_batch_stride=int(wt_batch_stride))
+    check(lib().stx_conv2d(C.byref(p), _stream()), "stx_conv2d")
+    return out
+
+
+def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, dw=None,
+                 accumulate=False):
+    _req(x, "x")
+    _req(dy, "dy")
+    n, _, h, w = x.shape
+    if pad is None:
+        pad = ks // 2
+    hv, wv = virtual_hw(h, w, in_mode)
+    ho, wo = dy.shape[2], dy.shape[3]
+    if dw is None:
+        dw = torch.empty((cout, cin, ks, ks), device=x.device, dtype=torch.float32)
+    L = lib()
+    need = L.stx_conv2d_wgrad_ws(n, cin, cout, ks, stride, ho, wo)
+    wp, wn = WS.get(need, x.device)
+    check(L.stx_conv2d_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(accumulate), n, cin,
+                             h, w, cout, ks, stride, pad, in_mode, hv, wv, ho, wo, wp, wn,
+                             _stream()), "stx_conv2d_wgrad")
+    return dw
+
+
+def bias_grad(dy, db=None, accumulate=False):
+    _req(dy, "dy")
+    n, c = dy.shape[:2]
+    hw = dy[0, 0].numel()
+    if db is None:
+        db = torch.empty(c, device=dy.device, dtype=torch.float32)
+    L = lib()
+    wp, wn = WS.get(L.stx_bias_grad_ws(n, c), dy.device)
+    check(L.stx_bias_grad(dy.data_ptr(), db.data_ptr(), n, c, hw, int(accumulate), wp, wn,
+                          _stream()), "stx_bias_grad")
+    return db
+
+
+# ----------------------------------------------------------------------- gram
+def gram(z, scale=None):
+    """G[b] = F F^T * scale (default 1/(C*H*W), StyleLoss.gram_matrix)."""
+    _req(z, "z")
+    b, c = z.shape[:2]
+    hw = z[0, 0].numel()
+    if scale is None:
+        scale = 1.0 / (c * hw)
+    g = torch.empty((b, c, c), device=z.device, dtype=torch.float32)
+    L = lib()
+    wp, wn = WS.get(L.stx_gram_ws(b, c, hw), z.device)
+    check(L.stx_gram(z.data_ptr(), g.data_ptr(), b, c, hw, float(scale), wp, wn, _stream()),
+          "stx_gram")
+    return g
+
+
+def coef_pitch(c):
+    return lib().stx_gram_coef_pitch(c)
+
+
+def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None, loss=None,
+               coef=None):
+    """mean((gram(z) - target)^2) -> 0-d loss; coef = d(weight*loss)/dz operator."""
+    _req(z, "z")
+    _req(target, "target")
+    b, c = z.shape[:2]
+    hw = z[0, 0].numel()
+    if loss is None:
+        loss = torch.empty((), device=z.device, dtype=torch.float32)
+    if want_coef and coef is None:
+        cp = coef_pitch(c)
+        coef = torch.empty((b, cp, cp), device=z.device, dtype=torch.float32)
+    L = lib()
+    wp, wn = WS.get(L.stx_gram_ws(b, c, hw), z.device)
+    check(L.stx_style_loss(z.data_ptr(), target.data_ptr(), _p(g_out), _p(coef) if want_coef
+                           else None, loss.data_ptr(), b, c, hw, float(weight),
+                           float(diag_alpha), wp, wn, _stream()), "stx_style_loss")
+    return loss, (coef if want_coef else None)
+
+
+def gram_bwd(coef, z, dz=None, acc_scale=None, mask=None, aux=None, aux_scale=0.0,
+             accumulate=False):
+    _req(z, "z")
+    b, c, h, w = z.shape
+    if dz is None:
+        dz = torch.empty_like(z)
+    check(lib().stx_gram_bwd(coef.data_ptr(), z.data_ptr(), dz.data_ptr(), b, c, h, w,
+                             _p(acc_scale), _p(mask), _p(aux), float(aux_scale), int(accumulate),
+                             _stream()), "stx_gram_bwd")
+    return dz
+
+
+# ----------------------------------------------------------------------- mse etc
+def mse(a, b, relu=False, mode=0, out=None, grad=None, gscale=1.0):
+    """mode 0: F.mse_loss (mean); mode 1: FeatureReconstructionLoss (out[1] = mean)."""
+    _req(a, "a")
+    _req(b, "b")
+    assert a.numel() == b.numel()
+    n = a.numel()
+    if out is None:
+        out = torch.empty(2 if mode == 1 else 1, device=a.device, dtype=torch.float32)
+    L = lib()
+    wp, wn = WS.get(L.stx_mse_ws(n), a.device)
+    check(L.stx_mse(a.data_ptr(), b.data_ptr(), n, int(relu), mode, out.data_ptr(), _p(grad),
+                    float(gscale), wp, wn, _stream()), "stx_mse")
+    return out
+
+
+def diff_scale(a, b, s0, s1=None, s2=None, relu=False, out=None, accumulate=False):
+    if out is None:
+        out = torch.empty_like(a)
+    check(lib().stx_diff_scale(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), float(s0),
+                               _p(s1), _p(s2), int(relu), int(accumulate), _stream()),
+          "stx_diff_scale")
+    return out
+
+
+def loss_combine(s, weights, out):
+    k = len(weights)
+    arr = (C.c_float * k)(*[float(x) for x in weights])
+    check(lib().stx_loss_combine(s.data_ptr(), k, arr, out.data_ptr(), _stream()),
+          "stx_loss_combine")
+    return out
+
+
+# ----------------------------------------------------------------------- pooling / relu
+def maxpool2x2(x, relu_input=False, want_idx=True):
+    _req(x, "x")
+    n, c, h, w = x.shape
+    y = torch.empty((n, c, h // 2, w // 2), device=x.device, dtype=torch.float32)
+    idx = torch.empty(y.shape, device=x.device, dtype=torch.int64) if want_idx else None
+    check(lib().stx_maxpool2x2_fwd(x.data_ptr(), y.data_ptr(), _p(idx), n * c, h, w,
+                                   int(relu_input), _stream()), "stx_maxpool2x2_fwd")
+    return y, idx
+
+
+def maxpool2x2_bwd(dy, idx, h, w):
+    n, c = dy.shape[:2]
+    dx = torch.empty((n, c, h, w), device=dy.device, dtype=torch.float32)
+    check(lib().stx_maxpool2x2_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), n * c, h, w,
+                                   _stream()), "stx_maxpool2x2_bwd")
+    return dx
+
+
+def relupool_bwd(dp, z, out=None):
+    n, c, h, w = z.shape
+    if out is None:
+        out = torch.empty_like(z)
+    check(lib().stx_relupool_bwd(dp.data_ptr(), z.data_ptr(), out.data_ptr(), n * c, h, w,
+                                 _stream()), "stx_relupool_bwd")
+    return out
+
+
+def relu(x):
+    _req(x, "x")
+    y = torch.empty_like(x)
+    check(lib().stx_relu_fwd(x.data_ptr(), y.data_ptr(), x.numel(), _stream()), "stx_relu_fwd")
+    return y
+
+
+def relu_bwd(dy, y):
+    dx = torch.empty_like(dy)
+    check(lib().stx_relu_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dy.numel(), _stream()),
+          "stx_relu_bwd")
+    return dx
+
+
+# ----------------------------------------------------------------------- adam
+def adam_step(p, g, m, v, step_dev, ws, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8):
+    check(lib().stx_adam_step(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
+                              float(lr), float(beta1), float(beta2), float(eps),
+                              step_dev.data_ptr(), ws.data_ptr(), _stream()), "stx_adam_step")
+
+
+# ----------------------------------------------------------------------- instance norm
+def instnorm_fwd(x, gamma, beta, res=None, eps=1e-5, relu=False, out=None):
+    _req(x, "x")
+    n, c = x.shape[:2]
+    hw = x[0, 0].numel()
+    if out is None:
+        out = torch.empty_like(x)
+    mean = torch.empty(n * c, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    check(lib().stx_instnorm_fwd(x.data_ptr(), _p(res), _p(gamma), _p(beta), out.data_ptr(),
+                                 mean.data_ptr(), rstd.data_ptr(), n, c, hw, float(eps),
+                                 int(relu), _stream()), "stx_instnorm_fwd")
+    return out, mean, rstd
+
+
+def instnorm_bwd(dy, y, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbeta=None,
+                 accumulate=False):
+    n, c = x.shape[:2]
+    hw = x[0, 0].numel()
+    du = torch.empty_like(x)
+    L = lib()
+    wp, wn = WS.get(L.stx_instnorm_bwd_ws(n, c), x.device)
+    check(L.stx_instnorm_bwd(dy.data_ptr(), _p(y), x.data_ptr(), _p(res), _p(gamma),
+                             mean.data_ptr(), rstd.data_ptr(), du.data_ptr(), _p(dgamma),
+                             _p(dbeta), n, c, hw, int(relu), int(accumulate), wp, wn, _stream()),
+          "stx_instnorm_bwd")
+    return du
+
+
+# ----------------------------------------------------------------------- upsample / tv
+def upsample2x(x):
+    n, c, h, w = x.shape
+    y = torch.empty((n, c, 2 * h, 2 * w), device=x.device, dtype=torch.float32)
+    check(lib().stx_upsample2x_fwd(x.data_ptr(), y.data_ptr(), n * c, h, w, _stream()),
+          "stx_upsample2x_fwd")
+    return y
+
+
+def upsample2x_bwd(dy):
+    n, c, H, W = dy.shape
+    dx = torch.empty((n, c, H // 2, W // 2), device=dy.device, dtype=torch.float32)
+    check(lib().stx_upsample2x_bwd(dy.data_ptr(), dx.data_ptr(), n * c, H // 2, W // 2,
+                                   _stream()), "stx_upsample2x_bwd")
+    return dx
+
+
+def tv_loss(y, factor=1e-6, grad=None, gscale=1.0, gscale_dev=None, out=None):
+    _req(y, "y")
+    n, c, h, w = y.shape
+    if out is None:
+        out = torch.empty((), device=y.device, dtype=torch.float32)
+    L = lib()
+    wp, wn = WS.get(L.stx_tv_ws(n, c, h, w), y.device)
+    check(L.stx_tv_loss(y.data_ptr(), out.data_ptr(), _p(grad), float(gscale), _p(gscale_dev),
+                        n, c, h, w, float(factor), wp, wn, _stream()), "stx_tv_loss")
+    return out

@@ -1,0 +1,247 @@
+"""Kernel-level numerics: every libstx kernel vs a plain PyTorch fp32 reference of
+the same op (computed by torch on the same device).  Tolerances are stated per
+test: rel = ||a-b|| / ||b|| over the whole tensor (fp32 MFMA is an exact fp32
+fmaf chain; differences are summation-order rounding only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from styletransfer_amd import _native as N
+from styletransfer_amd import ops
+
+pytestmark = pytest.mark.gpu
+TOL = 2e-5
+
+
+def rel(a, b):
+    a = a.double()
+    b = b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def rnd(*shape, dev, seed=0, scale=1.0, shift=0.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.rand(*shape, generator=g) * scale + shift).to(dev)
+
+
+def vinput(x, mode):
+    if mode == N.STX_IN_RELU:
+        return F.relu(x)
+    if mode == N.STX_IN_RELU_POOL2:
+        return F.max_pool2d(F.relu(x), 2, 2)
+    if mode == N.STX_IN_UPSAMPLE2:
+        return F.interpolate(x, scale_factor=2, mode="nearest")
+    return x
+
+
+CONV_CASES = [
+    # n, cin, cout, h, w, ks, stride, mode
+    (1, 3, 64, 37, 41, 3, 1, N.STX_IN_RAW),
+    (2, 64, 64, 34, 70, 3, 1, N.STX_IN_RELU),
+    (2, 64, 128, 34, 36, 3, 1, N.STX_IN_RELU_POOL2),
+    (1, 128, 256, 40, 40, 3, 1, N.STX_IN_RELU_POOL2),
+    (2, 128, 64, 12, 10, 3, 1, N.STX_IN_UPSAMPLE2),
+    (2, 3, 32, 24, 20, 9, 1, N.STX_IN_RAW),
+    (2, 32, 3, 24, 20, 9, 1, N.STX_IN_RAW),
+    (2, 32, 64, 33, 30, 3, 2, N.STX_IN_RAW),
+    (2, 64, 128, 64, 64, 3, 2, N.STX_IN_RAW),
+    (2, 128, 128, 16, 16, 3, 1, N.STX_IN_RAW),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd(dev, case):
+    n, cin, cout, h, w, ks, s, mode = case
+    x = rnd(n, cin, h, w, dev=dev, seed=1, scale=2, shift=-1)
+    wgt = rnd(cout, cin, ks, ks, dev=dev, seed=2, scale=0.2, shift=-0.1)
+    b = rnd(cout, dev=dev, seed=3)
+    wt = ops.conv_weight_prep(wgt)
+    y = ops.conv2d(x, wt, cin, cout, ks, stride=s, in_mode=mode, bias=b)
+    ref = F.conv2d(vinput(x, mode), wgt, b, stride=s, padding=ks // 2)
+    torch.cuda.synchronize()
+    assert y.shape == ref.shape
+    assert rel(y, ref) < TOL
+
+
+def test_conv_epilogue(dev):
+    n, cin, cout, h, w = 2, 64, 64, 20, 36
+    x = rnd(n, cin, h, w, dev=dev, seed=4, scale=2, shift=-1)
+    wgt = rnd(cout, cin, 3, 3, dev=dev, seed=5, scale=0.2, shift=-0.1)
+    mask = rnd(n, cout, h, w, dev=dev, seed=6, scale=2, shift=-1)
+    aux = rnd(n, cout, h, w, dev=dev, seed=7)
+    old = rnd(n, cout, h, w, dev=dev, seed=8)
+    sc = torch.tensor(0.75, device=dev)
+    wt = ops.conv_weight_prep(wgt)
+    out = old.clone()
+    ops.conv2d(x, wt, cin, cout, 3, mask=mask, aux=aux, aux_scale=-0.5, acc_scale=sc,
+               accumulate=True, relu_out=True, out=out)
+    ref = F.conv2d(x, wgt, padding=1) * 0.75
+    ref = torch.where(mask > 0, ref, torch.zeros_like(ref)) - 0.5 * aux + old
+    ref = F.relu(ref)
+    assert rel(out, ref) < TOL
+
+
+@pytest.mark.parametrize("case", [
+    (2, 64, 64, 20, 36, 3, 1),
+    (1, 128, 256, 16, 16, 3, 1),
+    (2, 32, 64, 33, 30, 3, 2),
+    (2, 64, 128, 32, 32, 3, 2),
+    (2, 32, 3, 24, 20, 9, 1),
+])
+def test_conv_dgrad(dev, case):
+    n, cin, cout, h, w, ks, s = case
+    x = rnd(n, cin, h, w, dev=dev, seed=11, scale=2, shift=-1).requires_grad_()
+    wgt = rnd(cout, cin, ks, ks, dev=dev, seed=12, scale=0.2, shift=-0.1)
+    y = F.conv2d(x, wgt, stride=s, padding=ks // 2)
+    dy = rnd(*y.shape, dev=dev, seed=13, scale=2, shift=-1)
+    (ref,) = torch.autograd.grad(y, x, dy)
+    wtT = ops.conv_weight_prep(wgt, transpose=True)
+    if s == 1:
+        dx = ops.conv2d(dy, wtT, cout, cin, ks)
+    else:
+        dx = ops.conv2d(dy, wtT, cout, cin, ks, in_mode=N.STX_IN_DILATE2, hv=h, wv=w)
+    assert dx.shape == ref.shape
+    assert rel(dx, ref) < TOL
+
+
+@pytest.mark.parametrize("case", [
+    (2, 64, 64, 20, 36, 3, 1, N.STX_IN_RAW),
+    (2, 128, 128, 16, 16, 3, 1, N.STX_IN_RAW),
+    (2, 32, 64, 33, 30, 3, 2, N.STX_IN_RAW),
+    (2, 128, 64, 12, 10, 3, 1, N.STX_IN_UPSAMPLE2),
+    (2, 3, 32, 24, 20, 9, 1, N.STX_IN_RAW),
+    (2, 32, 3, 24, 20, 9, 1, N.STX_IN_RAW),
+])
+def test_conv_wgrad_bias(dev, case):
+    n, cin, cout, h, w, ks, s, mode = case
+    x = rnd(n, cin, h, w, dev=dev, seed=21, scale=2, shift=-1)
+    wgt = rnd(cout, cin, ks, ks, dev=dev, seed=22, scale=0.2, shift=-0.1).requires_grad_()
+    b = torch.zeros(cout, device=dev, requires_grad=True)
+    y = F.conv2d(vinput(x, mode), wgt, b, stride=s, padding=ks // 2)
+    dy = rnd(*y.shape, dev=dev, seed=23, scale=2, shift=-1)
+    rw, rb = torch.autograd.grad(y, (wgt, b), dy)
+    dw = ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s, in_mode=mode)
+    db = ops.bias_grad(dy)
+    assert rel(dw, rw) < TOL
+    assert rel(db, rb) < TOL
+
+
+@pytest.mark.parametrize("shape", [(1, 64, 32, 32), (2, 128, 16, 24), (1, 256, 8, 8),
+                                   (1, 64, 512, 512), (3, 96, 7, 9)])
+def test_gram_and_style_loss(dev, shape):
+    b, c, h, w = shape
+    z = rnd(*shape, dev=dev, seed=31, scale=2, shift=-0.5)
+    t = rnd(1, c, h, w, dev=dev, seed=32)
+    f = z.view(b, c, h * w)
+    G = torch.bmm(f, f.transpose(1, 2)) / (c * h * w)
+    ft = t.view(1, c, h * w)
+    T = torch.bmm(ft, ft.transpose(1, 2)) / (c * h * w)
+    g = ops.gram(z)
+    assert rel(g, G) < TOL
+    zr = z.clone().requires_grad_()
+    fr = zr.view(b, c, h * w)
+    loss_ref = F.mse_loss(torch.bmm(fr, fr.transpose(1, 2)) / (c * h * w), T.expand(b, c, c))
+    (dz_ref,) = torch.autograd.grad(loss_ref * 3.0, zr)
+    loss, coef = ops.style_loss(z, T[0].contiguous(), weight=3.0)
+    assert rel(loss, loss_ref) < 1e-4
+    dz = ops.gram_bwd(coef, z)
+    assert rel(dz, dz_ref) < 1e-4
+
+
+def test_mse_feature_content(dev):
+    a = rnd(2, 128, 16, 16, dev=dev, seed=41, scale=2, shift=-1)
+    b = rnd(2, 128, 16, 16, dev=dev, seed=42, scale=2, shift=-1)
+    out = ops.mse(a, b)
+    assert rel(out[0], F.mse_loss(a, b)) < 1e-5
+    out = ops.mse(a, b, relu=True, mode=1)
+    m = F.mse_loss(F.relu(a), F.relu(b))
+    assert rel(out[0], m.pow(2) / a.numel()) < 1e-5
+    assert rel(out[1], m) < 1e-5
+    g = ops.diff_scale(a, b, 2.0 / a.numel())
+    ar = a.clone().requires_grad_()
+    (gr,) = torch.autograd.grad(F.mse_loss(ar, b), ar)
+    assert rel(g, gr) < 1e-6
+
+
+def test_maxpool_relu(dev):
+    x = rnd(2, 8, 10, 14, dev=dev, seed=51, scale=2, shift=-1)
+    x[0, 0, 0, :2] = 0.25  # ties
+    x[0, 1, :2, :2] = -1.0  # all negative -> relu ties at 0
+    y, idx = ops.maxpool2x2(x, relu_input=True)
+    ry, ridx = F.max_pool2d(F.relu(x).cpu(), 2, 2, return_indices=True)
+    assert torch.equal(y.cpu(), ry)
+    assert torch.equal(idx.cpu(), ridx)
+    dy = rnd(*y.shape, dev=dev, seed=52)
+    dx = ops.maxpool2x2_bwd(dy, idx, 10, 14)
+    xr = F.relu(x).cpu().requires_grad_()
+    (rdx,) = torch.autograd.grad(F.max_pool2d(xr, 2, 2), xr, dy.cpu())
+    assert torch.equal(dx.cpu(), rdx)
+    # fused relu+pool backward from the pre-relu tensor
+    dz = ops.relupool_bwd(dy, x)
+    xr2 = x.cpu().requires_grad_()
+    (rdz,) = torch.autograd.grad(F.max_pool2d(F.relu(xr2), 2, 2), xr2, dy.cpu())
+    assert torch.equal(dz.cpu(), rdz)
+    r = ops.relu(x)
+    assert torch.equal(r, F.relu(x))
+    assert torch.equal(ops.relu_bwd(x, r), torch.where(r > 0, x, torch.zeros_like(x)))
+
+
+def test_adam(dev):
+    n = 1001
+    p = rnd(n, dev=dev, seed=61)
+    g = rnd(n, dev=dev, seed=62, scale=2, shift=-1)
+    pr = p.clone().cpu().requires_grad_()
+    opt = torch.optim.Adam([pr])
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    step = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = torch.empty(16, dtype=torch.float32, device=dev)
+    for it in range(3):
+        gi = g * (it + 1)
+        pr.grad = gi.cpu()
+        opt.step()
+        ops.adam_step(p, gi, m, v, step, ws)
+    assert int(step.item()) == 3
+    assert rel(p, pr.detach().to(dev)) < 1e-6
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (False, True)])
+def test_instnorm(dev, relu, res):
+    x = rnd(2, 32, 12, 20, dev=dev, seed=71, scale=3, shift=-1).requires_grad_()
+    r = rnd(2, 32, 12, 20, dev=dev, seed=72).requires_grad_() if res else None
+    gamma = rnd(32, dev=dev, seed=73, shift=0.5).requires_grad_()
+    beta = rnd(32, dev=dev, seed=74).requires_grad_()
+    u = x + r if res else x
+    ref = F.instance_norm(u, weight=gamma, bias=beta, eps=1e-5)
+    if relu:
+        ref = F.relu(ref)
+    y, mean, rstd = ops.instnorm_fwd(x.detach(), gamma.detach(), beta.detach(),
+                                     res=r.detach() if res else None, relu=relu)
+    assert rel(y, ref) < 1e-5
+    dy = rnd(*y.shape, dev=dev, seed=75, scale=2, shift=-1)
+    grads = torch.autograd.grad(ref, [x, gamma, beta], dy)
+    dg = torch.empty(32, device=dev)
+    db = torch.empty(32, device=dev)
+    du = ops.instnorm_bwd(dy, y, x.detach(), r.detach() if res else None, gamma.detach(), mean,
+                          rstd, relu=relu, dgamma=dg, dbeta=db)
+    assert rel(du, grads[0]) < 1e-4
+    assert rel(dg, grads[1]) < 1e-5
+    assert rel(db, grads[2]) < 1e-5
+
+
+def test_upsample_tv(dev):
+    x = rnd(2, 3, 5, 7, dev=dev, seed=81)
+    assert torch.equal(ops.upsample2x(x), F.interpolate(x, scale_factor=2, mode="nearest"))
+    dy = rnd(2, 3, 10, 14, dev=dev, seed=82)
+    xr = x.clone().requires_grad_()
+    (rdx,) = torch.autograd.grad(F.interpolate(xr, scale_factor=2, mode="nearest"), xr, dy)
+    assert rel(ops.upsample2x_bwd(dy), rdx) < 1e-6
+    y = rnd(2, 3, 20, 24, dev=dev, seed=83, scale=3, shift=-1)
+    yr = y.clone().requires_grad_()
+    ref = 1e-6 * (torch.sum(torch.abs(yr[:, :, :, :-1] - yr[:, :, :, 1:]))
+                  + torch.sum(torch.abs(yr[:, :, :-1, :] - yr[:, :, 1:, :])))
+    (rg,) = torch.autograd.grad(ref, yr)
+    g = torch.empty_like(y)
+    loss = ops.tv_loss(y, 1e-6, grad=g)
+    assert rel(loss, ref) < 1e-5
+    assert rel(g, rg) < 1e-6
