@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: Gatys iters/s at 512x512 (+ fast_st train images/s at 256x256).
+
+BASELINE.json metric "Gatys iters/sec at 512x512 + fast_st images/sec at
+256x256, 1/2/4/8 GPUs".  `value` = Gatys iterations/s of the whole job (config 2:
+gatys_st 512x512 single image, Adam iterations = forward + backward + Adam update
+of the image, one hipGraph replay each).  Gatys optimises one image serially, so
+ranks run independent replicas and the job rate is the sum.
+The fast_st leg (config 4 shape: 256x256, per-GPU batch 8, data-parallel with one
+RCCL all-reduce of the flat ImageTransformNet gradient per step) is reported in
+the same line under "fast_st".  Inputs are resident in HBM before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...    (one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+os.environ.setdefault("STX_NO_LOGFILE", "1")
+
+from styletransfer_amd import ops  # noqa: E402
+from styletransfer_amd import vgg as V  # noqa: E402
+from styletransfer_amd import weights as W  # noqa: E402
+from styletransfer_amd import _native as N  # noqa: E402
+
+METRIC = ("Gatys iters/sec at 512×512 + fast_st images/sec at 256×256, "
+          "1/2/4/8 GPUs")
+# algorithmic FLOPs (2*MAC), SURVEY.md §8(d)
+GATYS_GFLOP = {512: 139.25, 256: 34.81}
+FAST_ST_GFLOP_PER_IMAGE = 107.59
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32-input MFMA = f32 vector peak
+PEAK_HBM_GBS = 8000.0
+
+
+def conv_gflop(cin, cout, h, w, ks=3):
+    return 2.0 * cin * cout * ks * ks * h * w / 1e9
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--fast-batch", type=int, default=8, help="fast_st images per GPU")
+    ap.add_argument("--fast-steps", type=int, default=0, help="default: max(2, steps//10)")
+    ap.add_argument("--skip-fast", action="store_true")
+    ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=4)
+    ap.add_argument("--no-graph", action="store_true")
+    return ap.parse_args()
+
+
+def timed(fn, k, world, dev):
+    """barrier + sync on both sides of exactly k calls; max over ranks (seconds)."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def event_avg_ms(fn, reps=10):
+    """Average duration of `fn` (one kernel launch) by HIP events on the stream the
+    kernel is launched on (torch's current stream)."""
+    st = torch.cuda.current_stream()
+    fn()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        fn()
+    e1.record(st)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def gatys_leg(args, world, rank, dev):
+    H = args.size
+    style = torch.from_numpy(W.synthetic_image(1000 + rank, (1, 3, H, H))).to(dev)
+    content = torch.from_numpy(W.synthetic_image(2000 + rank, (1, 3, H, H))).to(dev)
+    feat = V.VGGFeatures(V.load_vgg19_weights(), dev)
+    eng = V.GatysEngine(feat, style, content)
+    if args.no_graph:
+        for _ in range(args.warmup):
+            eng.step()
+    else:
+        eng.capture(warmup=max(1, args.warmup))
+    dt = timed(eng.step, args.steps, world, dev)
+    rate = world * args.steps / dt
+    # dominant kernel: the 3x3 implicit-GEMM conv at 64 channels, 512x512
+    # (conv1_2 forward; its data-gradient launch has the same shape and FLOPs)
+    z1 = eng.st.z[0]
+    out = torch.empty_like(z1)
+    fwd_ms = event_avg_ms(lambda: feat.conv(1, z1, out), reps=10)
+    dz = torch.empty_like(z1)
+    dgr_ms = event_avg_ms(lambda: ops.conv2d(z1, feat.wtT[1], 64, 64, 3, mask=z1, out=dz), 10)
+    gf = conv_gflop(64, 64, H, H)
+    avg_ms = 0.5 * (fwd_ms + dgr_ms)
+    achieved = gf / (avg_ms * 1e-3) / 1e3  # TFLOP/s
+    loss = float(eng.total)
+    return dict(rate=rate, dt=dt, loss=loss, kernel=dict(fwd_ms=fwd_ms, dgrad_ms=dgr_ms,
+                                                         gflop=gf, tflops=achieved))
+
+
+def fast_st_leg(args, world, rank, dev):
+    from styletransfer_amd import network
+    from styletransfer_amd.train import FastStTrainer
+    B = args.fast_batch
+    style = torch.from_numpy(W.synthetic_image(3000, (1, 3, 256, 256))).to(dev)
+    itn = network.ImageTransformNet(style, batch_size=B).to(dev)
+    itn.load_state_dict({k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)})
+    tr = FastStTrainer(itn, style, world_size=world)
+    batch = torch.from_numpy(W.synthetic_image(4000 + rank, (B, 3, 256, 256))).to(dev)
+    steps = args.fast_steps or max(2, args.steps // 10)
+    for _ in range(max(1, min(args.warmup, 2))):
+        tr.step(batch)
+    dt = timed(lambda: tr.step(batch), steps, world, dev)
+    ips = world * B * steps / dt
+    return dict(rate=ips, dt=dt, steps=steps, batch=B)
+
+
+def cpu_baseline(args):
+    """The oracle (torch-CPU restatement of the reference schedule) on host cores."""
+    from oracle import reference_cpu as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    H = args.size
+    s = torch.from_numpy(W.synthetic_image(1000, (1, 3, H, H)))
+    c = torch.from_numpy(W.synthetic_image(2000, (1, 3, H, H)))
+    net = O.StyleNetwork(s, c)
+    x = c.clone()
+    opt = net.get_content_optimizer(x)
+    O.gatys_adam_iter(net, x, c, opt)  # warm-up
+    n = args.cpu_iters
+    t0 = time.perf_counter()
+    for _ in range(n):
+        O.gatys_adam_iter(net, x, c, opt)
+    dt = time.perf_counter() - t0
+    model = ""
+    try:
+        out = subprocess.check_output(["lscpu"], text=True)
+        model = next((l.split(":", 1)[1].strip() for l in out.splitlines()
+                      if l.startswith("Model name")), "")
+    except Exception:  # noqa: BLE001
+        model = platform.processor()
+    return dict(value=n / dt, unit="iters/s", cores=threads, kind="port",
+                sample=f"oracle/reference_cpu.py Gatys Adam loop {H}x{H}, {n} timed iters "
+                       f"after 1 warm-up ({dt:.1f} s), reference schedule incl. prefix "
+                       f"re-runs and VGG wgrad; torch {torch.__version__} CPU, {model}")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    N.lib()
+    g = gatys_leg(args, world, rank, dev)
+    fs = None if args.skip_fast else fast_st_leg(args, world, rank, dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.skip_cpu:
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        k = g["kernel"]
+        res = {
+            "metric": METRIC,
+            "value": round(g["rate"], 3),
+            "unit": "iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * g["dt"] / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (hash-PRNG images and VGG-19 weights; no pretrained download)",
+            "config": {"workload": f"gatys_st {args.size}x{args.size} single image, Adam "
+                                   "iterations (BASELINE configs[1]); one independent image "
+                                   "per GPU (replicas)",
+                       "image": args.size, "batch": 1, "parallelism": f"replicas{world}",
+                       "graph": not args.no_graph},
+            "roofline": {
+                "bound": "mfma",
+                "kernel": "conv_fwd_kernel<3,1,8,64,64> (conv1_2 fwd + dgrad, 64->64 @ "
+                          f"{args.size}^2)",
+                "achieved": round(k["tflops"], 3),
+                "peak": PEAK_F32_MFMA_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(k["tflops"] / PEAK_F32_MFMA_TFLOPS, 4),
+                "traffic": None,
+                "per_launch_gflop": round(k["gflop"], 3),
+                "fwd_ms": round(k["fwd_ms"], 4),
+                "dgrad_ms": round(k["dgrad_ms"], 4),
+                "iteration_tflops": round(GATYS_GFLOP.get(args.size, float("nan")) * g["rate"]
+                                          / world / 1e3, 3),
+            },
+            "cpu_baseline": cpu,
+            "gatys_loss": g["loss"],
+        }
+        if fs:
+            res["fast_st"] = {
+                "value": round(fs["rate"], 3), "unit": "images/s",
+                "per_gpu_batch": fs["batch"], "global_batch": fs["batch"] * world,
+                "steps": fs["steps"], "ms_per_step": round(1e3 * fs["dt"] / fs["steps"], 3),
+                "parallelism": f"dp{world}", "scaling": "weak",
+                "collective": "RCCL all_reduce(SUM) of 1,679,235 fp32 grads per step"
+                              if world > 1 else None,
+                "tflops_per_gpu": round(FAST_ST_GFLOP_PER_IMAGE * fs["rate"] / world / 1e3, 3),
+            }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

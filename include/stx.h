@@ -104,8 +104,8 @@ int stx_gram(const float* z, float* g, int b, int c, int hw, float scale,
  * cpad = stx_gram_coef_pitch(c).  ws: stx_gram_ws(b, c, hw). */
 int stx_gram_coef_pitch(int c);
 int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
-                   float* loss, int b, int c, int hw, float weight, float diag_alpha,
-                   void* ws, size_t ws_bytes, void* stream);
+                   float* loss, int b, int c, int hw, int target_batched, float weight,
+                   float diag_alpha, void* ws, size_t ws_bytes, void* stream);
 /* dz (+)= s * A[b]·z[b] (+ aux_scale*aux) — Gram backward as a 1x1 MFMA conv with
  * per-image weights; z viewed [b][c][h][w]; s = *acc_scale_dev (or 1 if NULL) */
 int stx_gram_bwd(const float* coef, const float* z, float* dz, int b, int c, int h, int w,

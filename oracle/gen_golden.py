@@ -267,7 +267,7 @@ def case_stylenet(N, H=64):
         for it in range(3):
             losses.append(float(O.gatys_adam_iter(net, x, content, opt)))
             if it == 0:
-                out[f"{tag}_adam1"] = O.to_np(x)
+                out[f"{tag}_adam1"] = O.to_np(x).copy()  # .numpy() aliases the live tensor
         out[f"{tag}_adam3"] = O.to_np(x)
         out[f"{tag}_adam_losses"] = np.array(losses)
     close(out["ora_adam_losses"], out["ref_adam_losses"], rtol=1e-5, what="adam losses")

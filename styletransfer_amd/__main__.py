@@ -1,0 +1,4 @@
+from .clis import cli
+
+if __name__ == "__main__":
+    cli(prog_name="stransfer")

@@ -1,0 +1,248 @@
+"""torch.autograd.Functions over libstx so the reference-style module API
+(`loss.backward()` on StyleLoss/ContentLoss sums, ImageTransformNet training)
+runs on the HIP kernels unchanged."""
+from __future__ import annotations
+
+import torch
+
+from . import _native as N
+from . import ops
+from . import vgg as V
+
+
+def _c(t):
+    return t.contiguous() if t is not None and not t.is_contiguous() else t
+
+
+# ----------------------------------------------------------------------- conv
+class Conv2dFn(torch.autograd.Function):
+    """y = conv2d(V(x), w) + b with V = identity / relu / nearest-upsample-x2.
+    (nn.Conv2d of VGG-19 and ImageTransformNet; zero padding.)"""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, in_mode, wt=None):
+        x = _c(x)
+        cout, cin, ks, _ = w.shape
+        if wt is None:
+            wt = ops.conv_weight_prep(w.detach().contiguous())
+        y = ops.conv2d(x, wt, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
+                       bias=None if b is None else b.detach())
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, in_mode, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, in_mode, has_b = ctx.cfg
+        dy = _c(dy)
+        cout, cin, ks, _ = w.shape
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
+            h, wd = x.shape[2], x.shape[3]
+            hv, wv = ops.virtual_hw(h, wd, in_mode)
+            if stride == 1:
+                dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad)
+            elif stride == 2:
+                dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad,
+                                in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv)
+            else:
+                raise NotImplementedError("stride > 2")
+            if in_mode == N.STX_IN_UPSAMPLE2:
+                dx = ops.upsample2x_bwd(dv)
+            elif in_mode == N.STX_IN_RELU:
+                dx = ops.relu_bwd(dv, x)
+            elif in_mode == N.STX_IN_RAW:
+                dx = dv
+            else:
+                raise NotImplementedError("in_mode backward")
+        if ctx.needs_input_grad[1]:
+            dw = ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode)
+        if has_b and ctx.needs_input_grad[2]:
+            db = ops.bias_grad(dy)
+        return dx, dw, db, None, None, None, None
+
+
+def conv2d(x, w, b=None, stride=1, pad=None, in_mode=N.STX_IN_RAW, wt=None):
+    ks = w.shape[-1]
+    return Conv2dFn.apply(x, w, b, stride, ks // 2 if pad is None else pad, in_mode, wt)
+
+
+# ----------------------------------------------------------------------- relu / pool
+class ReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = ops.relu(_c(x))
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return ops.relu_bwd(_c(dy), y)
+
+
+class MaxPool2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _c(x)
+        y, idx = ops.maxpool2x2(x)
+        ctx.save_for_backward(idx)
+        ctx.hw = x.shape[2:]
+        ctx.mark_non_differentiable(idx)
+        return y, idx
+
+    @staticmethod
+    def backward(ctx, dy, _didx):
+        (idx,) = ctx.saved_tensors
+        return ops.maxpool2x2_bwd(_c(dy), idx, *ctx.hw)
+
+
+class Upsample2xFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return ops.upsample2x(_c(x))
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ops.upsample2x_bwd(_c(dy))
+
+
+# ----------------------------------------------------------------------- instance norm
+class InstanceNormFn(torch.autograd.Function):
+    """y = [relu](IN(x (+ res)) * gamma + beta), per-instance stats (eps 1e-5)."""
+
+    @staticmethod
+    def forward(ctx, x, res, gamma, beta, eps, relu):
+        x, res = _c(x), _c(res)
+        y, mean, rstd = ops.instnorm_fwd(x, None if gamma is None else gamma.detach(),
+                                         None if beta is None else beta.detach(), res=res,
+                                         eps=eps, relu=relu)
+        ctx.save_for_backward(x, res, gamma, y, mean, rstd)
+        ctx.relu = relu
+        ctx.has_res = res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, gamma, y, mean, rstd = ctx.saved_tensors
+        c = x.shape[1]
+        dg = torch.empty(c, device=x.device) if gamma is not None else None
+        db = torch.empty(c, device=x.device) if gamma is not None else None
+        du = ops.instnorm_bwd(_c(dy), y, x, res, None if gamma is None else gamma.detach(),
+                              mean, rstd, relu=ctx.relu, dgamma=dg, dbeta=db)
+        return du, (du if ctx.has_res else None), dg, db, None, None
+
+
+def instance_norm(x, gamma, beta, res=None, eps=1e-5, relu=False):
+    return InstanceNormFn.apply(x, res, gamma, beta, eps, relu)
+
+
+# ----------------------------------------------------------------------- losses
+class GramFn(torch.autograd.Function):
+    """StyleLoss.gram_matrix: G = F Fᵀ / (C·H·W) (stransfer/network.py:92-108)."""
+
+    @staticmethod
+    def forward(ctx, z):
+        z = _c(z)
+        ctx.save_for_backward(z)
+        return ops.gram(z)
+
+    @staticmethod
+    def backward(ctx, dG):
+        (z,) = ctx.saved_tensors
+        b, c = z.shape[:2]
+        n = z[0].numel()
+        cp = ops.coef_pitch(c)
+        # dz = (dG + dGᵀ) F / N as a per-image 1x1 MFMA conv
+        coef = torch.zeros((b, cp, cp), device=z.device, dtype=torch.float32)
+        coef[:, :c, :c] = (dG + dG.transpose(1, 2)) / n
+        return ops.gram_bwd(coef, z)
+
+
+class StyleLossFn(torch.autograd.Function):
+    """mean((gram(z) - T)^2) (StyleLoss.forward, stransfer/network.py:110-123)."""
+
+    @staticmethod
+    def forward(ctx, z, target):
+        z = _c(z)
+        loss, coef = ops.style_loss(z, _c(target.detach()), weight=1.0)
+        ctx.save_for_backward(z, coef)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        z, coef = ctx.saved_tensors
+        return ops.gram_bwd(coef, z, acc_scale=_c(g.reshape(1))), None
+
+
+class MSELossFn(torch.autograd.Function):
+    """F.mse_loss(x, target) (ContentLoss.forward, stransfer/network.py:155-164)."""
+
+    @staticmethod
+    def forward(ctx, x, target):
+        x, target = _c(x), _c(target.detach())
+        out = ops.mse(x, target)
+        ctx.save_for_backward(x, target)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        x, t = ctx.saved_tensors
+        return ops.diff_scale(x, t, 2.0 / x.numel(), s1=_c(g.reshape(1))), None
+
+
+class FeatureLossFn(torch.autograd.Function):
+    """mse(x, t)^2 / numel (FeatureReconstructionLoss.forward, :186-201)."""
+
+    @staticmethod
+    def forward(ctx, x, target):
+        x, target = _c(x), _c(target.detach())
+        # relu=False: the inputs are already what the tap sees
+        out = torch.empty(2, device=x.device, dtype=torch.float32)
+        ops.mse(x, target, mode=1, out=out)
+        ctx.save_for_backward(x, target, out)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        x, t, out = ctx.saved_tensors
+        n = float(x.numel())
+        return ops.diff_scale(x, t, 4.0 / (n * n), s1=_c(g.reshape(1)), s2=out[1:2]), None
+
+
+class TVLossFn(torch.autograd.Function):
+    """get_total_variation_regularization_loss (stransfer/network.py:621-641)."""
+
+    @staticmethod
+    def forward(ctx, y, factor):
+        y = _c(y)
+        ctx.save_for_backward(y)
+        ctx.factor = factor
+        return ops.tv_loss(y, factor)
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        grad = torch.empty_like(y)
+        ops.tv_loss(y, ctx.factor, grad=grad, gscale_dev=_c(g.reshape(1)))
+        return grad, None
+
+
+class VGGLossFn(torch.autograd.Function):
+    """All 7 StyleNetwork losses of a batch in one fused forward/backward:
+    returns [style1..5, content, feature] for input x given the style targets and
+    the content target c4 (engine: styletransfer_amd/vgg.py)."""
+
+    @staticmethod
+    def forward(ctx, x, c4, feat, targets):
+        st = V.loss_forward(feat, targets, _c(x), _c(c4))
+        ctx.st, ctx.feat = st, feat
+        return V.loss_values(st).clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        dx = V.loss_backward(ctx.feat, ctx.st, _c(g), feature_grad=True)
+        ctx.st = None
+        return dx, None, None, None

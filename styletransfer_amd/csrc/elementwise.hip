@@ -200,10 +200,10 @@ __global__ void adam_prepare_kernel(int* step, AdamScalars* sc, double lr, doubl
 __global__ void __launch_bounds__(256)
 adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
             float* __restrict__ v, long long n, float b1, float b2, float eps,
-            const AdamScalars* __restrict__ sc) {
+            const AdamScalars* __restrict__ sc, int vec) {
   const float step_size = sc->step_size, bc2s = sc->bc2_sqrt;
   const float w1 = 1.f - b1, w2 = 1.f - b2;
-  const long long n4 = n / 4;
+  const long long n4 = vec ? n / 4 : 0;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
@@ -456,17 +456,15 @@ extern "C" int stx_adam_step(float* p, const float* g, float* m, float* v, long 
     set_error("stx_adam_step: invalid args");
     return STX_E_INVALID;
   }
-  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) {
-    set_error("stx_adam_step: buffers must be 16-byte aligned");
-    return STX_E_INVALID;
-  }
+  const int vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
   hipStream_t st = (hipStream_t)stream;
   AdamScalars* sc = (AdamScalars*)ws;
   hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(1), 0, st, step_dev, sc, (double)lr,
                      (double)beta1, (double)beta2);
-  const int blocks = (int)std::max<long long>(1, std::min<long long>((n / 4 + 255) / 256, 4096));
+  const long long units = vec ? n / 4 : n;
+  const int blocks = (int)std::max<long long>(1, std::min<long long>((units + 255) / 256, 4096));
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, st, p, g, m, v, n, beta1, beta2,
-                     eps, sc);
+                     eps, sc, vec);
   return check_launch("stx_adam_step");
 }
 

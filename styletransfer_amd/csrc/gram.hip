@@ -106,7 +106,7 @@ gram_partial_kernel(const float* __restrict__ z, float* __restrict__ ws, int c, 
 // grid (ntu, B); 256 threads, 16 elements per thread
 __global__ void __launch_bounds__(256)
 gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scale,
-                     float* __restrict__ g_out, const float* __restrict__ target,
+                     float* __restrict__ g_out, const float* __restrict__ target, long long t_bstride,
                      float* __restrict__ coef, int cpad, float cA, float alpha,
                      float* __restrict__ loss_parts) {
   __shared__ float red[4];
@@ -127,7 +127,7 @@ gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scal
       if (I != J) g_out[((size_t)b * c + gj) * c + gi] = g;
     }
     if (target) {
-      const float d = g - target[(size_t)gi * c + gj];
+      const float d = g - target[(size_t)b * t_bstride + (size_t)gi * c + gj];
       sq += (I != J ? 2.f : 1.f) * d * d;
       if (coef) {
         const float a = cA * d;
@@ -179,7 +179,7 @@ static size_t gram_ws_bytes(int b, int c, int hw) {
 }
 
 static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_out,
-                    const float* target, float* coef, float cA, float alpha, float* loss,
+                    const float* target, long long t_bstride, float* coef, float cA, float alpha, float* loss,
                     float loss_inv, void* ws, size_t ws_bytes, hipStream_t st) {
   if (b <= 0 || c <= 0 || hw <= 0 || !z) {
     set_error("gram: invalid dims");
@@ -198,7 +198,7 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
                      hw, nsplit, split_len);
   const int cpad = stx_gram_coef_pitch(c);
   hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu, b), dim3(256), 0, st, slabs, c, nsplit,
-                     scale, g_out, target, coef, cpad, cA, alpha, parts);
+                     scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts);
   if (target && loss)
     hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, st, parts, b * ntu, loss_inv,
                        loss);
@@ -215,12 +215,12 @@ extern "C" int stx_gram_coef_pitch(int c) { return rup(c, 128); }
 
 extern "C" int stx_gram(const float* z, float* g, int b, int c, int hw, float scale, void* ws,
                         size_t ws_bytes, void* stream) {
-  return gram_run(z, b, c, hw, scale, g, nullptr, nullptr, 0.f, 0.f, nullptr, 0.f, ws, ws_bytes,
+  return gram_run(z, b, c, hw, scale, g, nullptr, 0, nullptr, 0.f, 0.f, nullptr, 0.f, ws, ws_bytes,
                   (hipStream_t)stream);
 }
 
 extern "C" int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
-                              float* loss, int b, int c, int hw, float weight, float diag_alpha,
+                              float* loss, int b, int c, int hw, int target_batched, float weight, float diag_alpha,
                               void* ws, size_t ws_bytes, void* stream) {
   if (!target || !loss) {
     set_error("stx_style_loss: target and loss are required");
@@ -237,7 +237,7 @@ extern "C" int stx_style_loss(const float* z, const float* target, float* g_out,
     hipLaunchKernelGGL(zero_kernel, dim3((int)std::min<long long>((cnt + 255) / 256, 2048)),
                        dim3(256), 0, st, coef, cnt);
   }
-  return gram_run(z, b, c, hw, scale, g_out, target, coef, cA, diag_alpha, loss,
+  return gram_run(z, b, c, hw, scale, g_out, target, target_batched ? (long long)c * c : 0, coef, cA, diag_alpha, loss,
                   (float)(1.0 / ((double)b * c * c)), ws, ws_bytes, st);
 }
 

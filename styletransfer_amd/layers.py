@@ -1,0 +1,78 @@
+"""nn layers whose forward runs on libstx.  They subclass the torch.nn layers
+the reference builds its networks from (so `isinstance(layer, nn.Conv2d)`,
+parameter names and `state_dict()` keys are unchanged) and keep the same class
+names, because the reference names VGG layers by `type(layer).__name__`
+(stransfer/network.py:273-274: 'Conv2d_4', 'ReLU_4', ...)."""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _native as N
+from . import autograd as A
+
+
+class Conv2d(nn.Conv2d):
+    """nn.Conv2d on the HIP implicit-GEMM kernel.  `padding_mode='reflection'`
+    (stransfer/network.py:473,...,609) is not a torch padding mode; at the
+    reference's pinned torch==1.1.0 it fell through to zero padding, which is
+    what is implemented here."""
+
+    def __init__(self, *args, padding_mode="zeros", **kwargs):
+        if padding_mode == "reflection":
+            padding_mode = "zeros"
+        super().__init__(*args, padding_mode=padding_mode, **kwargs)
+        if self.padding_mode != "zeros":
+            raise NotImplementedError(f"padding_mode={self.padding_mode}")
+        if self.groups != 1 or self.dilation != (1, 1):
+            raise NotImplementedError("groups/dilation")
+        if self.kernel_size[0] != self.kernel_size[1] or self.kernel_size[0] not in (1, 3, 9):
+            raise NotImplementedError(f"kernel_size {self.kernel_size}")
+        self._wt_cache = None
+
+    def prepped(self):
+        """Cached GEMM slab of a frozen weight (re-prepped when the weight changes)."""
+        w = self.weight
+        key = (w.data_ptr(), w._version, w.device)
+        if self._wt_cache is None or self._wt_cache[0] != key:
+            from . import ops
+            self._wt_cache = (key, ops.conv_weight_prep(w.detach().contiguous()))
+        return self._wt_cache[1]
+
+    def forward(self, x, in_mode=N.STX_IN_RAW):
+        wt = None if self.weight.requires_grad else self.prepped()
+        return A.conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], in_mode, wt)
+
+
+class ReLU(nn.ReLU):
+    def forward(self, x):
+        return A.ReLUFn.apply(x)
+
+
+class MaxPool2d(nn.MaxPool2d):
+    def __init__(self, kernel_size=2, stride=2, **kw):
+        super().__init__(kernel_size, stride, **kw)
+        if self.kernel_size not in (2, (2, 2)) or self.stride not in (2, (2, 2)) or \
+                self.padding not in (0, (0, 0)) or self.ceil_mode or self.dilation not in (1,):
+            raise NotImplementedError("only MaxPool2d(2, 2)")
+
+    def forward(self, x):
+        y, idx = A.MaxPool2dFn.apply(x)
+        return (y, idx) if self.return_indices else y
+
+
+class InstanceNorm2d(nn.InstanceNorm2d):
+    def forward(self, x, relu=False, res=None):
+        if self.track_running_stats:
+            raise NotImplementedError("track_running_stats")
+        return A.instance_norm(x, self.weight, self.bias, res=res, eps=self.eps, relu=relu)
+
+
+class Upsample(nn.Upsample):
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        if self.mode != "nearest" or float(self.scale_factor) != 2.0:
+            raise NotImplementedError("only nearest x2 upsampling")
+
+    def forward(self, x):
+        return A.Upsample2xFn.apply(x)

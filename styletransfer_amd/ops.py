@@ -181,6 +181,10 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
     _req(target, "target")
     b, c = z.shape[:2]
     hw = z[0, 0].numel()
+    # target [c][c] / [1][c][c] broadcast over the batch (expand_as), or [b][c][c]
+    tb = target.numel() == b * c * c and b > 1
+    if not tb and target.numel() != c * c:
+        raise ValueError(f"style target {tuple(target.shape)} cannot expand to ({b},{c},{c})")
     if loss is None:
         loss = torch.empty((), device=z.device, dtype=torch.float32)
     if want_coef and coef is None:
@@ -189,7 +193,7 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
     L = lib()
     wp, wn = WS.get(L.stx_gram_ws(b, c, hw), z.device)
     check(L.stx_style_loss(z.data_ptr(), target.data_ptr(), _p(g_out), _p(coef) if want_coef
-                           else None, loss.data_ptr(), b, c, hw, float(weight),
+                           else None, loss.data_ptr(), b, c, hw, int(tb), float(weight),
                            float(diag_alpha), wp, wn, _stream()), "stx_style_loss")
     return loss, (coef if want_coef else None)
 

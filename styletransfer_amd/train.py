@@ -1,0 +1,98 @@
+"""fast_st training step on libstx, single GPU or data-parallel over RCCL.
+
+One step = the `static_train` closure + `optimizer.step` of the reference
+(stransfer/network.py:690-731, :765):
+
+    y = itn(batch); loss_network(y, content_image=batch)
+    total = style_weight*sum(style) + content_weight*content + TV(y); total.backward(); adam
+
+Parameters and gradients of the ImageTransformNet live in ONE flat fp32 buffer
+each (the nn.Parameters are views), so the data-parallel exchange is a single
+RCCL all-reduce of 1,679,235 floats per step and Adam is a single kernel.
+
+Data-parallel scaling trap: style/content are batch MEANS, TV is
+a batch SUM.  With the global batch split into W equal shards, the gradient of
+the single-device loss equals SUM over ranks of the gradient of
+    (style_weight*style_r + content_weight*content_r) / W + TV_r,
+which is what each rank back-propagates before the SUM all-reduce.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import autograd as A
+from . import constants
+from . import vgg as V
+from .optim import FlatAdam
+
+
+def flatten_parameters(module: torch.nn.Module, device):
+    """Re-home every parameter (and its .grad) as a view of one flat buffer."""
+    params = [p for p in module.parameters()]
+    total = sum(p.numel() for p in params)
+    flat = torch.empty(total, device=device, dtype=torch.float32)
+    grad = torch.zeros(total, device=device, dtype=torch.float32)
+    o = 0
+    for p in params:
+        n = p.numel()
+        flat[o:o + n].copy_(p.data.reshape(-1))
+        p.data = flat[o:o + n].view_as(p)
+        p.grad = grad[o:o + n].view_as(p)
+        o += n
+    return flat, grad
+
+
+class FastStTrainer:
+    def __init__(self, itn, style_image, style_weight=100_000, content_weight=1, lr=1e-3,
+                 world_size=1, process_group=None, vgg_weights=None, tv_factor=1e-6):
+        dev = constants.DEVICE if not isinstance(style_image, torch.Tensor) or \
+            not style_image.is_cuda else style_image.device
+        self.itn = itn
+        self.device = torch.device(dev)
+        self.feat = V.VGGFeatures(V.load_vgg19_weights(vgg_weights), self.device)
+        style = style_image.to(self.device, torch.float32)
+        if style.dim() == 3:
+            style = style.unsqueeze(0)
+        self.style_image = style
+        self.targets = self.feat.style_targets(style)
+        self.sw, self.cw, self.tv = float(style_weight), float(content_weight), float(tv_factor)
+        self.world = int(world_size)
+        self.pg = process_group
+        self.flat, self.flat_grad = flatten_parameters(itn, self.device)
+        self.opt = FlatAdam(self.flat, self.flat_grad, lr=lr)
+        self.vgg_weights = vgg_weights
+
+    def resync_params(self):
+        """No-op: load_state_dict copies into the flat views in place."""
+
+    def loss_network(self):
+        """A StyleNetwork (reference API) with the same VGG weights and style targets,
+        for static_test (stransfer/network.py:661-663)."""
+        from .network import StyleNetwork
+        return StyleNetwork(self.style_image, torch.rand([1, 3, 256, 256]),
+                            vgg_weights=self.vgg_weights)
+
+    def _total(self, batch, y):
+        with torch.no_grad():
+            c4 = V.content_target(self.feat, batch)
+        losses = A.VGGLossFn.apply(y, c4, self.feat, self.targets)
+        tv = A.TVLossFn.apply(y, self.tv)
+        w = self.world
+        return (self.sw / w) * losses[:5].sum() + (self.cw / w) * losses[5] + tv
+
+    def step(self, batch: torch.Tensor) -> torch.Tensor:
+        batch = batch.to(self.device, torch.float32).contiguous()
+        self.flat_grad.zero_()
+        y = self.itn(batch)
+        total = self._total(batch, y)
+        total.backward()
+        if self.world > 1:
+            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
+        self.opt.step()
+        return total.detach()
+
+    @torch.no_grad()
+    def evaluate(self, batch: torch.Tensor) -> torch.Tensor:
+        batch = batch.to(self.device, torch.float32).contiguous()
+        return self._total(batch, self.itn(batch))

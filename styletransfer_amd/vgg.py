@@ -1,0 +1,280 @@
+"""VGG-19 loss network on libstx: the fused forward/backward of the StyleNetwork
+losses (Gatys hot loop and the fast_st loss network).
+
+Reference semantics (stransfer/network.py:204-401): the VGG-19 `.features`
+stack is sliced into pieces at the loss taps
+
+    [conv1_1] [relu, conv1_2] [relu, pool, conv2_1] [relu, conv2_2] [relu] [pool, conv3_1]
+
+with StyleLoss on the outputs of Conv2d_1..Conv2d_5 (pre-ReLU), ContentLoss on
+Conv2d_4 (pre-ReLU) and FeatureReconstructionLoss on ReLU_4.  The reference
+re-runs the prefix from the image for every loss (7x for the input, 2x for the
+content image) and also computes VGG weight gradients; both are redundant work,
+so this engine runs each layer once:
+
+  forward   Z1 = conv1_1(x)            Z2 = conv1_2(relu Z1)
+            Z3 = conv2_1(pool relu Z2) Z4 = conv2_2(relu Z3)   Z5 = conv3_1(pool relu Z4)
+            (ReLU and ReLU+MaxPool are fused into the next conv's LDS halo load)
+            style_l = mean((gram(Z_l) - T_l)^2)   content = mse(Z4, C4)
+            feature = mse(relu Z4, relu C4)^2 / numel(Z4)
+  backward  dZ5 = g_s5 A5 Z5 ; dP2 = conv3_1ᵀ(dZ5) ; dZ4 = unpool(dP2)·[Z4>0] + g_s4 A4 Z4
+            + content/feature terms ; dZ3 = conv2_2ᵀ(dZ4)·[Z3>0] + g_s3 A3 Z3 ; ...
+            dx = conv1_1ᵀ(dZ1)
+where g is the vector of upstream gradients of the 7 losses (device tensor),
+so the same code serves `total.backward()` for any loss combination.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import ops
+from . import weights as W
+
+# tap layout of the reference StyleNetwork (stransfer/network.py:214-232)
+STYLE_CONVS = (0, 1, 2, 3, 4)   # Conv2d_1..Conv2d_5
+CONTENT_CONV = 3                # Conv2d_4
+N_LOSSES = 7                    # style x5, content, feature
+VGG_CONV_SHAPES = [(64, 3), (64, 64), (128, 64), (128, 128), (256, 128)]
+# how each conv's input is formed from the previous conv's output
+IN_MODES = [N.STX_IN_RAW, N.STX_IN_RELU, N.STX_IN_RELU_POOL2, N.STX_IN_RELU,
+            N.STX_IN_RELU_POOL2]
+
+
+def load_vgg19_weights(path: str | None = None, seed: int = 1234):
+    """The first five VGG-19 convs as [(w, b)] numpy arrays.
+
+    `torchvision.models.vgg19(pretrained=True)` (stransfer/network.py:246) needs a
+    download.  A local torchvision state_dict (keys `features.{0,2,5,7,10}.*` or
+    `{0,2,5,7,10}.*`) is used when `path` or $STX_VGG19_WEIGHTS names one (loaded
+    with weights_only=True); otherwise deterministic synthetic weights."""
+    path = path or os.environ.get("STX_VGG19_WEIGHTS")
+    if path and os.path.exists(path):
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        out = []
+        for idx in (0, 2, 5, 7, 10):
+            for pre in ("features.", ""):
+                if f"{pre}{idx}.weight" in sd:
+                    out.append((sd[f"{pre}{idx}.weight"].float().numpy(),
+                                sd[f"{pre}{idx}.bias"].float().numpy()))
+                    break
+            else:
+                raise KeyError(f"VGG-19 weights file {path} lacks conv index {idx}")
+        return out
+    return W.vgg19_synthetic(seed, 5)
+
+
+class VGGFeatures:
+    """Frozen conv1_1..conv3_1 with prepped forward and data-gradient slabs."""
+
+    def __init__(self, convs, device):
+        self.device = torch.device(device)
+        self.w, self.b, self.wt, self.wtT = [], [], [], []
+        for (w, b), (cout, cin) in zip(convs, VGG_CONV_SHAPES):
+            wt = torch.as_tensor(np.ascontiguousarray(w), dtype=torch.float32).to(self.device)
+            bt = torch.as_tensor(np.ascontiguousarray(b), dtype=torch.float32).to(self.device)
+            assert tuple(wt.shape) == (cout, cin, 3, 3), wt.shape
+            self.w.append(wt)
+            self.b.append(bt)
+            self.wt.append(ops.conv_weight_prep(wt))
+            self.wtT.append(ops.conv_weight_prep(wt, transpose=True))
+
+    @classmethod
+    def from_modules(cls, convs, device):
+        """From five nn.Conv2d modules (the layers of a StyleNetwork)."""
+        return cls([(c.weight.detach().cpu().numpy(), c.bias.detach().cpu().numpy())
+                    for c in convs], device)
+
+    def conv(self, l, x, out=None):
+        cout, cin = VGG_CONV_SHAPES[l]
+        return ops.conv2d(x, self.wt[l], cin, cout, 3, in_mode=IN_MODES[l], bias=self.b[l],
+                          out=out)
+
+    def forward(self, x, upto=5, outs=None):
+        """[Z1..Z_upto] (pre-ReLU conv outputs)."""
+        zs, cur = [], x
+        for l in range(upto):
+            cur = self.conv(l, cur, None if outs is None else outs[l])
+            zs.append(cur)
+        return zs
+
+    def style_targets(self, style_image):
+        """T_l = gram(Z_l(style)) [C][C] (StyleLoss.set_target, :125-131)."""
+        zs = self.forward(style_image.contiguous())
+        return [ops.gram(z) for z in zs]
+
+
+@dataclass
+class LossState:
+    """Activations + scratch of one loss evaluation (kept for the backward)."""
+    z: list = field(default_factory=list)       # Z1..Z5
+    coef: list = field(default_factory=list)    # A_l per style layer
+    c4: torch.Tensor = None                     # content target (pre-ReLU conv2_2)
+    losses: torch.Tensor = None                 # [7] style x5, content, feature
+    fmean: torch.Tensor = None                  # [2] feature loss, its mse
+
+
+def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
+                 style_weight_in_coef=1.0):
+    """Forward of all 7 losses for input batch x [B,3,H,W] given style targets and
+    the content target c4 (= Z4 of the content image, pre-ReLU)."""
+    if st is None:
+        st = LossState()
+    st.z = feat.forward(x, 5, st.z if st.z else None)
+    if st.losses is None:
+        # [style x5, content, feature, feature-mse]
+        st.losses = torch.empty(N_LOSSES + 1, device=x.device, dtype=torch.float32)
+        st.fmean = st.losses[6:8]
+    if not st.coef:
+        st.coef = [None] * 5
+    for i, l in enumerate(STYLE_CONVS):
+        _, st.coef[i] = ops.style_loss(st.z[l], targets[i], weight=style_weight_in_coef,
+                                       loss=st.losses[i], coef=st.coef[i])
+    z4 = st.z[CONTENT_CONV]
+    assert c4.shape == z4.shape, (c4.shape, z4.shape)
+    st.c4 = c4
+    ops.mse(z4, c4, out=st.losses[5:6])
+    ops.mse(z4, c4, relu=True, mode=1, out=st.fmean)
+    return st
+
+
+def loss_values(st: LossState):
+    """[style1..5, content, feature] (a view of the device loss vector)."""
+    return st.losses[:N_LOSSES]
+
+
+def loss_backward(feat: VGGFeatures, st: LossState, g, dx=None, feature_grad=True,
+                  scratch=None):
+    """dx = sum_i g[i] * d loss_i / dx.  g: device [7] (style x5, content, feature)."""
+    z = st.z
+    B = z[0].shape[0]
+    sc = scratch if scratch is not None else {}
+
+    def buf(name, like_shape):
+        t = sc.get(name)
+        if t is None or tuple(t.shape) != tuple(like_shape):
+            t = torch.empty(like_shape, device=z[0].device, dtype=torch.float32)
+            sc[name] = t
+        return t
+
+    # conv3_1 output
+    dz5 = ops.gram_bwd(st.coef[4], z[4], buf("dz5", z[4].shape), acc_scale=g[4:5])
+    # dgrad conv3_1 -> grad wrt pool(relu Z4)
+    n4 = (B, 128, z[3].shape[2] // 2, z[3].shape[3] // 2)
+    dp2 = ops.conv2d(dz5, feat.wtT[4], 256, 128, 3, out=buf("dp2", n4))
+    dz4 = ops.relupool_bwd(dp2, z[3], out=buf("dz4", z[3].shape))
+    ops.gram_bwd(st.coef[3], z[3], dz4, acc_scale=g[3:4], accumulate=True)
+    n = z[3].numel()
+    ops.diff_scale(z[3], st.c4, 2.0 / n, s1=g[5:6], out=dz4, accumulate=True)
+    if feature_grad:
+        ops.diff_scale(z[3], st.c4, 4.0 / (float(n) * float(n)), s1=g[6:7], s2=st.fmean[1:2],
+                       relu=True, out=dz4, accumulate=True)
+    # conv2_2 dgrad, relu mask of Z3, + style3
+    dz3 = ops.conv2d(dz4, feat.wtT[3], 128, 128, 3, mask=z[2], out=buf("dz3", z[2].shape))
+    ops.gram_bwd(st.coef[2], z[2], dz3, acc_scale=g[2:3], accumulate=True)
+    # conv2_1 dgrad -> grad wrt pool(relu Z2)
+    n2 = (B, 64, z[1].shape[2] // 2, z[1].shape[3] // 2)
+    dp1 = ops.conv2d(dz3, feat.wtT[2], 128, 64, 3, out=buf("dp1", n2))
+    dz2 = ops.relupool_bwd(dp1, z[1], out=buf("dz2", z[1].shape))
+    ops.gram_bwd(st.coef[1], z[1], dz2, acc_scale=g[1:2], accumulate=True)
+    # conv1_2 dgrad, relu mask of Z1, + style1
+    dz1 = ops.conv2d(dz2, feat.wtT[1], 64, 64, 3, mask=z[0], out=buf("dz1", z[0].shape))
+    ops.gram_bwd(st.coef[0], z[0], dz1, acc_scale=g[0:1], accumulate=True)
+    # conv1_1 dgrad -> image
+    xs = (B, 3, z[0].shape[2], z[0].shape[3])
+    if dx is None:
+        dx = torch.empty(xs, device=z[0].device, dtype=torch.float32)
+    return ops.conv2d(dz1, feat.wtT[0], 64, 3, 3, out=dx)
+
+
+def content_target(feat: VGGFeatures, content, out=None):
+    """C4 = conv2_2 output of the content image (ContentLoss target, pre-ReLU)."""
+    return feat.forward(content.contiguous(), 4)[3] if out is None else \
+        feat.forward(content.contiguous(), 4, [None, None, None, out])[3]
+
+
+class GatysEngine:
+    """One Gatys iteration = forward + backward + Adam on the image, as a single
+    hipGraph replay (BASELINE.json config 2):
+
+        opt.zero_grad(); net(x, content)
+        (style_weight*sum(style) + content_weight*content).backward(); opt.step()
+
+    All buffers are static so the iteration can be captured once and replayed.
+    """
+
+    def __init__(self, feat: VGGFeatures, style_image, content_image, style_weight=100_000,
+                 content_weight=1, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, init=None,
+                 targets=None):
+        dev = feat.device
+        self.feat = feat
+        if targets is None:
+            targets = feat.style_targets(style_image.to(dev, torch.float32))
+        self.targets = [t.reshape(t.shape[-2:]).contiguous() for t in targets]
+        self.content = content_image.to(dev, torch.float32).contiguous()
+        self.c4 = content_target(feat, self.content).clone()
+        src = self.content if init is None else init.to(dev, torch.float32)
+        self.x = src.clone().contiguous()
+        self.grad = torch.zeros_like(self.x)
+        self.m = torch.zeros_like(self.x)
+        self.v = torch.zeros_like(self.x)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.adam_ws = torch.zeros(16, dtype=torch.float32, device=dev)
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.sw, self.cw = float(style_weight), float(content_weight)
+        self.g = torch.tensor([self.sw] * 5 + [self.cw, 0.0], device=dev, dtype=torch.float32)
+        self.total = torch.zeros((), device=dev, dtype=torch.float32)
+        self.st = LossState()
+        self.scratch = {}
+        self.graph = None
+
+    def _iteration(self):
+        loss_forward(self.feat, self.targets, self.x, self.c4, self.st)
+        ops.loss_combine(self.st.losses, [self.sw] * 5 + [self.cw], self.total)
+        loss_backward(self.feat, self.st, self.g, dx=self.grad, feature_grad=False,
+                      scratch=self.scratch)
+        ops.adam_step(self.x, self.grad, self.m, self.v, self.step_dev, self.adam_ws, self.lr,
+                      self.betas[0], self.betas[1], self.eps)
+
+    def capture(self, warmup=2):
+        """Capture one iteration into a hipGraph (after `warmup` eager iterations,
+        which also allocate every buffer)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._iteration()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._iteration()
+        return self
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._iteration()
+        return self.total
+
+    def run(self, steps, graph=True):
+        """`steps` iterations; with graph=True the first one runs eagerly (it
+        allocates every buffer) and the rest replay a captured hipGraph."""
+        if steps <= 0:
+            return self.x
+        if not graph:
+            for _ in range(steps):
+                self._iteration()
+            return self.x
+        self.capture(warmup=1)
+        for _ in range(steps - 1):
+            self.graph.replay()
+        return self.x
+
+    def losses(self):
+        """[style x5, content, feature] of the last forward (device tensor)."""
+        return loss_values(self.st)
