@@ -103,7 +103,10 @@ gram_partial_kernel(const float* __restrict__ z, float* __restrict__ ws, int c, 
   }
 }
 
-// grid (ntu, B); 256 threads, 16 elements per thread
+// grid (ntu * 16, B); one thread per tile element (256 elements per block).  The
+// split partials are summed in a fixed order (bit-reproducible); loads are
+// independent and unrolled so a block streams its slab column at full rate.
+constexpr int FSUB = GT * GT / 256;
 __global__ void __launch_bounds__(256)
 gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scale,
                      float* __restrict__ g_out, const float* __restrict__ target, long long t_bstride,
@@ -111,16 +114,26 @@ gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scal
                      float* __restrict__ loss_parts) {
   __shared__ float red[4];
   const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
+  const int tile = blockIdx.x / FSUB, sub = blockIdx.x % FSUB;
   int I, J;
-  tile_ij(blockIdx.x, nt, I, J);
+  tile_ij(tile, nt, I, J);
   const int b = blockIdx.y;
-  const float* src = ws + ((size_t)b * ntu + blockIdx.x) * nsplit * (GT * GT);
+  const float* src = ws + ((size_t)b * ntu + tile) * nsplit * (GT * GT);
   float sq = 0.f;
-  for (int e = threadIdx.x; e < GT * GT; e += 256) {
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += src[(size_t)k * GT * GT + e];
+  {
+    const int e = sub * 256 + threadIdx.x;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int k = 0;
+    for (; k + 4 <= nsplit; k += 4) {
+      s0 += src[(size_t)(k + 0) * GT * GT + e];
+      s1 += src[(size_t)(k + 1) * GT * GT + e];
+      s2 += src[(size_t)(k + 2) * GT * GT + e];
+      s3 += src[(size_t)(k + 3) * GT * GT + e];
+    }
+    for (; k < nsplit; ++k) s0 += src[(size_t)k * GT * GT + e];
+    const float s = (s0 + s1) + (s2 + s3);
     const int gi = I * GT + e / GT, gj = J * GT + e % GT;
-    if (gi >= c || gj >= c) continue;
+    if (gi < c && gj < c) {
     const float g = s * scale;
     if (g_out) {
       g_out[((size_t)b * c + gi) * c + gj] = g;
@@ -136,10 +149,11 @@ gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scal
         if (I != J) cb[(size_t)gj * cpad + gi] = a;
       }
     }
+    }
   }
   if (target) {
     const float t = block_sum<256>(sq, red);
-    if (threadIdx.x == 0) loss_parts[b * ntu + blockIdx.x] = t;
+    if (threadIdx.x == 0) loss_parts[(size_t)b * ntu * FSUB + blockIdx.x] = t;
   }
 }
 
@@ -163,9 +177,9 @@ static void gram_geometry(int c, int hw, int b, int& nsplit, int& split_len, int
   const int nt = cdiv(c, GT);
   ntu = nt * (nt + 1) / 2;
   const int chunks = cdiv(hw, GKC);
-  // aim for ~1024 blocks in flight, at least 4 chunks per split
-  int want = cdiv(1024, ntu * b);
-  want = std::max(1, std::min(want, cdiv(chunks, 4)));
+  // aim for ~512 blocks (2 per CU), at least 8 chunks (512 pixels) per split
+  int want = cdiv(512, ntu * b);
+  want = std::max(1, std::min(want, cdiv(chunks, 8)));
   const int per = cdiv(chunks, want);
   split_len = per * GKC;
   nsplit = cdiv(hw, split_len);
@@ -175,7 +189,7 @@ static size_t gram_ws_bytes(int b, int c, int hw) {
   int nsplit, split_len, ntu;
   gram_geometry(c, hw, b, nsplit, split_len, ntu);
   // partial slabs + loss parts
-  return ((size_t)b * ntu * nsplit * GT * GT + (size_t)b * ntu + 64) * sizeof(float);
+  return ((size_t)b * ntu * nsplit * GT * GT + (size_t)b * ntu * FSUB + 64) * sizeof(float);
 }
 
 static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_out,
@@ -197,11 +211,11 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
   hipLaunchKernelGGL(gram_partial_kernel, dim3(nsplit, ntu, b), dim3(256), 0, st, z, slabs, c,
                      hw, nsplit, split_len);
   const int cpad = stx_gram_coef_pitch(c);
-  hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu, b), dim3(256), 0, st, slabs, c, nsplit,
-                     scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts);
+  hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(256), 0, st, slabs, c,
+                     nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts);
   if (target && loss)
-    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, st, parts, b * ntu, loss_inv,
-                       loss);
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, st, parts, b * ntu * FSUB,
+                       loss_inv, loss);
   return check_launch("gram");
 }
 
