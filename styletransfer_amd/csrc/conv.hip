@@ -74,10 +74,38 @@ struct ConvCfg {
   static_assert(NPIX % TW == 0, "tile");
 };
 
+// Halo element i of this thread (idx = tid + i*256) always maps to the same
+// (ci_local, r, c) and, for a given block, to the same source offset within the
+// input-channel plane; only the channel base moves from chunk to chunk.  So the
+// per-element offsets and the in-bounds mask are computed once per block and the
+// per-chunk fetch is one (or, for the fused 2x2 pool, four) loads per element.
+template <int MODE, int NH, int HALO, int RHW>
+__device__ __forceinline__ void halo_fetch(float (&hreg)[NH], const float* __restrict__ src,
+                                           const int (&hoff)[NH], uint64_t hvalid, int w,
+                                           int ci_lim, int tid) {
+#pragma unroll
+  for (int i = 0; i < NH; ++i) {
+    bool ok = (hvalid >> i) & 1;
+    if (ci_lim < 0x7fffffff) ok = ok && ((tid + i * 256) / RHW) < ci_lim;
+    float v = 0.f;
+    if (ok) {
+      const float* q = src + hoff[i];
+      if (MODE == STX_IN_RELU_POOL2) {
+        v = fmaxf(fmaxf(fmaxf(q[0], q[1]), fmaxf(q[w], q[w + 1])), 0.f);
+      } else {
+        v = q[0];
+        if (MODE == STX_IN_RELU) v = fmaxf(v, 0.f);
+      }
+    }
+    hreg[i] = v;
+  }
+}
+
 template <int KS, int S, int CIS, int BM, int TW>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 2)
 conv_fwd_kernel(stx_conv_params p, int tiles_x) {
   using C = ConvCfg<KS, S, CIS, BM, TW>;
+  static_assert(C::RWP == C::RW, "halo LDS index == element index");
   __shared__ __attribute__((aligned(16))) float smem[C::LDS_FLOATS];
   float* lds_in = smem;
   float* lds_w = smem + C::LDS_IN;
@@ -96,6 +124,35 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
   const float* __restrict__ wt = p.wt + (size_t)n * p.wt_batch_stride;
   const int vy0 = ty0 * S - p.pad, vx0 = tx0 * S - p.pad;
   const int mode = p.in_mode;
+  const int plane_in = p.h * p.w;
+
+  // chunk-invariant halo source offsets + validity
+  int hoff[C::NH];
+  uint64_t hvalid = 0;
+#pragma unroll
+  for (int i = 0; i < C::NH; ++i) {
+    const int idx = tid + i * 256;
+    const int ci = idx / (C::RH * C::RW);
+    const int rem = idx - ci * (C::RH * C::RW);
+    const int r = rem / C::RW, c = rem - r * C::RW;
+    const int vy = vy0 + r, vx = vx0 + c;
+    bool ok = idx < C::HALO && vy >= 0 && vx >= 0 && vy < p.hv && vx < p.wv;
+    int sy = vy, sx = vx;
+    if (mode == STX_IN_RELU_POOL2) {
+      sy = 2 * vy;
+      sx = 2 * vx;
+    } else if (mode == STX_IN_UPSAMPLE2) {
+      sy = vy >> 1;
+      sx = vx >> 1;
+    } else if (mode == STX_IN_DILATE2) {
+      ok = ok && !((vy | vx) & 1);
+      sy = vy >> 1;
+      sx = vx >> 1;
+      ok = ok && sy < p.h && sx < p.w;
+    }
+    hoff[i] = ok ? ci * plane_in + sy * p.w + sx : 0;
+    if (ok) hvalid |= (uint64_t)1 << i;
+  }
 
   f32x16 acc[C::MI][C::NI];
 #pragma unroll
@@ -121,18 +178,16 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
 
   auto fetch = [&](int chunk) {
     const int c0 = chunk * CIS;
-#pragma unroll
-    for (int i = 0; i < C::NH; ++i) {
-      const int idx = tid + i * 256;
-      float v = 0.f;
-      if (idx < C::HALO) {
-        const int ci = idx / (C::RH * C::RW);
-        const int rem = idx - ci * (C::RH * C::RW);
-        const int r = rem / C::RW, c = rem - r * C::RW;
-        v = load_virtual(xn, mode, p.cin, p.h, p.w, p.hv, p.wv, c0 + ci, vy0 + r, vx0 + c);
-      }
-      hreg[i] = v;
-    }
+    const float* src = xn + (size_t)c0 * plane_in;
+    const int ci_lim = (c0 + CIS <= p.cin) ? 0x7fffffff : p.cin - c0;
+    constexpr int RHW = C::RH * C::RW;
+    if (mode == STX_IN_RELU_POOL2)
+      halo_fetch<STX_IN_RELU_POOL2, C::NH, C::HALO, RHW>(hreg, src, hoff, hvalid, p.w, ci_lim,
+                                                          tid);
+    else if (mode == STX_IN_RELU)
+      halo_fetch<STX_IN_RELU, C::NH, C::HALO, RHW>(hreg, src, hoff, hvalid, p.w, ci_lim, tid);
+    else
+      halo_fetch<STX_IN_RAW, C::NH, C::HALO, RHW>(hreg, src, hoff, hvalid, p.w, ci_lim, tid);
     const float* wsrc = wt + (size_t)c0 * C::KK * p.cout_pad + co0;
 #pragma unroll
     for (int i = 0; i < C::NW; ++i) {
@@ -147,12 +202,7 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
 #pragma unroll
     for (int i = 0; i < C::NH; ++i) {
       const int idx = tid + i * 256;
-      if (idx < C::HALO) {
-        const int ci = idx / (C::RH * C::RW);
-        const int rem = idx - ci * (C::RH * C::RW);
-        const int r = rem / C::RW, c = rem - r * C::RW;
-        lds_in[ci * C::CH + r * C::RWP + c] = hreg[i];
-      }
+      if (idx < C::HALO) lds_in[idx] = hreg[i];
     }
 #pragma unroll
     for (int i = 0; i < C::NW; ++i) {

@@ -1,0 +1,77 @@
+"""Microbenchmark of the libstx conv / gram kernels at the hot-path shapes (HIP
+events on the launch stream).  Prints TFLOP/s per shape (algorithmic 2*MAC)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from styletransfer_amd import _native as N  # noqa: E402
+from styletransfer_amd import ops  # noqa: E402
+
+
+def ev(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    cases = [
+        # name, n, cin, cout, h, w, ks, stride, mode, transpose(dgrad)
+        ("vgg conv1_1 fwd 512", 1, 3, 64, 512, 512, 3, 1, N.STX_IN_RAW),
+        ("vgg conv1_2 fwd 512", 1, 64, 64, 512, 512, 3, 1, N.STX_IN_RELU),
+        ("vgg conv2_1 fwd 512", 1, 64, 128, 512, 512, 3, 1, N.STX_IN_RELU_POOL2),
+        ("vgg conv2_2 fwd 256", 1, 128, 128, 256, 256, 3, 1, N.STX_IN_RELU),
+        ("vgg conv3_1 fwd 256", 1, 128, 256, 256, 256, 3, 1, N.STX_IN_RELU_POOL2),
+        ("vgg dgrad1_1 (64->3) 512", 1, 64, 3, 512, 512, 3, 1, N.STX_IN_RAW),
+        ("itn res conv B8 64^2", 8, 128, 128, 64, 64, 3, 1, N.STX_IN_RAW),
+        ("itn conv0 9x9 B8 256", 8, 3, 32, 256, 256, 9, 1, N.STX_IN_RAW),
+        ("itn conv22 9x9 B8 256", 8, 32, 3, 256, 256, 9, 1, N.STX_IN_RAW),
+        ("itn up conv B8 128->64 @128", 8, 128, 64, 64, 64, 3, 1, N.STX_IN_UPSAMPLE2),
+        ("itn down s2 B8 32->64", 8, 32, 64, 256, 256, 3, 2, N.STX_IN_RAW),
+    ]
+    for name, n, cin, cout, h, w, ks, s, mode in cases:
+        x = torch.randn(n, cin, h, w, generator=g).to(dev)
+        wt = ops.conv_weight_prep(torch.randn(cout, cin, ks, ks, generator=g).to(dev) * 0.05)
+        hv, wv = ops.virtual_hw(h, w, mode)
+        ho, wo = ops.conv_out_hw(hv, wv, ks, s, ks // 2)
+        out = torch.empty(n, cout, ho, wo, device=dev)
+        ms = ev(lambda: ops.conv2d(x, wt, cin, cout, ks, stride=s, in_mode=mode, out=out))
+        gf = 2.0 * n * cin * cout * ks * ks * ho * wo / 1e9
+        print(f"{name:32s} {ms * 1e3:9.1f} us  {gf / ms:8.2f} TFLOP/s")
+    for name, n, c, h in (("gram C64 512^2", 1, 64, 512), ("gram C128 256^2", 1, 128, 256),
+                          ("gram C256 128^2", 1, 256, 128), ("gram C64 B8 256^2", 8, 64, 256)):
+        z = torch.randn(n, c, h, h, generator=g).to(dev)
+        t = torch.randn(c, c, generator=g).to(dev)
+        coef = None
+        ms = ev(lambda: ops.style_loss(z, t))
+        _, coef = ops.style_loss(z, t)
+        dz = torch.empty_like(z)
+        ms2 = ev(lambda: ops.gram_bwd(coef, z, dz, accumulate=True))
+        gf = 2.0 * n * c * c * h * h / 1e9
+        print(f"{name:32s} fwd {ms * 1e3:8.1f} us {gf / ms:7.2f} TF | bwd {ms2 * 1e3:8.1f} us "
+              f"{gf / ms2:7.2f} TF")
+    # wgrad
+    for name, n, cin, cout, h, ks, s in (("wgrad res B8 128 64^2", 8, 128, 128, 64, 3, 1),
+                                         ("wgrad conv0 9x9 B8", 8, 3, 32, 256, 9, 1),
+                                         ("wgrad conv22 9x9 B8", 8, 32, 3, 256, 9, 1)):
+        x = torch.randn(n, cin, h, h, generator=g).to(dev)
+        ho = (h + 2 * (ks // 2) - ks) // s + 1
+        dy = torch.randn(n, cout, ho, ho, generator=g).to(dev)
+        ms = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s), reps=10)
+        gf = 2.0 * n * cin * cout * ks * ks * ho * ho / 1e9
+        print(f"{name:32s} {ms * 1e3:9.1f} us  {gf / ms:8.2f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()
