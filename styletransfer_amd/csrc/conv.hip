@@ -261,6 +261,153 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
   }
 }
 
+// ------------------------------------------------------- small-cout direct conv
+// cout <= 4, stride 1 (VGG conv1_1 data-gradient 64->3, ImageTransformNet's final
+// 9x9 conv 32->3).  An MFMA tile would be >= 90% padding here, so this is a VALU
+// direct convolution: thread = 4 consecutive output pixels x all output channels,
+// block = 16 x 64 output pixels; the input halo of CIS channels is staged in LDS
+// (row pitch padded to 16 B for ds_read_b128); weights are read from the standard
+// prepped slab at wave-uniform addresses (scalar loads), so every FMA takes one
+// LDS value that is re-used KS times across kw and COUT times across channels.
+constexpr int SC_TW = 64, SC_PX = 4;
+
+template <int KS, int CIS, int TH>
+struct SmallCfg {
+  static constexpr int NT = 16 * TH;                   // threads: 16 per output row
+  static constexpr int RH = TH + KS - 1;
+  static constexpr int RW = SC_TW + KS - 1;
+  static constexpr int RWP = (RW + 3) / 4 * 4;
+  static constexpr int CH = RH * RWP;
+  static constexpr int PL = RH * RW;                   // halo elements per channel plane
+  static constexpr int NE = (PL + NT - 1) / NT;
+  static constexpr int NV = (SC_PX + KS - 1 + 3) / 4;  // float4 reads per row
+};
+
+template <int KS, int CIS, int TH>
+__global__ void __launch_bounds__(16 * TH)
+conv_smallc_kernel(stx_conv_params p, int tiles_x) {
+  using C = SmallCfg<KS, CIS, TH>;
+  constexpr int COUT = 4;
+  __shared__ __attribute__((aligned(16))) float halo[CIS * C::CH];
+  __shared__ __attribute__((aligned(16))) f32x4 wts[CIS * KS * KS];  // [ci][tap] -> 4 couts
+  const int tid = threadIdx.x;
+  const int ty = tid / 16, tx = tid % 16;
+  const int tile = blockIdx.x, n = blockIdx.z;
+  const int oy0 = (tile / tiles_x) * TH, ox0 = (tile % tiles_x) * SC_TW;
+  const int vy0 = oy0 - p.pad, vx0 = ox0 - p.pad;
+  const float* __restrict__ xn = p.x + (size_t)n * p.cin * p.h * p.w;
+  const float* __restrict__ wt = p.wt + (size_t)n * p.wt_batch_stride;
+  const int plane_in = p.h * p.w;
+  const int KK = KS * KS;
+  const bool relu_in = p.in_mode == STX_IN_RELU;
+
+  // plane-invariant halo offsets (source and LDS) of this thread's elements
+  int eoff[C::NE], loff[C::NE];
+  uint32_t evalid = 0;
+#pragma unroll
+  for (int e = 0; e < C::NE; ++e) {
+    const int idx = tid + e * C::NT;
+    const int r = idx / C::RW, c = idx - (idx / C::RW) * C::RW;
+    const int vy = vy0 + r, vx = vx0 + c;
+    const bool in_tile = idx < C::PL;
+    const bool ok = in_tile && vy >= 0 && vx >= 0 && vy < p.hv && vx < p.wv;
+    eoff[e] = ok ? vy * p.w + vx : 0;
+    loff[e] = in_tile ? r * C::RWP + c : -1;
+    if (ok) evalid |= 1u << e;
+  }
+
+  float acc[COUT][SC_PX];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c)
+#pragma unroll
+    for (int q = 0; q < SC_PX; ++q) acc[c][q] = 0.f;
+
+  for (int c0 = 0; c0 < p.cin; c0 += CIS) {
+    const int cn = min(CIS, p.cin - c0);
+    float hv[CIS][C::NE];
+#pragma unroll
+    for (int cil = 0; cil < CIS; ++cil) {  // all loads of the chunk in flight together
+      const float* src = xn + (size_t)(c0 + cil) * plane_in;
+#pragma unroll
+      for (int e = 0; e < C::NE; ++e) {
+        float v = 0.f;
+        if (cil < cn && ((evalid >> e) & 1)) {
+          v = src[eoff[e]];
+          if (relu_in) v = fmaxf(v, 0.f);
+        }
+        hv[cil][e] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cil = 0; cil < CIS; ++cil)
+#pragma unroll
+      for (int e = 0; e < C::NE; ++e)
+        if (loff[e] >= 0) halo[cil * C::CH + loff[e]] = hv[cil][e];
+    for (int i = tid; i < CIS * KK; i += C::NT) {
+      const int cil = i / KK;
+      const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+      wts[i] = cil < cn ? *reinterpret_cast<const f32x4*>(
+                              wt + (size_t)((c0 + cil) * KK + (i - cil * KK)) * p.cout_pad)
+                        : zero;
+    }
+    __syncthreads();
+    for (int cil = 0; cil < cn; ++cil) {
+      const f32x4* wk = wts + cil * KK;
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh) {
+        float in[C::NV * 4];
+        const float* row = halo + cil * C::CH + (ty + kh) * C::RWP + tx * SC_PX;
+#pragma unroll
+        for (int v = 0; v < C::NV; ++v) {
+          const f32x4 t = *reinterpret_cast<const f32x4*>(row + 4 * v);
+          in[4 * v + 0] = t[0];
+          in[4 * v + 1] = t[1];
+          in[4 * v + 2] = t[2];
+          in[4 * v + 3] = t[3];
+        }
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          const f32x4 w4 = wk[kh * KS + kw];  // LDS broadcast (same address in all lanes)
+#pragma unroll
+          for (int c = 0; c < COUT; ++c)
+#pragma unroll
+            for (int q = 0; q < SC_PX; ++q) acc[c][q] = fmaf(w4[c], in[q + kw], acc[c][q]);
+        }
+      }
+    }
+  }
+  const int oy = oy0 + ty;
+  if (oy >= p.ho) return;
+  const size_t plane = (size_t)p.ho * p.wo;
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) {
+    if (c >= p.cout) break;
+#pragma unroll
+    for (int q = 0; q < SC_PX; ++q) {
+      const int ox = ox0 + tx * SC_PX + q;
+      if (ox >= p.wo) continue;
+      const size_t o = ((size_t)n * p.cout + c) * plane + (size_t)oy * p.wo + ox;
+      float v = acc[c][q];
+      if (p.acc_scale) v *= *p.acc_scale;
+      if (p.bias) v += p.bias[c];
+      if (p.mask) v = p.mask[o] > 0.f ? v : 0.f;
+      if (p.aux) v += p.aux_scale * p.aux[o];
+      if (p.accumulate) v += p.y[o];
+      if (p.relu_out) v = fmaxf(v, 0.f);
+      p.y[o] = v;
+    }
+  }
+}
+
+template <int KS, int TH>
+static int launch_smallc(const stx_conv_params& p, hipStream_t st) {
+  const int tiles_x = cdiv(p.wo, SC_TW), tiles_y = cdiv(p.ho, TH);
+  dim3 grid(tiles_x * tiles_y, 1, p.n);
+  hipLaunchKernelGGL((conv_smallc_kernel<KS, 8, TH>), grid, dim3(16 * TH), 0, st, p, tiles_x);
+  return check_launch("stx_conv2d(smallc)");
+}
+
 // ---------------------------------------------------------------- weight prep
 __global__ void weight_prep_kernel(const float* __restrict__ w, float* __restrict__ wt, int cout,
                                    int cin, int ks, int transpose, int rows_pad, int cols_pad) {
@@ -363,6 +510,12 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   if (p.in_mode <= STX_IN_RELU && (p.hv != p.h || p.wv != p.w)) {
     set_error("stx_conv2d: raw dims");
     return STX_E_INVALID;
+  }
+  if (p.cout <= 4 && p.stride == 1 && (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) &&
+      (p.ks == 3 || p.ks == 9)) {
+    const long long blocks16 = (long long)cdiv(p.wo, SC_TW) * cdiv(p.ho, 16) * p.n;
+    if (p.ks == 3) return blocks16 >= 512 ? launch_smallc<3, 16>(p, st) : launch_smallc<3, 8>(p, st);
+    return blocks16 >= 512 ? launch_smallc<9, 16>(p, st) : launch_smallc<9, 8>(p, st);
   }
   const bool big = p.cout > 64;
   if (p.ks == 3 && p.stride == 1)

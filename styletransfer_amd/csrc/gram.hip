@@ -103,6 +103,140 @@ gram_partial_kernel(const float* __restrict__ z, float* __restrict__ ws, int c, 
   }
 }
 
+// Register-direct Gram partial (hw % 4 == 0).  No LDS staging of F: lane
+// (r = l&31, h = l>>5) of a wave streams 16 consecutive pixels of its own rows
+// (float4 x4 per row: lanes l and l+32 cover one full 128-B line) and feeds them
+// straight to v_mfma_f32_32x32x2_f32 — the k index of step t for lane half h is
+// pixel p0 + 16h + t, identical for the A (rows I) and B (rows J) operands.
+// Each wave owns a full 64x64 tile over its own 32-pixel steps (waves interleave
+// steps); diagonal tiles (I == J) load each row once and skip the mirrored
+// quadrant.  Blocks of one split run all of its tiles on one XCD (blocks b and
+// b+8 share an XCD under round-robin dispatch) so the row tiles re-read by
+// several tiles come from that XCD's L2 (speed only).  The 4 wave partials are
+// summed through LDS into one deterministic slab per (block, tile).
+// index of tile (I, J), I <= J, in the row-major upper-triangle enumeration
+__device__ __forceinline__ int tile_index(int I, int J, int nt) {
+  return I * nt - I * (I - 1) / 2 + (J - I);
+}
+
+// DIAG: one launch over the diagonal tiles (each row tile loaded once, 3 of the 4
+// quadrants computed: fits 4 waves/SIMD); !DIAG: the off-diagonal tiles.
+template <bool DIAG>
+__global__ void __launch_bounds__(256, DIAG ? 4 : 2)
+gram_partial_v2_kernel(const float* __restrict__ z, float* __restrict__ ws, int c, int hw,
+                       int nsplit, int split_len) {
+  __shared__ __attribute__((aligned(16))) float red[2 * GT * GT];
+  const int nt = cdiv(c, GT);
+  const int ntu = nt * (nt + 1) / 2;
+  const int nk = DIAG ? nt : ntu - nt;  // tiles of this launch
+  const int L = blockIdx.x;
+  const int xcd = L & 7, rest = L >> 3;
+  const int k = rest % nk, split = (rest / nk) * 8 + xcd;
+  int I, J;
+  if (DIAG) {
+    I = J = k;
+  } else {  // k-th pair I < J, row-major
+    int i = 0, t = k;
+    while (t >= nt - 1 - i) {
+      t -= nt - 1 - i;
+      ++i;
+    }
+    I = i;
+    J = i + 1 + t;
+  }
+  const int tileu = tile_index(I, J, nt);
+  constexpr bool diag = DIAG;
+  const int b = blockIdx.z;
+  const int p_begin = split * split_len;
+  const int p_end = min(hw, p_begin + split_len);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const float* zb = z + (size_t)b * c * hw;
+  const int ra0 = I * GT + r, ra1 = I * GT + 32 + r;
+  const int rb0 = J * GT + r, rb1 = J * GT + 32 + r;
+  const float* pa0 = zb + (size_t)min(ra0, c - 1) * hw;
+  const float* pa1 = zb + (size_t)min(ra1, c - 1) * hw;
+  const float* pb0 = zb + (size_t)min(rb0, c - 1) * hw;
+  const float* pb1 = zb + (size_t)min(rb1, c - 1) * hw;
+  const bool va0 = ra0 < c, va1 = ra1 < c, vb0 = rb0 < c, vb1 = rb1 < c;
+
+  f32x16 a00, a01, a10, a11;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) a00[k] = a01[k] = a10[k] = a11[k] = 0.f;
+
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  for (int p0 = p_begin + wave * 32; p0 < p_end; p0 += 128) {
+    f32x4 A0[4], A1[4];
+    const int base = p0 + h * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int pp = base + q * 4;
+      const bool ok = pp < p_end;  // hw % 4 == 0: a float4 is all in or all out
+      A0[q] = (ok && va0) ? *reinterpret_cast<const f32x4*>(pa0 + pp) : zero;
+      A1[q] = (ok && va1) ? *reinterpret_cast<const f32x4*>(pa1 + pp) : zero;
+    }
+    if (diag) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const float x0 = A0[t >> 2][t & 3], x1 = A1[t >> 2][t & 3];
+        a00 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, x0, a00, 0, 0, 0);
+        a01 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, x1, a01, 0, 0, 0);
+        a11 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, x1, a11, 0, 0, 0);
+      }
+    } else {
+      f32x4 B0[4], B1[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int pp = base + q * 4;
+        const bool ok = pp < p_end;
+        B0[q] = (ok && vb0) ? *reinterpret_cast<const f32x4*>(pb0 + pp) : zero;
+        B1[q] = (ok && vb1) ? *reinterpret_cast<const f32x4*>(pb1 + pp) : zero;
+      }
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const float x0 = A0[t >> 2][t & 3], x1 = A1[t >> 2][t & 3];
+        const float y0 = B0[t >> 2][t & 3], y1 = B1[t >> 2][t & 3];
+        a00 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, y0, a00, 0, 0, 0);
+        a01 = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, y1, a01, 0, 0, 0);
+        a10 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, y0, a10, 0, 0, 0);
+        a11 = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, y1, a11, 0, 0, 0);
+      }
+    }
+  }
+  // 4 wave partials -> 2 LDS images (32 KB): waves 2,3 store, waves 0,1 add, then sum
+  auto put = [&](float* img, bool add) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int row = (k & 3) + 8 * (k >> 2) + 4 * h;
+      float* q00 = img + row * GT + r;
+      float* q01 = img + row * GT + 32 + r;
+      float* q11 = img + (32 + row) * GT + 32 + r;
+      float* q10 = img + (32 + row) * GT + r;
+      *q00 = add ? *q00 + a00[k] : a00[k];
+      *q01 = add ? *q01 + a01[k] : a01[k];
+      *q11 = add ? *q11 + a11[k] : a11[k];
+      if (!diag) *q10 = add ? *q10 + a10[k] : a10[k];
+    }
+  };
+  if (wave >= 2) put(red + (wave - 2) * GT * GT, false);
+  __syncthreads();
+  if (wave < 2) put(red + wave * GT * GT, true);
+  __syncthreads();
+  float* out = ws + (((size_t)b * ntu + tileu) * nsplit + split) * (GT * GT);
+#pragma unroll
+  for (int q = 0; q < (GT * GT) / 256; ++q) {
+    const int e = q * 256 + tid;
+    int row = e / GT, col = e % GT;
+    if (diag && row >= 32 && col < 32) {  // mirrored quadrant of a diagonal tile
+      const int t = row;
+      row = col;
+      col = t;
+    }
+    const int o = row * GT + col;
+    out[e] = red[o] + red[GT * GT + o];
+  }
+}
+
 // grid (ntu * 16, B); one thread per tile element (256 elements per block).  The
 // split partials are summed in a fixed order (bit-reproducible); loads are
 // independent and unrolled so a block streams its slab column at full rate.
@@ -176,6 +310,16 @@ __global__ void zero_kernel(float* p, long long n) {
 static void gram_geometry(int c, int hw, int b, int& nsplit, int& split_len, int& ntu) {
   const int nt = cdiv(c, GT);
   ntu = nt * (nt + 1) / 2;
+  if (hw % 4 == 0) {
+    // v2: splits in multiples of 8 (XCD grouping), >= 512 pixels (4 steps/wave),
+    // ~4 blocks per CU
+    int want = rup(cdiv(1024, ntu * b), 8);
+    const int max_splits = std::max(1, cdiv(hw, 512));
+    want = std::max(8, std::min(want, rup(max_splits, 8)));
+    split_len = rup(cdiv(hw, want), 128);
+    nsplit = rup(cdiv(hw, split_len), 8);
+    return;
+  }
   const int chunks = cdiv(hw, GKC);
   // aim for ~512 blocks (2 per CU), at least 8 chunks (512 pixels) per split
   int want = cdiv(512, ntu * b);
@@ -208,8 +352,16 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
   }
   float* slabs = (float*)ws;
   float* parts = slabs + (size_t)b * ntu * nsplit * GT * GT;
-  hipLaunchKernelGGL(gram_partial_kernel, dim3(nsplit, ntu, b), dim3(256), 0, st, z, slabs, c,
-                     hw, nsplit, split_len);
+  if (hw % 4 == 0) {
+    const int nt = cdiv(c, GT);
+    hipLaunchKernelGGL(gram_partial_v2_kernel<true>, dim3(nsplit * nt, 1, b), dim3(256), 0, st,
+                       z, slabs, c, hw, nsplit, split_len);
+    if (ntu > nt)
+      hipLaunchKernelGGL(gram_partial_v2_kernel<false>, dim3(nsplit * (ntu - nt), 1, b),
+                         dim3(256), 0, st, z, slabs, c, hw, nsplit, split_len);
+  } else
+    hipLaunchKernelGGL(gram_partial_kernel, dim3(nsplit, ntu, b), dim3(256), 0, st, z, slabs, c,
+                       hw, nsplit, split_len);
   const int cpad = stx_gram_coef_pitch(c);
   hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(256), 0, st, slabs, c,
                      nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts);
