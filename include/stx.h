@@ -59,6 +59,22 @@ typedef struct stx_conv_params {
   int ho, wo;         /* output dims */
   int cin_pad, cout_pad;
   long long wt_batch_stride; /* floats between per-image weight matrices (0 = shared) */
+  /* optional fused second GEMM phase (Gram backward inside the data-gradient conv):
+   * after the main K loop the mask is applied, then
+   *   value += (*p2_scale) * sum_c A[n][c][co] * p2_z[n][c][oy][ox]
+   * A = p2_wt + n*p2_wt_batch_stride, laid out [c (padded to cin_pad rule of a 1x1 conv)]
+   * [cout_pad]; p2_z [n][p2_c][ho][wo].  p2_z == NULL disables it.  stride 1 only. */
+  const float* p2_z;
+  const float* p2_wt;
+  const float* p2_scale;
+  int p2_c;
+  long long p2_wt_batch_stride;
+  /* optional fused ReLU+MaxPool2d backward epilogue:
+   *   value += unpool(up_dp)[co][oy][ox] * (up_z > 0)
+   * with the 2x2 argmax (first max of relu(up_z), row-major) recomputed from up_z
+   * [n][cout][ho][wo]; up_dp [n][cout][ho/2][wo/2].  up_dp == NULL disables it. */
+  const float* up_dp;
+  const float* up_z;
 } stx_conv_params;
 
 int stx_version(void);

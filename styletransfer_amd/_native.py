@@ -32,6 +32,8 @@ class ConvParams(C.Structure):
         ("cout", i32), ("ks", i32), ("stride", i32), ("pad", i32),
         ("in_mode", i32), ("hv", i32), ("wv", i32), ("ho", i32), ("wo", i32),
         ("cin_pad", i32), ("cout_pad", i32), ("wt_batch_stride", i64),
+        ("p2_z", vp), ("p2_wt", vp), ("p2_scale", vp), ("p2_c", i32), ("p2_wt_batch_stride", i64),
+        ("up_dp", vp), ("up_z", vp),
     ]
 
 

@@ -236,13 +236,13 @@ class VGGLossFn(torch.autograd.Function):
     the content target c4 (engine: styletransfer_amd/vgg.py)."""
 
     @staticmethod
-    def forward(ctx, x, c4, feat, targets):
+    def forward(ctx, x, c4, feat, targets, feature_grad=True):
         st = V.loss_forward(feat, targets, _c(x), _c(c4))
-        ctx.st, ctx.feat = st, feat
+        ctx.st, ctx.feat, ctx.feature_grad = st, feat, feature_grad
         return V.loss_values(st).clone()
 
     @staticmethod
     def backward(ctx, g):
-        dx = V.loss_backward(ctx.feat, ctx.st, _c(g), feature_grad=True)
+        dx = V.loss_backward(ctx.feat, ctx.st, _c(g), feature_grad=ctx.feature_grad)
         ctx.st = None
-        return dx, None, None, None
+        return dx, None, None, None, None

@@ -233,8 +233,100 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
     }
   }
 
-  // epilogue
   const size_t plane = (size_t)p.ho * p.wo;
+  bool mask_done = false;
+  if (p.p2_z) {
+    // ---- fused second phase: acc = acc*(mask>0) + s2 * A[n] . z2 (1x1, no halo) ----
+    if (p.acc_scale) {
+      const float sc = *p.acc_scale;
+#pragma unroll
+      for (int i = 0; i < C::MI; ++i)
+#pragma unroll
+        for (int j = 0; j < C::NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
+    }
+    if (p.mask) {
+#pragma unroll
+      for (int j = 0; j < C::NI; ++j) {
+        const int pix = (wn * C::NI + j) * 32 + l32;
+        const int oy = min(ty0 + pix / TW, p.ho - 1), ox = min(tx0 + pix % TW, p.wo - 1);
+        const size_t pofs = (size_t)oy * p.wo + ox;
+#pragma unroll
+        for (int i = 0; i < C::MI; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int co = min(co0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h,
+                               p.cout - 1);
+            if (!(p.mask[((size_t)n * p.cout + co) * plane + pofs] > 0.f)) acc[i][j][r] = 0.f;
+          }
+      }
+    }
+    mask_done = true;
+    const float s2 = p.p2_scale ? *p.p2_scale : 1.f;
+    const float* __restrict__ z2 = p.p2_z + (size_t)n * p.p2_c * plane;
+    const float* __restrict__ w2 = p.p2_wt + (size_t)n * p.p2_wt_batch_stride;
+    constexpr int E2 = CIS * C::NPIX;               // staged floats per phase-2 chunk
+    constexpr int N2 = (E2 + 255) / 256;
+    constexpr int WQ2 = CIS * BM / 4;
+    constexpr int NW2 = (WQ2 + 255) / 256;
+    static_assert(E2 <= C::LDS_IN && CIS * BM <= C::KC * BM, "phase-2 staging fits");
+    int b2_base[C::NI];
+#pragma unroll
+    for (int j = 0; j < C::NI; ++j)
+      b2_base[j] = h * (CIS / 2) * C::NPIX + (wn * C::NI + j) * 32 + l32;
+    const int a2_base = h * (CIS / 2) * BM + wm * 64 + l32;
+    for (int c0 = 0; c0 < p.p2_c; c0 += CIS) {
+      float v2[N2];
+#pragma unroll
+      for (int e = 0; e < N2; ++e) {
+        const int idx = tid + e * 256;
+        const int ci = idx / C::NPIX, px = idx % C::NPIX;
+        const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+        float v = 0.f;
+        if (idx < E2 && c0 + ci < p.p2_c && oy < p.ho && ox < p.wo)
+          v = s2 * z2[(size_t)(c0 + ci) * plane + (size_t)oy * p.wo + ox];
+        v2[e] = v;
+      }
+      f32x4 wv2[NW2];
+#pragma unroll
+      for (int e = 0; e < NW2; ++e) {
+        const int idx = tid + e * 256;
+        if (idx < WQ2) {
+          const int kr = idx / (BM / 4), c4 = idx - kr * (BM / 4);
+          wv2[e] = *reinterpret_cast<const f32x4*>(w2 + (size_t)(c0 + kr) * p.cout_pad + co0 +
+                                                  c4 * 4);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < N2; ++e) {
+        const int idx = tid + e * 256;
+        if (idx < E2) lds_in[idx] = v2[e];
+      }
+#pragma unroll
+      for (int e = 0; e < NW2; ++e) {
+        const int idx = tid + e * 256;
+        if (idx < WQ2) *reinterpret_cast<f32x4*>(lds_w + idx * 4) = wv2[e];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < CIS / 2; ++s) {
+        float a[C::MI], b[C::NI];
+#pragma unroll
+        for (int i = 0; i < C::MI; ++i) a[i] = lds_w[a2_base + s * BM + i * 32];
+#pragma unroll
+        for (int j = 0; j < C::NI; ++j) b[j] = lds_in[b2_base[j] + s * C::NPIX];
+#pragma unroll
+        for (int i = 0; i < C::MI; ++i)
+#pragma unroll
+          for (int j = 0; j < C::NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue
 #pragma unroll
   for (int j = 0; j < C::NI; ++j) {
     const int pix = (wn * C::NI + j) * 32 + l32;
@@ -249,9 +341,29 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
         if (co >= p.cout) continue;
         const size_t o = ((size_t)n * p.cout + co) * plane + pofs;
         float v = acc[i][j][r];
-        if (p.acc_scale) v *= *p.acc_scale;
+        if (!mask_done) {
+          if (p.acc_scale) v *= *p.acc_scale;
+          if (p.mask) v = p.mask[o] > 0.f ? v : 0.f;
+        }
         if (p.bias) v += p.bias[co];
-        if (p.mask) v = p.mask[o] > 0.f ? v : 0.f;
+        if (p.up_dp) {
+          // ReLU + MaxPool2d(2,2) backward, argmax recomputed from up_z
+          const float* zc = p.up_z + ((size_t)n * p.cout + co) * plane;
+          const int hp = p.ho >> 1, wp = p.wo >> 1;
+          const int py = oy >> 1, px2 = ox >> 1;
+          if (py < hp && px2 < wp && zc[pofs] > 0.f) {
+            const float* q = zc + (size_t)(2 * py) * p.wo + 2 * px2;
+            const float z0 = fmaxf(q[0], 0.f), z1 = fmaxf(q[1], 0.f);
+            const float z2v = fmaxf(q[p.wo], 0.f), z3 = fmaxf(q[p.wo + 1], 0.f);
+            int bi = 0;
+            float best = z0;
+            if (z1 > best) { best = z1; bi = 1; }
+            if (z2v > best) { best = z2v; bi = 2; }
+            if (z3 > best) { bi = 3; }
+            if (bi == ((oy & 1) * 2 + (ox & 1)))
+              v += p.up_dp[(((size_t)n * p.cout + co) * hp + py) * wp + px2];
+          }
+        }
         if (p.aux) v += p.aux_scale * p.aux[o];
         if (p.accumulate) v += p.y[o];
         if (p.relu_out) v = fmaxf(v, 0.f);
@@ -511,8 +623,16 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     set_error("stx_conv2d: raw dims");
     return STX_E_INVALID;
   }
+  if (p.p2_z && (p.stride != 1 || !p.p2_wt || p.p2_c <= 0)) {
+    set_error("stx_conv2d: fused phase 2 needs stride 1, p2_wt and p2_c > 0");
+    return STX_E_INVALID;
+  }
+  if (p.up_dp && (!p.up_z || p.ho < 2 || p.wo < 2)) {
+    set_error("stx_conv2d: unpool epilogue needs up_z");
+    return STX_E_INVALID;
+  }
   if (p.cout <= 4 && p.stride == 1 && (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) &&
-      (p.ks == 3 || p.ks == 9)) {
+      (p.ks == 3 || p.ks == 9) && !p.p2_z && !p.up_dp) {
     const long long blocks16 = (long long)cdiv(p.wo, SC_TW) * cdiv(p.ho, 16) * p.n;
     if (p.ks == 3) return blocks16 >= 512 ? launch_smallc<3, 16>(p, st) : launch_smallc<3, 8>(p, st);
     return blocks16 >= 512 ? launch_smallc<9, 16>(p, st) : launch_smallc<9, 8>(p, st);

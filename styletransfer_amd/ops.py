@@ -96,8 +96,11 @@ def conv_out_hw(hv, wv, ks, stride, pad):
 
 def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=None,
            out=None, mask=None, aux=None, aux_scale=0.0, acc_scale=None, accumulate=False,
-           relu_out=False, wt_batch_stride=0, hv=None, wv=None):
-    """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`."""
+           relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
+           p2_scale=None, up_dp=None, up_z=None):
+    """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
+    p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
+    up_dp/up_z: fused ReLU+MaxPool2d backward epilogue."""
     _req(x, "x")
     n, c, h, w = x.shape
     assert c == cin, (c, cin)
@@ -117,6 +120,13 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
                    n=n, cin=cin, h=h, w=w, cout=cout, ks=ks, stride=stride, pad=pad,
                    in_mode=in_mode, hv=hv, wv=wv, ho=ho, wo=wo, cin_pad=cp, cout_pad=op,
                    wt_batch_stride=int(wt_batch_stride))
+    if p2_z is not None:
+        assert p2_coef is not None and p2_coef.shape[-1] == op, (p2_coef.shape, op)
+        p.p2_z, p.p2_wt, p.p2_scale = p2_z.data_ptr(), p2_coef.data_ptr(), _p(p2_scale)
+        p.p2_c = p2_z.shape[1]
+        p.p2_wt_batch_stride = p2_coef.shape[-1] * p2_coef.shape[-2]
+    if up_dp is not None:
+        p.up_dp, p.up_z = up_dp.data_ptr(), up_z.data_ptr()
     check(lib().stx_conv2d(C.byref(p), _stream()), "stx_conv2d")
     return out
 
@@ -196,6 +206,15 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
                            else None, loss.data_ptr(), b, c, hw, int(tb), float(weight),
                            float(diag_alpha), wp, wn, _stream()), "stx_style_loss")
     return loss, (coef if want_coef else None)
+
+
+def gram_bwd_fused(coef, z, out=None, acc_scale=None, up_dp=None, aux=None, aux_scale=0.0):
+    """out = s*A[n].z[n] (+ unpool(up_dp)*(z>0)) (+ aux_scale*aux): the Gram backward
+    as a 1x1 MFMA conv with the ReLU+MaxPool backward fused into its epilogue."""
+    b, c = z.shape[:2]
+    return conv2d(z, coef, c, c, 1, pad=0, out=out, acc_scale=acc_scale, aux=aux,
+                  aux_scale=aux_scale, wt_batch_stride=coef.shape[-1] * coef.shape[-2],
+                  up_dp=up_dp, up_z=z if up_dp is not None else None)
 
 
 def gram_bwd(coef, z, dz=None, acc_scale=None, mask=None, aux=None, aux_scale=0.0,

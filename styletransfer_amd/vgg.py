@@ -114,14 +114,22 @@ class LossState:
     z: list = field(default_factory=list)       # Z1..Z5
     coef: list = field(default_factory=list)    # A_l per style layer
     c4: torch.Tensor = None                     # content target (pre-ReLU conv2_2)
-    losses: torch.Tensor = None                 # [7] style x5, content, feature
+    losses: torch.Tensor = None                 # [8] style x5, content, feature, f-mse
     fmean: torch.Tensor = None                  # [2] feature loss, its mse
+    folded: bool = False                        # loss weights baked into coef
+    alpha: float = 0.0
 
 
 def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
-                 style_weight_in_coef=1.0):
+                 folded_weights=None):
     """Forward of all 7 losses for input batch x [B,3,H,W] given style targets and
-    the content target c4 (= Z4 of the content image, pre-ReLU)."""
+    the content target c4 (= Z4 of the content image, pre-ReLU).
+
+    folded_weights=(style_weight, content_weight): constant loss weights are baked
+    into the backward operators (A_l scaled by style_weight; the content term's
+    alpha*Z4 on A_4's diagonal) so the backward needs no device scalars — the
+    Gatys engine's case.  None: operators for weight 1; the backward scales by the
+    upstream gradient vector (autograd case)."""
     if st is None:
         st = LossState()
     st.z = feat.forward(x, 5, st.z if st.z else None)
@@ -131,11 +139,18 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         st.fmean = st.losses[6:8]
     if not st.coef:
         st.coef = [None] * 5
-    for i, l in enumerate(STYLE_CONVS):
-        _, st.coef[i] = ops.style_loss(st.z[l], targets[i], weight=style_weight_in_coef,
-                                       loss=st.losses[i], coef=st.coef[i])
     z4 = st.z[CONTENT_CONV]
     assert c4.shape == z4.shape, (c4.shape, z4.shape)
+    sw, alpha = 1.0, 0.0
+    st.folded = folded_weights is not None
+    if st.folded:
+        sw = float(folded_weights[0])
+        alpha = float(folded_weights[1]) * 2.0 / z4.numel()
+    st.alpha = alpha
+    for i, l in enumerate(STYLE_CONVS):
+        _, st.coef[i] = ops.style_loss(st.z[l], targets[i], weight=sw,
+                                       diag_alpha=alpha if l == CONTENT_CONV else 0.0,
+                                       loss=st.losses[i], coef=st.coef[i])
     st.c4 = c4
     ops.mse(z4, c4, out=st.losses[5:6])
     ops.mse(z4, c4, relu=True, mode=1, out=st.fmean)
@@ -147,43 +162,53 @@ def loss_values(st: LossState):
     return st.losses[:N_LOSSES]
 
 
-def loss_backward(feat: VGGFeatures, st: LossState, g, dx=None, feature_grad=True,
+def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_grad=True,
                   scratch=None):
-    """dx = sum_i g[i] * d loss_i / dx.  g: device [7] (style x5, content, feature)."""
+    """dx = sum_i g[i] * d loss_i / dx (g: device [7]: style x5, content, feature), or,
+    for a folded forward, the gradient of the folded weighted total (g ignored).
+
+    Six launches: the Gram backward of the pooled layers runs as a 1x1 MFMA conv with
+    the ReLU+MaxPool backward fused into its epilogue; the Gram backward of the
+    other layers is a second GEMM phase inside the data-gradient conv, after its
+    ReLU mask."""
     z = st.z
     B = z[0].shape[0]
     sc = scratch if scratch is not None else {}
 
-    def buf(name, like_shape):
+    def buf(name, shape):
         t = sc.get(name)
-        if t is None or tuple(t.shape) != tuple(like_shape):
-            t = torch.empty(like_shape, device=z[0].device, dtype=torch.float32)
+        if t is None or tuple(t.shape) != tuple(shape):
+            t = torch.empty(shape, device=z[0].device, dtype=torch.float32)
             sc[name] = t
         return t
 
-    # conv3_1 output
-    dz5 = ops.gram_bwd(st.coef[4], z[4], buf("dz5", z[4].shape), acc_scale=g[4:5])
-    # dgrad conv3_1 -> grad wrt pool(relu Z4)
+    folded = st.folded
+    s = (lambda i: None) if folded else (lambda i: g[i:i + 1])
+    # conv3_1 output: dZ5 = A5 Z5
+    dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4))
+    # -> grad wrt pool(relu Z4)
     n4 = (B, 128, z[3].shape[2] // 2, z[3].shape[3] // 2)
     dp2 = ops.conv2d(dz5, feat.wtT[4], 256, 128, 3, out=buf("dp2", n4))
-    dz4 = ops.relupool_bwd(dp2, z[3], out=buf("dz4", z[3].shape))
-    ops.gram_bwd(st.coef[3], z[3], dz4, acc_scale=g[3:4], accumulate=True)
+    # dZ4 = unpool(dP2)*[Z4>0] + A4 Z4 (+ content)
+    dz4 = ops.gram_bwd_fused(st.coef[3], z[3], out=buf("dz4", z[3].shape), acc_scale=s(3),
+                             up_dp=dp2, aux=st.c4 if folded else None, aux_scale=-st.alpha)
     n = z[3].numel()
-    ops.diff_scale(z[3], st.c4, 2.0 / n, s1=g[5:6], out=dz4, accumulate=True)
-    if feature_grad:
-        ops.diff_scale(z[3], st.c4, 4.0 / (float(n) * float(n)), s1=g[6:7], s2=st.fmean[1:2],
-                       relu=True, out=dz4, accumulate=True)
-    # conv2_2 dgrad, relu mask of Z3, + style3
-    dz3 = ops.conv2d(dz4, feat.wtT[3], 128, 128, 3, mask=z[2], out=buf("dz3", z[2].shape))
-    ops.gram_bwd(st.coef[2], z[2], dz3, acc_scale=g[2:3], accumulate=True)
-    # conv2_1 dgrad -> grad wrt pool(relu Z2)
+    if not folded:
+        ops.diff_scale(z[3], st.c4, 2.0 / n, s1=g[5:6], out=dz4, accumulate=True)
+        if feature_grad:
+            ops.diff_scale(z[3], st.c4, 4.0 / (float(n) * float(n)), s1=g[6:7],
+                           s2=st.fmean[1:2], relu=True, out=dz4, accumulate=True)
+    # dZ3 = conv2_2^T(dZ4)*[Z3>0] + A3 Z3
+    dz3 = ops.conv2d(dz4, feat.wtT[3], 128, 128, 3, mask=z[2], out=buf("dz3", z[2].shape),
+                     p2_z=z[2], p2_coef=st.coef[2], p2_scale=s(2))
+    # -> grad wrt pool(relu Z2)
     n2 = (B, 64, z[1].shape[2] // 2, z[1].shape[3] // 2)
     dp1 = ops.conv2d(dz3, feat.wtT[2], 128, 64, 3, out=buf("dp1", n2))
-    dz2 = ops.relupool_bwd(dp1, z[1], out=buf("dz2", z[1].shape))
-    ops.gram_bwd(st.coef[1], z[1], dz2, acc_scale=g[1:2], accumulate=True)
-    # conv1_2 dgrad, relu mask of Z1, + style1
-    dz1 = ops.conv2d(dz2, feat.wtT[1], 64, 64, 3, mask=z[0], out=buf("dz1", z[0].shape))
-    ops.gram_bwd(st.coef[0], z[0], dz1, acc_scale=g[0:1], accumulate=True)
+    dz2 = ops.gram_bwd_fused(st.coef[1], z[1], out=buf("dz2", z[1].shape), acc_scale=s(1),
+                             up_dp=dp1)
+    # dZ1 = conv1_2^T(dZ2)*[Z1>0] + A1 Z1
+    dz1 = ops.conv2d(dz2, feat.wtT[1], 64, 64, 3, mask=z[0], out=buf("dz1", z[0].shape),
+                     p2_z=z[0], p2_coef=st.coef[0], p2_scale=s(0))
     # conv1_1 dgrad -> image
     xs = (B, 3, z[0].shape[2], z[0].shape[3])
     if dx is None:
@@ -233,9 +258,10 @@ class GatysEngine:
         self.graph = None
 
     def _iteration(self):
-        loss_forward(self.feat, self.targets, self.x, self.c4, self.st)
+        loss_forward(self.feat, self.targets, self.x, self.c4, self.st,
+                     folded_weights=(self.sw, self.cw))
         ops.loss_combine(self.st.losses, [self.sw] * 5 + [self.cw], self.total)
-        loss_backward(self.feat, self.st, self.g, dx=self.grad, feature_grad=False,
+        loss_backward(self.feat, self.st, dx=self.grad, feature_grad=False,
                       scratch=self.scratch)
         ops.adam_step(self.x, self.grad, self.m, self.v, self.step_dev, self.adam_ws, self.lr,
                       self.betas[0], self.betas[1], self.eps)

@@ -245,3 +245,27 @@ def test_upsample_tv(dev):
     loss = ops.tv_loss(y, 1e-6, grad=g)
     assert rel(loss, ref) < 1e-5
     assert rel(g, rg) < 1e-6
+
+
+def test_conv_fused_gram_phase_and_unpool(dev):
+    """dgrad conv with fused ReLU mask + Gram-backward phase, and the 1x1 Gram-backward
+    conv with the fused ReLU+MaxPool backward epilogue, vs unfused torch."""
+    n, c, h, w = 2, 64, 20, 36
+    z = rnd(n, c, h, w, dev=dev, seed=91, scale=2, shift=-1)
+    dy = rnd(n, c, h, w, dev=dev, seed=92, scale=2, shift=-1)
+    wgt = rnd(c, c, 3, 3, dev=dev, seed=93, scale=0.2, shift=-0.1)
+    t = rnd(c, c, dev=dev, seed=94)
+    loss, coef = ops.style_loss(z, t, weight=2.0)
+    s2 = torch.tensor(0.5, device=dev)
+    wtT = ops.conv_weight_prep(wgt, transpose=True)
+    out = ops.conv2d(dy, wtT, c, c, 3, mask=z, p2_z=z, p2_coef=coef, p2_scale=s2)
+    xr = z.clone().requires_grad_()
+    (ref_d,) = torch.autograd.grad(F.conv2d(xr, wgt, padding=1), xr, dy)
+    ref = torch.where(z > 0, ref_d, torch.zeros_like(ref_d)) + 0.5 * ops.gram_bwd(coef, z)
+    assert rel(out, ref) < TOL
+    # unpool epilogue: out = s*A.z + unpool(dp)*(z>0)
+    dp = rnd(n, c, h // 2, w // 2, dev=dev, seed=95, scale=2, shift=-1)
+    aux = rnd(n, c, h, w, dev=dev, seed=96)
+    out2 = ops.gram_bwd_fused(coef, z, acc_scale=s2, up_dp=dp, aux=aux, aux_scale=-0.25)
+    ref2 = 0.5 * ops.gram_bwd(coef, z) + ops.relupool_bwd(dp, z) - 0.25 * aux
+    assert rel(out2, ref2) < TOL
