@@ -132,6 +132,9 @@ int stx_gram_bwd(const float* coef, const float* z, float* dz, int b, int c, int
  *   s = sum((f(a) - f(b))^2), f = relu if relu_inputs else identity
  *   mode 0: *out = s / n                        (F.mse_loss, mean)
  *   mode 1: out[0] = (s / n)^2 / n, out[1] = s / n   (FeatureReconstructionLoss)
+ *   mode 2: both from one pass (16-B aligned a, b; relu_inputs ignored):
+ *           out[0] = mean((a-b)^2), out[1] = mean((relu a - relu b)^2)^2 / n,
+ *           out[2] = mean((relu a - relu b)^2)   (content + feature at conv2_2)
  * grad (optional, mode 0): grad = gscale * 2*(a-b)/n. */
 size_t stx_mse_ws(long long n);
 int stx_mse(const float* a, const float* b, long long n, int relu_inputs, int mode,

@@ -434,11 +434,13 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
 #pragma unroll
     for (int q = 0; q < SC_PX; ++q) acc[c][q] = 0.f;
 
-  for (int c0 = 0; c0 < p.cin; c0 += CIS) {
+  // register-prefetched staging: the halo loads of chunk c+1 are issued before the
+  // FMAs of chunk c (1 wave/SIMD when the image is small, so latency must overlap)
+  float hv[CIS][C::NE];
+  auto fetch = [&](int c0) {
     const int cn = min(CIS, p.cin - c0);
-    float hv[CIS][C::NE];
 #pragma unroll
-    for (int cil = 0; cil < CIS; ++cil) {  // all loads of the chunk in flight together
+    for (int cil = 0; cil < CIS; ++cil) {
       const float* src = xn + (size_t)(c0 + cil) * plane_in;
 #pragma unroll
       for (int e = 0; e < C::NE; ++e) {
@@ -450,6 +452,10 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
         hv[cil][e] = v;
       }
     }
+  };
+  fetch(0);
+  for (int c0 = 0; c0 < p.cin; c0 += CIS) {
+    const int cn = min(CIS, p.cin - c0);
     __syncthreads();
 #pragma unroll
     for (int cil = 0; cil < CIS; ++cil)
@@ -464,6 +470,7 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
                         : zero;
     }
     __syncthreads();
+    if (c0 + CIS < p.cin) fetch(c0 + CIS);
     for (int cil = 0; cil < cn; ++cil) {
       const f32x4* wk = wts + cil * KK;
 #pragma unroll
@@ -543,7 +550,11 @@ __global__ void weight_prep_kernel(const float* __restrict__ w, float* __restric
   }
 }
 
-static int cis_for(int ks) { return ks == 9 ? 2 : (ks == 1 ? 16 : 8); }
+// input channels per K chunk; 3x3 convs over <= 4 channels (conv1_1, 3-channel
+// images) use 4 so the RGB input is padded to 4, not 8
+static int cis_for(int ks, int cin) {
+  return ks == 9 ? 2 : (ks == 1 ? 16 : (cin <= 4 ? 4 : 8));
+}
 
 template <int KS, int S, int CIS, int BM, int TW>
 static int launch_fwd(const stx_conv_params& p, hipStream_t st) {
@@ -557,6 +568,10 @@ static int launch_fwd(const stx_conv_params& p, hipStream_t st) {
 template <int KS, int S, int BM>
 static int dispatch_tw(const stx_conv_params& p, hipStream_t st) {
   constexpr int CIS = KS == 9 ? 2 : (KS == 1 ? 16 : 8);
+  if (KS == 3 && S == 1 && BM == 64 && p.cin_pad == 4) {  // 3-channel input
+    if (p.wo > 32) return launch_fwd<3, 1, 4, 64, 64>(p, st);
+    return launch_fwd<3, 1, 4, 64, 16>(p, st);
+  }
   if (p.wo > 32) return launch_fwd<KS, S, CIS, BM, 64>(p, st);
   if (p.wo > 16) return launch_fwd<KS, S, CIS, BM, 32>(p, st);
   return launch_fwd<KS, S, CIS, BM, 16>(p, st);
@@ -571,8 +586,9 @@ extern "C" int stx_conv_weight_dims(int cin, int cout, int ks, int* cin_pad, int
     set_error("stx_conv_weight_dims: unsupported kernel size %d", ks);
     return STX_E_INVALID;
   }
-  if (cin_pad) *cin_pad = rup(cin, cis_for(ks));
-  if (cout_pad) *cout_pad = rup(cout, 128);
+  if (cin_pad) *cin_pad = rup(cin, cis_for(ks, cin));
+  // BM is 64 for cout <= 64 and 128 otherwise; pad to the tile so VGG widths need none
+  if (cout_pad) *cout_pad = cout <= 64 ? rup(cout, 64) : rup(cout, 128);
   return STX_OK;
 }
 

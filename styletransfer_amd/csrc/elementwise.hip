@@ -57,6 +57,57 @@ __global__ void mse_finalize_kernel(const float* __restrict__ parts, int nparts,
   }
 }
 
+// ContentLoss on conv2_2 and FeatureReconstructionLoss on relu(conv2_2) read the
+// same two tensors: one pass computes both sums (float4 when aligned).
+__global__ void __launch_bounds__(RB)
+sqdiff2_partial_kernel(const float* __restrict__ a, const float* __restrict__ b, long long n,
+                       float* __restrict__ parts) {
+  __shared__ float red[RB / 64];
+  float s = 0.f, sr = 0.f;
+  const long long n4 = n / 4;
+  const long long stride = (long long)gridDim.x * RB;
+  for (long long i = blockIdx.x * (long long)RB + threadIdx.x; i < n4; i += stride) {
+    const f32x4 x = reinterpret_cast<const f32x4*>(a)[i];
+    const f32x4 y = reinterpret_cast<const f32x4*>(b)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = x[k] - y[k], dr = fmaxf(x[k], 0.f) - fmaxf(y[k], 0.f);
+      s += d * d;
+      sr += dr * dr;
+    }
+  }
+  for (long long i = n4 * 4 + blockIdx.x * (long long)RB + threadIdx.x; i < n; i += stride) {
+    const float d = a[i] - b[i], dr = fmaxf(a[i], 0.f) - fmaxf(b[i], 0.f);
+    s += d * d;
+    sr += dr * dr;
+  }
+  s = block_sum<RB>(s, red);
+  sr = block_sum<RB>(sr, red);
+  if (threadIdx.x == 0) {
+    parts[2 * blockIdx.x] = s;
+    parts[2 * blockIdx.x + 1] = sr;
+  }
+}
+
+// out[0] = mean sq diff; out[1] = mean(relu sq diff)^2 / n; out[2] = mean relu sq diff
+__global__ void mse2_finalize_kernel(const float* __restrict__ parts, int nparts, double n,
+                                     float* __restrict__ out) {
+  __shared__ float red[RB / 64];
+  float s = 0.f, sr = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += RB) {
+    s += parts[2 * i];
+    sr += parts[2 * i + 1];
+  }
+  s = block_sum<RB>(s, red);
+  sr = block_sum<RB>(sr, red);
+  if (threadIdx.x == 0) {
+    const float mr = (float)(sr / n);
+    out[0] = (float)(s / n);
+    out[1] = (float)((double)(mr * mr) / n);
+    out[2] = mr;
+  }
+}
+
 // grad = s0 * (*s1) * (*s2) * (f(a) - f(b))   (autograd backward of the MSE losses)
 __global__ void diff_scale_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                   float* __restrict__ g, long long n, float s0,
@@ -361,12 +412,12 @@ static int ew_blocks(long long n) {
 
 using namespace stx;
 
-extern "C" size_t stx_mse_ws(long long n) { return (size_t)(red_blocks(n) + 4) * sizeof(float); }
+extern "C" size_t stx_mse_ws(long long n) { return (size_t)(2 * red_blocks(n) + 4) * sizeof(float); }
 
 extern "C" int stx_mse(const float* a, const float* b, long long n, int relu_inputs, int mode,
                        float* out, float* grad, float gscale, void* ws, size_t ws_bytes,
                        void* stream) {
-  if (n <= 0 || !a || !b || !out || (mode != 0 && mode != 1) || (grad && mode != 0)) {
+  if (n <= 0 || !a || !b || !out || mode < 0 || mode > 2 || (grad && mode != 0)) {
     set_error("stx_mse: invalid args");
     return STX_E_INVALID;
   }
@@ -377,6 +428,16 @@ extern "C" int stx_mse(const float* a, const float* b, long long n, int relu_inp
   hipStream_t st = (hipStream_t)stream;
   const int nb = red_blocks(n);
   float* parts = (float*)ws;
+  if (mode == 2) {
+    if (((uintptr_t)a | (uintptr_t)b) & 15) {
+      set_error("stx_mse: mode 2 needs 16-byte aligned inputs");
+      return STX_E_INVALID;
+    }
+    hipLaunchKernelGGL(sqdiff2_partial_kernel, dim3(nb), dim3(RB), 0, st, a, b, n, parts);
+    hipLaunchKernelGGL(mse2_finalize_kernel, dim3(1), dim3(RB), 0, st, parts, nb, (double)n,
+                       out);
+    return check_launch("stx_mse");
+  }
   const float gs = (float)(gscale * 2.0 / (double)n);
   hipLaunchKernelGGL(sqdiff_partial_kernel, dim3(nb), dim3(RB), 0, st, a, b, n, relu_inputs,
                      parts, grad, gs);

@@ -240,12 +240,18 @@ gram_partial_v2_kernel(const float* __restrict__ z, float* __restrict__ ws, int 
 // grid (ntu * 16, B); one thread per tile element (256 elements per block).  The
 // split partials are summed in a fixed order (bit-reproducible); loads are
 // independent and unrolled so a block streams its slab column at full rate.
-constexpr int FSUB = GT * GT / 256;
+// 16 tile elements x 16 split-lanes per block: each split-lane sums every 16th
+// partial (4 loads in flight), the 16 lane sums are combined through LDS in a
+// fixed order, so the result is bit-reproducible and a C=64 tile's 512 partials
+// are read by 256 blocks instead of 16.
+constexpr int FEL = 16, FKL = 16;
+constexpr int FSUB = GT * GT / FEL;   // blocks per tile
 __global__ void __launch_bounds__(256)
 gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scale,
                      float* __restrict__ g_out, const float* __restrict__ target, long long t_bstride,
                      float* __restrict__ coef, int cpad, float cA, float alpha,
                      float* __restrict__ loss_parts) {
+  __shared__ float part[FKL][FEL + 1];
   __shared__ float red[4];
   const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
   const int tile = blockIdx.x / FSUB, sub = blockIdx.x % FSUB;
@@ -253,36 +259,43 @@ gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scal
   tile_ij(tile, nt, I, J);
   const int b = blockIdx.y;
   const float* src = ws + ((size_t)b * ntu + tile) * nsplit * (GT * GT);
-  float sq = 0.f;
+  const int el = threadIdx.x % FEL, kl = threadIdx.x / FEL;
+  const int e = sub * FEL + el;
   {
-    const int e = sub * 256 + threadIdx.x;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int k = 0;
-    for (; k + 4 <= nsplit; k += 4) {
-      s0 += src[(size_t)(k + 0) * GT * GT + e];
-      s1 += src[(size_t)(k + 1) * GT * GT + e];
-      s2 += src[(size_t)(k + 2) * GT * GT + e];
-      s3 += src[(size_t)(k + 3) * GT * GT + e];
+    int k = kl;
+    for (; k + 3 * FKL < nsplit; k += 4 * FKL) {
+      s0 += src[(size_t)(k + 0 * FKL) * GT * GT + e];
+      s1 += src[(size_t)(k + 1 * FKL) * GT * GT + e];
+      s2 += src[(size_t)(k + 2 * FKL) * GT * GT + e];
+      s3 += src[(size_t)(k + 3 * FKL) * GT * GT + e];
     }
-    for (; k < nsplit; ++k) s0 += src[(size_t)k * GT * GT + e];
-    const float s = (s0 + s1) + (s2 + s3);
+    for (; k < nsplit; k += FKL) s0 += src[(size_t)k * GT * GT + e];
+    part[kl][el] = (s0 + s1) + (s2 + s3);
+  }
+  __syncthreads();
+  float sq = 0.f;
+  if (kl == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < FKL; ++q) s += part[q][el];
     const int gi = I * GT + e / GT, gj = J * GT + e % GT;
     if (gi < c && gj < c) {
-    const float g = s * scale;
-    if (g_out) {
-      g_out[((size_t)b * c + gi) * c + gj] = g;
-      if (I != J) g_out[((size_t)b * c + gj) * c + gi] = g;
-    }
-    if (target) {
-      const float d = g - target[(size_t)b * t_bstride + (size_t)gi * c + gj];
-      sq += (I != J ? 2.f : 1.f) * d * d;
-      if (coef) {
-        const float a = cA * d;
-        float* cb = coef + (size_t)b * cpad * cpad;
-        cb[(size_t)gi * cpad + gj] = a + (gi == gj ? alpha : 0.f);
-        if (I != J) cb[(size_t)gj * cpad + gi] = a;
+      const float g = s * scale;
+      if (g_out) {
+        g_out[((size_t)b * c + gi) * c + gj] = g;
+        if (I != J) g_out[((size_t)b * c + gj) * c + gi] = g;
       }
-    }
+      if (target) {
+        const float d = g - target[(size_t)b * t_bstride + (size_t)gi * c + gj];
+        sq = (I != J ? 2.f : 1.f) * d * d;
+        if (coef) {
+          const float a = cA * d;
+          float* cb = coef + (size_t)b * cpad * cpad;
+          cb[(size_t)gi * cpad + gj] = a + (gi == gj ? alpha : 0.f);
+          if (I != J) cb[(size_t)gj * cpad + gi] = a;
+        }
+      }
     }
   }
   if (target) {
@@ -377,7 +390,7 @@ using namespace stx;
 
 extern "C" size_t stx_gram_ws(int b, int c, int hw) { return gram_ws_bytes(b, c, hw); }
 
-extern "C" int stx_gram_coef_pitch(int c) { return rup(c, 128); }
+extern "C" int stx_gram_coef_pitch(int c) { return c <= 64 ? rup(c, 64) : rup(c, 128); }
 
 extern "C" int stx_gram(const float* z, float* g, int b, int c, int hw, float scale, void* ws,
                         size_t ws_bytes, void* stream) {
@@ -397,7 +410,7 @@ extern "C" int stx_style_loss(const float* z, const float* target, float* g_out,
   const float scale = (float)(1.0 / n);
   // d(weight*mean((G-T)^2))/dF_b = weight * 2(G-T)/(B C^2) * 2 F_b / N   (G symmetric)
   const float cA = (float)(weight * 4.0 / ((double)b * c * c * n));
-  if (coef) {
+  if (coef && stx_gram_coef_pitch(c) != c) {  // zero the padding (finalize writes c x c)
     const int cpad = stx_gram_coef_pitch(c);
     const long long cnt = (long long)b * cpad * cpad;
     hipLaunchKernelGGL(zero_kernel, dim3((int)std::min<long long>((cnt + 255) / 256, 2048)),

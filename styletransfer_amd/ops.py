@@ -237,7 +237,7 @@ def mse(a, b, relu=False, mode=0, out=None, grad=None, gscale=1.0):
     assert a.numel() == b.numel()
     n = a.numel()
     if out is None:
-        out = torch.empty(2 if mode == 1 else 1, device=a.device, dtype=torch.float32)
+        out = torch.empty({0: 1, 1: 2, 2: 3}[mode], device=a.device, dtype=torch.float32)
     L = lib()
     wp, wn = WS.get(L.stx_mse_ws(n), a.device)
     check(L.stx_mse(a.data_ptr(), b.data_ptr(), n, int(relu), mode, out.data_ptr(), _p(grad),

@@ -152,8 +152,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                                        diag_alpha=alpha if l == CONTENT_CONV else 0.0,
                                        loss=st.losses[i], coef=st.coef[i])
     st.c4 = c4
-    ops.mse(z4, c4, out=st.losses[5:6])
-    ops.mse(z4, c4, relu=True, mode=1, out=st.fmean)
+    ops.mse(z4, c4, mode=2, out=st.losses[5:8])  # content, feature, feature-mse: one pass
     return st
 
 

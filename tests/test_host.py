@@ -27,9 +27,9 @@ def test_library_exports_header_symbols():
 
 def test_host_queries_without_gpu():
     from styletransfer_amd import ops
-    assert ops.conv_weight_dims(3, 64, 3) == (8, 128)
+    assert ops.conv_weight_dims(3, 64, 3) == (4, 64)
     assert ops.conv_weight_dims(128, 256, 3) == (128, 256)
-    assert ops.coef_pitch(64) == 128
+    assert ops.coef_pitch(64) == 64 and ops.coef_pitch(96) == 128
     from styletransfer_amd import _native as N
     assert N.lib().stx_gram_ws(1, 64, 262144) > 0
     assert N.lib().stx_conv2d_wgrad_ws(8, 128, 128, 3, 1, 64, 64) > 0
