@@ -35,6 +35,26 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;
 }
 
+// Raw buffer loads with the hardware range check: an offset at or past the
+// descriptor's byte count returns 0.  Gather loaders address every element through
+// one per-chunk descriptor and mark padding/out-of-tile elements with BUF_OOB, so
+// the fetch is straight-line code (no per-element exec branches, no serialising
+// vmcnt(0) per load) and channel padding past the tensor end reads as zero.
+constexpr uint32_t BUF_OOB = 0x80000000u;  // callers keep byte counts below this
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const float* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ inline int rup(int a, int b) { return cdiv(a, b) * b; }
 

@@ -68,8 +68,9 @@ struct ConvCfg {
   static constexpr int NH = (HALO + 255) / 256;
   static constexpr int WQ = KC * BM / 4;       // float4 per weight slab
   static constexpr int NW = (WQ + 255) / 256;
-  static constexpr int LDS_IN = CIS * CH;
-  static constexpr int LDS_FLOATS = LDS_IN + KC * BM;
+  // halo / slab regions padded to whole 256-thread rounds: the stores are unconditional
+  static constexpr int LDS_IN = NH * 256;
+  static constexpr int LDS_FLOATS = LDS_IN + NW * 1024;
   static_assert(CIS % 2 == 0, "CIS must be even (two lane halves)");
   static_assert(NPIX % TW == 0, "tile");
 };
@@ -79,29 +80,47 @@ struct ConvCfg {
 // input-channel plane; only the channel base moves from chunk to chunk.  So the
 // per-element offsets and the in-bounds mask are computed once per block and the
 // per-chunk fetch is one (or, for the fused 2x2 pool, four) loads per element.
-template <int MODE, int NH, int HALO, int RHW>
-__device__ __forceinline__ void halo_fetch(float (&hreg)[NH], const float* __restrict__ src,
-                                           const int (&hoff)[NH], uint64_t hvalid, int w,
-                                           int ci_lim, int tid) {
+// Halo element i of this thread (idx = tid + i*256) always maps to the same
+// (ci_local, r, c) and, for a given block, to the same byte offset from the
+// chunk's first input channel; only the chunk base moves.  So the offsets are
+// computed once per block (BUF_OOB for zero padding) and the per-chunk fetch is
+// one (or, for the fused 2x2 pool, four) unconditional buffer loads per element.
+// The loads land raw in registers; the relu / pool transform runs in
+// halo_store, after the MFMA loop, so no wait on them is exposed before it.
+template <bool POOL, int NH>
+__device__ __forceinline__ void halo_fetch(float (&hraw)[NH][4], __amdgpu_buffer_rsrc_t rs,
+                                           const uint32_t (&hoff)[NH], uint32_t wb) {
 #pragma unroll
   for (int i = 0; i < NH; ++i) {
-    bool ok = (hvalid >> i) & 1;
-    if (ci_lim < 0x7fffffff) ok = ok && ((tid + i * 256) / RHW) < ci_lim;
-    float v = 0.f;
-    if (ok) {
-      const float* q = src + hoff[i];
-      if (MODE == STX_IN_RELU_POOL2) {
-        v = fmaxf(fmaxf(fmaxf(q[0], q[1]), fmaxf(q[w], q[w + 1])), 0.f);
-      } else {
-        v = q[0];
-        if (MODE == STX_IN_RELU) v = fmaxf(v, 0.f);
-      }
+    const uint32_t o = hoff[i];
+    hraw[i][0] = buf_ld(rs, o);
+    if (POOL) {
+      hraw[i][1] = buf_ld(rs, o + 4);
+      hraw[i][2] = buf_ld(rs, o + wb);
+      hraw[i][3] = buf_ld(rs, o + wb + 4);
     }
-    hreg[i] = v;
   }
 }
 
-template <int KS, int S, int CIS, int BM, int TW>
+template <int MODE, int NH>
+__device__ __forceinline__ void halo_store(float* __restrict__ lds_in, const float (&hraw)[NH][4],
+                                           int tid) {
+#pragma unroll
+  for (int i = 0; i < NH; ++i) {
+    const int idx = tid + i * 256;
+    float v = hraw[i][0];
+    if (MODE == STX_IN_RELU_POOL2)
+      v = fmaxf(fmaxf(fmaxf(v, hraw[i][1]), fmaxf(hraw[i][2], hraw[i][3])), 0.f);
+    else if (MODE == STX_IN_RELU)
+      v = fmaxf(v, 0.f);
+    lds_in[idx] = v;  // idx >= HALO lands in the padding of the halo region
+  }
+}
+
+// LM: loader mode of the halo fetch -- STX_IN_RAW (also serves UPSAMPLE2 and
+// DILATE2, whose index maps live in the precomputed offsets), STX_IN_RELU or
+// STX_IN_RELU_POOL2 (four loads per element).
+template <int KS, int S, int CIS, int BM, int TW, int LM>
 __global__ void __launch_bounds__(256, 2)
 conv_fwd_kernel(stx_conv_params p, int tiles_x) {
   using C = ConvCfg<KS, S, CIS, BM, TW>;
@@ -126,9 +145,8 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
   const int mode = p.in_mode;
   const int plane_in = p.h * p.w;
 
-  // chunk-invariant halo source offsets + validity
-  int hoff[C::NH];
-  uint64_t hvalid = 0;
+  // chunk-invariant halo byte offsets (BUF_OOB = zero padding)
+  uint32_t hoff[C::NH];
 #pragma unroll
   for (int i = 0; i < C::NH; ++i) {
     const int idx = tid + i * 256;
@@ -150,8 +168,7 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
       sx = vx >> 1;
       ok = ok && sy < p.h && sx < p.w;
     }
-    hoff[i] = ok ? ci * plane_in + sy * p.w + sx : 0;
-    if (ok) hvalid |= (uint64_t)1 << i;
+    hoff[i] = ok ? (uint32_t)(ci * plane_in + sy * p.w + sx) * 4u : BUF_OOB;
   }
 
   f32x16 acc[C::MI][C::NI];
@@ -172,43 +189,35 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
   }
   const int a_base = h * (CIS / 2) * C::KK * BM + wm * 64 + l32;
 
-  float hreg[C::NH];
+  float hraw[C::NH][4];
   f32x4 wreg[C::NW];
   const int nchunks = p.cin_pad / CIS;
 
+  // chunk-invariant weight-slab byte offsets (from the chunk's first slab row)
+  uint32_t woff[C::NW];
+#pragma unroll
+  for (int i = 0; i < C::NW; ++i) {
+    const int idx = tid + i * 256;
+    const int kr = idx / (BM / 4), c4 = idx - kr * (BM / 4);
+    woff[i] = idx < C::WQ ? (uint32_t)(kr * p.cout_pad + co0 + c4 * 4) * 4u : BUF_OOB;
+  }
+  const uint32_t wbytes = (uint32_t)p.cin_pad * C::KK * p.cout_pad * 4u;
+
   auto fetch = [&](int chunk) {
     const int c0 = chunk * CIS;
-    const float* src = xn + (size_t)c0 * plane_in;
-    const int ci_lim = (c0 + CIS <= p.cin) ? 0x7fffffff : p.cin - c0;
-    constexpr int RHW = C::RH * C::RW;
-    if (mode == STX_IN_RELU_POOL2)
-      halo_fetch<STX_IN_RELU_POOL2, C::NH, C::HALO, RHW>(hreg, src, hoff, hvalid, p.w, ci_lim,
-                                                          tid);
-    else if (mode == STX_IN_RELU)
-      halo_fetch<STX_IN_RELU, C::NH, C::HALO, RHW>(hreg, src, hoff, hvalid, p.w, ci_lim, tid);
-    else
-      halo_fetch<STX_IN_RAW, C::NH, C::HALO, RHW>(hreg, src, hoff, hvalid, p.w, ci_lim, tid);
-    const float* wsrc = wt + (size_t)c0 * C::KK * p.cout_pad + co0;
+    // descriptor over channels [c0, cin): padding channels past cin read 0
+    const auto rs = make_srd(xn + (size_t)c0 * plane_in, (uint32_t)(p.cin - c0) * plane_in * 4u);
+    halo_fetch<LM == STX_IN_RELU_POOL2, C::NH>(hraw, rs, hoff, 4u * p.w);
+    const uint32_t wskip = (uint32_t)c0 * C::KK * p.cout_pad * 4u;
+    const auto rw = make_srd(wt + (size_t)c0 * C::KK * p.cout_pad, wbytes - wskip);
 #pragma unroll
-    for (int i = 0; i < C::NW; ++i) {
-      const int idx = tid + i * 256;
-      if (idx < C::WQ) {
-        const int kr = idx / (BM / 4), c4 = idx - kr * (BM / 4);
-        wreg[i] = *reinterpret_cast<const f32x4*>(wsrc + (size_t)kr * p.cout_pad + c4 * 4);
-      }
-    }
+    for (int i = 0; i < C::NW; ++i) wreg[i] = buf_ld4(rw, woff[i]);
   };
   auto store = [&]() {
+    halo_store<LM, C::NH>(lds_in, hraw, tid);
 #pragma unroll
-    for (int i = 0; i < C::NH; ++i) {
-      const int idx = tid + i * 256;
-      if (idx < C::HALO) lds_in[idx] = hreg[i];
-    }
-#pragma unroll
-    for (int i = 0; i < C::NW; ++i) {
-      const int idx = tid + i * 256;
-      if (idx < C::WQ) *reinterpret_cast<f32x4*>(lds_w + idx * 4) = wreg[i];
-    }
+    for (int i = 0; i < C::NW; ++i)
+      *reinterpret_cast<f32x4*>(lds_w + (tid + i * 256) * 4) = wreg[i];
   };
 
   fetch(0);
@@ -217,19 +226,34 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
     store();
     __syncthreads();
     if (chunk + 1 < nchunks) fetch(chunk + 1);  // overlaps the MFMA loop below
-#pragma unroll
-    for (int s = 0; s < (CIS / 2) * C::KK; ++s) {
+    // Software-pipelined operand reads: a ring of PD register slots; the LDS reads
+    // of step s+PD are issued right after step s's MFMAs consume slot s%PD, so an
+    // LDS round trip is hidden behind PD steps (4 MFMAs = 256 cycles each).
+    constexpr int NS = (CIS / 2) * C::KK;
+    constexpr int PD = 3;
+    float ra[PD][C::MI], rb[PD][C::NI];
+    auto rd = [&](int s, float (&a)[C::MI], float (&b)[C::NI]) {
       const int cil = s / C::KK, r = s % C::KK, kh = r / KS, kw = r % KS;
-      float a[C::MI], b[C::NI];
 #pragma unroll
       for (int i = 0; i < C::MI; ++i) a[i] = lds_w[a_base + s * BM + i * 32];
 #pragma unroll
       for (int j = 0; j < C::NI; ++j) b[j] = lds_in[b_base[j] + cil * C::CH + kh * C::RWP + kw];
+    };
+#pragma unroll
+    for (int s = 0; s < PD && s < NS; ++s) rd(s, ra[s], rb[s]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int slot = s % PD;
 #pragma unroll
       for (int i = 0; i < C::MI; ++i)
 #pragma unroll
         for (int j = 0; j < C::NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[slot][i], rb[slot][j], acc[i][j],
+                                                           0, 0, 0);
+      if (s + PD < NS) rd(s + PD, ra[slot], rb[slot]);
+      // keep the prefetch reads ahead of the next step's MFMAs (the scheduler
+      // otherwise sinks them next to their use and waits lgkmcnt(0) every step)
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
@@ -276,18 +300,20 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
     for (int j = 0; j < C::NI; ++j)
       b2_base[j] = h * (CIS / 2) * C::NPIX + (wn * C::NI + j) * 32 + l32;
     const int a2_base = h * (CIS / 2) * BM + wm * 64 + l32;
+    uint32_t off2[N2];  // chunk-invariant byte offsets of the staged Z elements
+#pragma unroll
+    for (int e = 0; e < N2; ++e) {
+      const int idx = tid + e * 256;
+      const int ci = idx / C::NPIX, px = idx % C::NPIX;
+      const int oy = ty0 + px / TW, ox = tx0 + px % TW;
+      const bool ok = idx < E2 && oy < p.ho && ox < p.wo;
+      off2[e] = ok ? (uint32_t)(ci * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
+    }
     for (int c0 = 0; c0 < p.p2_c; c0 += CIS) {
+      const auto rz = make_srd(z2 + (size_t)c0 * plane, (uint32_t)((p.p2_c - c0) * plane * 4));
       float v2[N2];
 #pragma unroll
-      for (int e = 0; e < N2; ++e) {
-        const int idx = tid + e * 256;
-        const int ci = idx / C::NPIX, px = idx % C::NPIX;
-        const int oy = ty0 + px / TW, ox = tx0 + px % TW;
-        float v = 0.f;
-        if (idx < E2 && c0 + ci < p.p2_c && oy < p.ho && ox < p.wo)
-          v = s2 * z2[(size_t)(c0 + ci) * plane + (size_t)oy * p.wo + ox];
-        v2[e] = v;
-      }
+      for (int e = 0; e < N2; ++e) v2[e] = s2 * buf_ld(rz, off2[e]);
       f32x4 wv2[NW2];
 #pragma unroll
       for (int e = 0; e < NW2; ++e) {
@@ -556,25 +582,28 @@ static int cis_for(int ks, int cin) {
   return ks == 9 ? 2 : (ks == 1 ? 16 : (cin <= 4 ? 4 : 8));
 }
 
-template <int KS, int S, int CIS, int BM, int TW>
+template <int KS, int S, int CIS, int BM, int TW, int LM>
 static int launch_fwd(const stx_conv_params& p, hipStream_t st) {
   using C = ConvCfg<KS, S, CIS, BM, TW>;
   const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
   dim3 grid(tiles_x * tiles_y, cdiv(p.cout, BM), p.n);
-  hipLaunchKernelGGL((conv_fwd_kernel<KS, S, CIS, BM, TW>), grid, dim3(256), 0, st, p, tiles_x);
+  hipLaunchKernelGGL((conv_fwd_kernel<KS, S, CIS, BM, TW, LM>), grid, dim3(256), 0, st, p,
+                     tiles_x);
   return check_launch("stx_conv2d");
 }
 
-template <int KS, int S, int BM>
+template <int KS, int S, int BM, int LM>
 static int dispatch_tw(const stx_conv_params& p, hipStream_t st) {
   constexpr int CIS = KS == 9 ? 2 : (KS == 1 ? 16 : 8);
-  if (KS == 3 && S == 1 && BM == 64 && p.cin_pad == 4) {  // 3-channel input
-    if (p.wo > 32) return launch_fwd<3, 1, 4, 64, 64>(p, st);
-    return launch_fwd<3, 1, 4, 64, 16>(p, st);
+  if constexpr (KS == 3 && S == 1 && BM == 64 && LM == STX_IN_RAW) {  // RGB input
+    if (p.cin_pad == 4) {
+      if (p.wo > 32) return launch_fwd<3, 1, 4, 64, 64, LM>(p, st);
+      return launch_fwd<3, 1, 4, 64, 16, LM>(p, st);
+    }
   }
-  if (p.wo > 32) return launch_fwd<KS, S, CIS, BM, 64>(p, st);
-  if (p.wo > 16) return launch_fwd<KS, S, CIS, BM, 32>(p, st);
-  return launch_fwd<KS, S, CIS, BM, 16>(p, st);
+  if (p.wo > 32) return launch_fwd<KS, S, CIS, BM, 64, LM>(p, st);
+  if (p.wo > 16) return launch_fwd<KS, S, CIS, BM, 32, LM>(p, st);
+  return launch_fwd<KS, S, CIS, BM, 16, LM>(p, st);
 }
 
 }  // namespace stx
@@ -639,6 +668,15 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     set_error("stx_conv2d: raw dims");
     return STX_E_INVALID;
   }
+  // buffer-descriptor byte counts (and the BUF_OOB sentinel) are 32-bit
+  const long long in_bytes = 4LL * p.cin * p.h * p.w;
+  const long long wt_bytes = 4LL * p.cin_pad * p.ks * p.ks * p.cout_pad;
+  const long long p2_bytes = p.p2_z ? 4LL * p.p2_c * p.ho * p.wo : 0;
+  if (in_bytes >= (long long)BUF_OOB / 2 || wt_bytes >= (long long)BUF_OOB / 2 ||
+      p2_bytes >= (long long)BUF_OOB / 2) {
+    set_error("stx_conv2d: per-image tensor too large (>= 1 GiB)");
+    return STX_E_INVALID;
+  }
   if (p.p2_z && (p.stride != 1 || !p.p2_wt || p.p2_c <= 0)) {
     set_error("stx_conv2d: fused phase 2 needs stride 1, p2_wt and p2_c > 0");
     return STX_E_INVALID;
@@ -654,13 +692,26 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     return blocks16 >= 512 ? launch_smallc<9, 16>(p, st) : launch_smallc<9, 8>(p, st);
   }
   const bool big = p.cout > 64;
+  if (p.in_mode == STX_IN_RELU || p.in_mode == STX_IN_RELU_POOL2) {
+    // fused relu / relu+pool loaders: the VGG 3x3 stride-1 layers
+    if (p.ks != 3 || p.stride != 1 || p.cin_pad % 8) {
+      set_error("stx_conv2d: relu/pool input modes need a 3x3 stride-1 conv with cin > 4");
+      return STX_E_INVALID;
+    }
+    if (p.in_mode == STX_IN_RELU)
+      return big ? dispatch_tw<3, 1, 128, STX_IN_RELU>(p, st)
+                 : dispatch_tw<3, 1, 64, STX_IN_RELU>(p, st);
+    return big ? dispatch_tw<3, 1, 128, STX_IN_RELU_POOL2>(p, st)
+               : dispatch_tw<3, 1, 64, STX_IN_RELU_POOL2>(p, st);
+  }
+  constexpr int R = STX_IN_RAW;
   if (p.ks == 3 && p.stride == 1)
-    return big ? dispatch_tw<3, 1, 128>(p, st) : dispatch_tw<3, 1, 64>(p, st);
+    return big ? dispatch_tw<3, 1, 128, R>(p, st) : dispatch_tw<3, 1, 64, R>(p, st);
   if (p.ks == 3 && p.stride == 2)
-    return big ? dispatch_tw<3, 2, 128>(p, st) : dispatch_tw<3, 2, 64>(p, st);
-  if (p.ks == 9 && p.stride == 1) return dispatch_tw<9, 1, 64>(p, st);
+    return big ? dispatch_tw<3, 2, 128, R>(p, st) : dispatch_tw<3, 2, 64, R>(p, st);
+  if (p.ks == 9 && p.stride == 1) return dispatch_tw<9, 1, 64, R>(p, st);
   if (p.ks == 1 && p.stride == 1)
-    return big ? dispatch_tw<1, 1, 128>(p, st) : dispatch_tw<1, 1, 64>(p, st);
+    return big ? dispatch_tw<1, 1, 128, R>(p, st) : dispatch_tw<1, 1, 64, R>(p, st);
   set_error("stx_conv2d: unsupported ks=%d stride=%d", p.ks, p.stride);
   return STX_E_INVALID;
 }

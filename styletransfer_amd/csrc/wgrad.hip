@@ -162,13 +162,25 @@ wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* _
     store();
     __syncthreads();
     if (kt + 1 < kt_end) fetch(kt + 1);
-#pragma unroll
-    for (int s = 0; s < NPIX / 2; ++s) {
+    // operand reads software-pipelined PD steps ahead (see conv_fwd_kernel)
+    constexpr int NS = NPIX / 2, PD = 2;
+    float ra[PD], rb[PD][NI];
+    auto rd = [&](int s, float& a, float (&b)[NI]) {
       const int poff = (s / TW) * S * C::RWP + (s % TW) * S;
-      const float a = ldy[aoff + s];
+      a = ldy[aoff + s];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) b[ni] = halo[boff[ni] + poff];
+    };
+#pragma unroll
+    for (int s = 0; s < PD; ++s) rd(s, ra[s], rb[s]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int slot = s % PD;
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
-        acc[ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, halo[boff[ni] + poff], acc[ni], 0, 0, 0);
+        acc[ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[slot], rb[slot][ni], acc[ni], 0, 0, 0);
+      if (s + PD < NS) rd(s + PD, ra[slot], rb[slot]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 

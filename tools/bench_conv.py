@@ -24,6 +24,10 @@ def ev(fn, reps=20):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="run only cases whose name contains this")
+    args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     cases = [
@@ -41,6 +45,8 @@ def main():
         ("itn down s2 B8 32->64", 8, 32, 64, 256, 256, 3, 2, N.STX_IN_RAW),
     ]
     for name, n, cin, cout, h, w, ks, s, mode in cases:
+        if args.only not in name:
+            continue
         x = torch.randn(n, cin, h, w, generator=g).to(dev)
         wt = ops.conv_weight_prep(torch.randn(cout, cin, ks, ks, generator=g).to(dev) * 0.05)
         hv, wv = ops.virtual_hw(h, w, mode)
@@ -51,6 +57,8 @@ def main():
         print(f"{name:32s} {ms * 1e3:9.1f} us  {gf / ms:8.2f} TFLOP/s")
     for name, n, c, h in (("gram C64 512^2", 1, 64, 512), ("gram C128 256^2", 1, 128, 256),
                           ("gram C256 128^2", 1, 256, 128), ("gram C64 B8 256^2", 8, 64, 256)):
+        if args.only not in name:
+            continue
         z = torch.randn(n, c, h, h, generator=g).to(dev)
         t = torch.randn(c, c, generator=g).to(dev)
         coef = None
@@ -65,6 +73,8 @@ def main():
     for name, n, cin, cout, h, ks, s in (("wgrad res B8 128 64^2", 8, 128, 128, 64, 3, 1),
                                          ("wgrad conv0 9x9 B8", 8, 3, 32, 256, 9, 1),
                                          ("wgrad conv22 9x9 B8", 8, 32, 3, 256, 9, 1)):
+        if args.only not in name:
+            continue
         x = torch.randn(n, cin, h, h, generator=g).to(dev)
         ho = (h + 2 * (ks // 2) - ks) // s + 1
         dy = torch.randn(n, cout, ho, ho, generator=g).to(dev)
