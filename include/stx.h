@@ -75,6 +75,22 @@ typedef struct stx_conv_params {
    * [n][cout][ho][wo]; up_dp [n][cout][ho/2][wo/2].  up_dp == NULL disables it. */
   const float* up_dp;
   const float* up_z;
+  /* fp16 hi/lo split path (3x3 stride-1 convs, cin >= 16, cout > 4): when wt16 is
+   * non-NULL the conv runs on v_mfma_f32_32x32x16_f16 with both operands split as
+   * s*v = hi + lo (fp16 each, s a per-tensor power of two) and the three products
+   * hi*hi + hi*lo + lo*hi accumulated in fp32 (fp32-level accuracy).
+   * wt16/w_amax come from stx_conv_weight_prep16; in_amax is a device scalar
+   * >= max|x| over the physical input (stx_amax, or a producer's out_amax). */
+  const void* wt16;
+  const float* w_amax;
+  const float* in_amax;
+  /* optional: *out_amax = max(*out_amax, max|y|) over the values this call writes
+   * (caller zeroes it first) — the next split conv's in_amax at no extra pass. */
+  float* out_amax;
+  /* optional fused VGG ReLU + MaxPool2d(2,2) output: pool_out [n][cout][ho/2][wo/2] =
+   * maxpool(relu(y)) (torch floor mode), written beside y.  Split path (wt16) with
+   * wo > 32 only; the next conv then reads it with STX_IN_RAW. */
+  float* pool_out;
 } stx_conv_params;
 
 int stx_version(void);
@@ -89,6 +105,18 @@ int stx_conv_weight_dims(int cin, int cout, int ks, int* cin_pad, int* cout_pad)
  * (cin'=cout, cout'=cin) padded by stx_conv_weight_dims(cout, cin, ks). */
 int stx_conv_weight_prep(const float* w, float* wt, int cout, int cin, int ks, int transpose,
                          void* stream);
+
+/* fp16 hi/lo split weight slab for the wt16 path: bytes of the slab for GEMM dims
+ * (cin', cout') = (cin, cout), or (cout, cin) for transpose=1, ks = 3. */
+size_t stx_conv_weight16_bytes(int cin, int cout, int ks, int transpose);
+/* w [cout][cin][3][3] -> split slab wt16 ([cin'/16][tap][hi,lo][cin' group of 8]
+ * [cout' padded to 64][8] fp16, scaled by 2^(15-e), max|w| < 2^e) and *w_amax =
+ * max|w| (device scalar).  transpose=1: the data-gradient weights (as
+ * stx_conv_weight_prep). */
+int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax, int cout, int cin, int ks,
+                           int transpose, void* stream);
+/* *out = max |x[i]| over n floats (device scalar; NaN propagates). */
+int stx_amax(const float* x, long long n, float* out, void* stream);
 
 /* Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32), fused input
  * transform (in_mode) and epilogue (bias, mask, aux, accumulate, relu). */

@@ -34,6 +34,8 @@ class ConvParams(C.Structure):
         ("cin_pad", i32), ("cout_pad", i32), ("wt_batch_stride", i64),
         ("p2_z", vp), ("p2_wt", vp), ("p2_scale", vp), ("p2_c", i32), ("p2_wt_batch_stride", i64),
         ("up_dp", vp), ("up_z", vp),
+        ("wt16", vp), ("w_amax", vp), ("in_amax", vp), ("out_amax", vp),
+        ("pool_out", vp),
     ]
 
 
@@ -44,6 +46,9 @@ SIGNATURES = {
     "stx_conv_weight_dims": (i32, [i32, i32, i32, C.POINTER(i32), C.POINTER(i32)]),
     "stx_conv_weight_prep": (i32, [vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv2d": (i32, [C.POINTER(ConvParams), vp]),
+    "stx_conv_weight16_bytes": (sz, [i32, i32, i32, i32]),
+    "stx_conv_weight_prep16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
+    "stx_amax": (i32, [vp, i64, vp, vp]),
     "stx_conv2d_wgrad_ws": (sz, [i32, i32, i32, i32, i32, i32, i32]),
     "stx_conv2d_wgrad": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                i32, i32, i32, i32, vp, sz, vp]),

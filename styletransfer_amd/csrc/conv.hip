@@ -20,6 +20,7 @@
 // (stransfer/network.py:468-481, 525-609; zero padding = torch 1.1.0 semantics
 // of padding_mode='reflection').
 #include "common.h"
+#include "conv_epi.h"
 #include "../../include/stx.h"
 
 namespace stx {
@@ -180,11 +181,14 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // per-lane LDS bases
+  // 1x1 convs (the Gram backward with the fused unpool epilogue) use the row-pair
+  // pixel mapping so each 2x2 pooling window lies inside one wave
+  constexpr bool ROWPAIR = KS == 1 && TW == 64;
   int b_base[C::NI];
 #pragma unroll
   for (int j = 0; j < C::NI; ++j) {
-    const int pix = (wn * C::NI + j) * 32 + l32;
-    const int ty = pix / TW, tx = pix % TW;
+    int ty, tx;
+    tile_pix<TW, ROWPAIR>(wn, j, l32, ty, tx);
     b_base[j] = h * (CIS / 2) * C::CH + ty * S * C::RWP + tx * S;
   }
   const int a_base = h * (CIS / 2) * C::KK * BM + wm * 64 + l32;
@@ -257,161 +261,27 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
     }
   }
 
-  const size_t plane = (size_t)p.ho * p.wo;
-  bool mask_done = false;
-  if (p.p2_z) {
-    // ---- fused second phase: acc = acc*(mask>0) + s2 * A[n] . z2 (1x1, no halo) ----
-    if (p.acc_scale) {
-      const float sc = *p.acc_scale;
-#pragma unroll
-      for (int i = 0; i < C::MI; ++i)
-#pragma unroll
-        for (int j = 0; j < C::NI; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
-    }
-    if (p.mask) {
-#pragma unroll
-      for (int j = 0; j < C::NI; ++j) {
-        const int pix = (wn * C::NI + j) * 32 + l32;
-        const int oy = min(ty0 + pix / TW, p.ho - 1), ox = min(tx0 + pix % TW, p.wo - 1);
-        const size_t pofs = (size_t)oy * p.wo + ox;
-#pragma unroll
-        for (int i = 0; i < C::MI; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int co = min(co0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h,
-                               p.cout - 1);
-            if (!(p.mask[((size_t)n * p.cout + co) * plane + pofs] > 0.f)) acc[i][j][r] = 0.f;
-          }
-      }
-    }
-    mask_done = true;
-    const float s2 = p.p2_scale ? *p.p2_scale : 1.f;
-    const float* __restrict__ z2 = p.p2_z + (size_t)n * p.p2_c * plane;
-    const float* __restrict__ w2 = p.p2_wt + (size_t)n * p.p2_wt_batch_stride;
-    constexpr int E2 = CIS * C::NPIX;               // staged floats per phase-2 chunk
-    constexpr int N2 = (E2 + 255) / 256;
-    constexpr int WQ2 = CIS * BM / 4;
-    constexpr int NW2 = (WQ2 + 255) / 256;
-    static_assert(E2 <= C::LDS_IN && CIS * BM <= C::KC * BM, "phase-2 staging fits");
-    int b2_base[C::NI];
-#pragma unroll
-    for (int j = 0; j < C::NI; ++j)
-      b2_base[j] = h * (CIS / 2) * C::NPIX + (wn * C::NI + j) * 32 + l32;
-    const int a2_base = h * (CIS / 2) * BM + wm * 64 + l32;
-    uint32_t off2[N2];  // chunk-invariant byte offsets of the staged Z elements
-#pragma unroll
-    for (int e = 0; e < N2; ++e) {
-      const int idx = tid + e * 256;
-      const int ci = idx / C::NPIX, px = idx % C::NPIX;
-      const int oy = ty0 + px / TW, ox = tx0 + px % TW;
-      const bool ok = idx < E2 && oy < p.ho && ox < p.wo;
-      off2[e] = ok ? (uint32_t)(ci * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
-    }
-    for (int c0 = 0; c0 < p.p2_c; c0 += CIS) {
-      const auto rz = make_srd(z2 + (size_t)c0 * plane, (uint32_t)((p.p2_c - c0) * plane * 4));
-      float v2[N2];
-#pragma unroll
-      for (int e = 0; e < N2; ++e) v2[e] = s2 * buf_ld(rz, off2[e]);
-      f32x4 wv2[NW2];
-#pragma unroll
-      for (int e = 0; e < NW2; ++e) {
-        const int idx = tid + e * 256;
-        if (idx < WQ2) {
-          const int kr = idx / (BM / 4), c4 = idx - kr * (BM / 4);
-          wv2[e] = *reinterpret_cast<const f32x4*>(w2 + (size_t)(c0 + kr) * p.cout_pad + co0 +
-                                                  c4 * 4);
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int e = 0; e < N2; ++e) {
-        const int idx = tid + e * 256;
-        if (idx < E2) lds_in[idx] = v2[e];
-      }
-#pragma unroll
-      for (int e = 0; e < NW2; ++e) {
-        const int idx = tid + e * 256;
-        if (idx < WQ2) *reinterpret_cast<f32x4*>(lds_w + idx * 4) = wv2[e];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < CIS / 2; ++s) {
-        float a[C::MI], b[C::NI];
-#pragma unroll
-        for (int i = 0; i < C::MI; ++i) a[i] = lds_w[a2_base + s * BM + i * 32];
-#pragma unroll
-        for (int j = 0; j < C::NI; ++j) b[j] = lds_in[b2_base[j] + s * C::NPIX];
-#pragma unroll
-        for (int i = 0; i < C::MI; ++i)
-#pragma unroll
-          for (int j = 0; j < C::NI; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
-    }
-  }
-
-  // epilogue
-#pragma unroll
-  for (int j = 0; j < C::NI; ++j) {
-    const int pix = (wn * C::NI + j) * 32 + l32;
-    const int oy = ty0 + pix / TW, ox = tx0 + pix % TW;
-    if (oy >= p.ho || ox >= p.wo) continue;
-    const size_t pofs = (size_t)oy * p.wo + ox;
-#pragma unroll
-    for (int i = 0; i < C::MI; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = co0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (co >= p.cout) continue;
-        const size_t o = ((size_t)n * p.cout + co) * plane + pofs;
-        float v = acc[i][j][r];
-        if (!mask_done) {
-          if (p.acc_scale) v *= *p.acc_scale;
-          if (p.mask) v = p.mask[o] > 0.f ? v : 0.f;
-        }
-        if (p.bias) v += p.bias[co];
-        if (p.up_dp) {
-          // ReLU + MaxPool2d(2,2) backward, argmax recomputed from up_z
-          const float* zc = p.up_z + ((size_t)n * p.cout + co) * plane;
-          const int hp = p.ho >> 1, wp = p.wo >> 1;
-          const int py = oy >> 1, px2 = ox >> 1;
-          if (py < hp && px2 < wp && zc[pofs] > 0.f) {
-            const float* q = zc + (size_t)(2 * py) * p.wo + 2 * px2;
-            const float z0 = fmaxf(q[0], 0.f), z1 = fmaxf(q[1], 0.f);
-            const float z2v = fmaxf(q[p.wo], 0.f), z3 = fmaxf(q[p.wo + 1], 0.f);
-            int bi = 0;
-            float best = z0;
-            if (z1 > best) { best = z1; bi = 1; }
-            if (z2v > best) { best = z2v; bi = 2; }
-            if (z3 > best) { bi = 3; }
-            if (bi == ((oy & 1) * 2 + (ox & 1)))
-              v += p.up_dp[(((size_t)n * p.cout + co) * hp + py) * wp + px2];
-          }
-        }
-        if (p.aux) v += p.aux_scale * p.aux[o];
-        if (p.accumulate) v += p.y[o];
-        if (p.relu_out) v = fmaxf(v, 0.f);
-        p.y[o] = v;
-      }
-    }
-  }
+  static_assert(CIS * C::NPIX <= C::LDS_IN && CIS * BM <= C::KC * BM, "phase-2 staging fits");
+  const EpiTile et{n, co0, ty0, tx0, wm, wn, h, l32};
+  conv_epilogue<BM, TW, C::NPIX, CIS, ROWPAIR>(acc, p, et, 1.f, lds_in, lds_w);
 }
 
 // ------------------------------------------------------- small-cout direct conv
 // cout <= 4, stride 1 (VGG conv1_1 data-gradient 64->3, ImageTransformNet's final
 // 9x9 conv 32->3).  An MFMA tile would be >= 90% padding here, so this is a VALU
-// direct convolution: thread = 4 consecutive output pixels x all output channels,
-// block = 16 x 64 output pixels; the input halo of CIS channels is staged in LDS
-// (row pitch padded to 16 B for ds_read_b128); weights are read from the standard
-// prepped slab at wave-uniform addresses (scalar loads), so every FMA takes one
-// LDS value that is re-used KS times across kw and COUT times across channels.
-constexpr int SC_TW = 64, SC_PX = 4;
+// direct convolution: thread = 4 consecutive output pixels x all output channels;
+// a block is G = 2 channel groups x (TH x 64 output pixels): group g takes the
+// input-channel chunks g, g+2, ... (so one image tile keeps 2x the waves in flight),
+// and the two partial sums are added in a fixed order at the end (deterministic).
+// Per chunk of CIS channels the input halo (row pitch padded to 16 B for
+// ds_read_b128) and the chunk's weights are prefetched into registers during the
+// previous chunk's FMAs and staged in LDS; every FMA takes one LDS value re-used KS
+// times across kw and COUT times across output channels; weights are LDS broadcasts.
+constexpr int SC_TW = 64, SC_PX = 4, SC_G = 2;
 
 template <int KS, int CIS, int TH>
 struct SmallCfg {
-  static constexpr int NT = 16 * TH;                   // threads: 16 per output row
+  static constexpr int NT = 16 * TH;                   // threads per channel group
   static constexpr int RH = TH + KS - 1;
   static constexpr int RW = SC_TW + KS - 1;
   static constexpr int RWP = (RW + 3) / 4 * 4;
@@ -419,16 +289,18 @@ struct SmallCfg {
   static constexpr int PL = RH * RW;                   // halo elements per channel plane
   static constexpr int NE = (PL + NT - 1) / NT;
   static constexpr int NV = (SC_PX + KS - 1 + 3) / 4;  // float4 reads per row
+  static constexpr int WU = CIS * KS * KS;             // f32x4 weight units per chunk
+  static constexpr int NWU = (WU + NT - 1) / NT;
 };
 
 template <int KS, int CIS, int TH>
-__global__ void __launch_bounds__(16 * TH)
+__global__ void __launch_bounds__(SC_G * 16 * TH)
 conv_smallc_kernel(stx_conv_params p, int tiles_x) {
   using C = SmallCfg<KS, CIS, TH>;
   constexpr int COUT = 4;
-  __shared__ __attribute__((aligned(16))) float halo[CIS * C::CH];
-  __shared__ __attribute__((aligned(16))) f32x4 wts[CIS * KS * KS];  // [ci][tap] -> 4 couts
-  const int tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float halo[SC_G][CIS * C::CH];
+  __shared__ __attribute__((aligned(16))) f32x4 wts[SC_G][C::WU];  // [ci][tap] -> 4 couts
+  const int g = threadIdx.x / C::NT, tid = threadIdx.x % C::NT;
   const int ty = tid / 16, tx = tid % 16;
   const int tile = blockIdx.x, n = blockIdx.z;
   const int oy0 = (tile / tiles_x) * TH, ox0 = (tile % tiles_x) * SC_TW;
@@ -436,7 +308,7 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
   const float* __restrict__ xn = p.x + (size_t)n * p.cin * p.h * p.w;
   const float* __restrict__ wt = p.wt + (size_t)n * p.wt_batch_stride;
   const int plane_in = p.h * p.w;
-  const int KK = KS * KS;
+  constexpr int KK = KS * KS;
   const bool relu_in = p.in_mode == STX_IN_RELU;
 
   // plane-invariant halo offsets (source and LDS) of this thread's elements
@@ -460,9 +332,8 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
 #pragma unroll
     for (int q = 0; q < SC_PX; ++q) acc[c][q] = 0.f;
 
-  // register-prefetched staging: the halo loads of chunk c+1 are issued before the
-  // FMAs of chunk c (1 wave/SIMD when the image is small, so latency must overlap)
   float hv[CIS][C::NE];
+  f32x4 wv[C::NWU];
   auto fetch = [&](int c0) {
     const int cn = min(CIS, p.cin - c0);
 #pragma unroll
@@ -478,31 +349,48 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
         hv[cil][e] = v;
       }
     }
-  };
-  fetch(0);
-  for (int c0 = 0; c0 < p.cin; c0 += CIS) {
-    const int cn = min(CIS, p.cin - c0);
-    __syncthreads();
 #pragma unroll
-    for (int cil = 0; cil < CIS; ++cil)
-#pragma unroll
-      for (int e = 0; e < C::NE; ++e)
-        if (loff[e] >= 0) halo[cil * C::CH + loff[e]] = hv[cil][e];
-    for (int i = tid; i < CIS * KK; i += C::NT) {
+    for (int k = 0; k < C::NWU; ++k) {
+      const int i = tid + k * C::NT;
       const int cil = i / KK;
       const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-      wts[i] = cil < cn ? *reinterpret_cast<const f32x4*>(
-                              wt + (size_t)((c0 + cil) * KK + (i - cil * KK)) * p.cout_pad)
-                        : zero;
+      wv[k] = (i < C::WU && cil < cn)
+                  ? *reinterpret_cast<const f32x4*>(wt + (size_t)((c0 + cil) * KK + (i - cil * KK)) *
+                                                             p.cout_pad)
+                  : zero;
+    }
+  };
+  // chunks of this group: c0 = (2k + g) * CIS
+  const int nch = cdiv(p.cin, CIS);
+  int chunk = g;
+  if (chunk < nch) fetch(chunk * CIS);
+  // every thread runs the same number of loop trips (barriers): groups idle past nch
+  const int trips = cdiv(nch, SC_G);
+  for (int it = 0; it < trips; ++it, chunk += SC_G) {
+    const bool active = chunk < nch;
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int cil = 0; cil < CIS; ++cil)
+#pragma unroll
+        for (int e = 0; e < C::NE; ++e)
+          if (loff[e] >= 0) halo[g][cil * C::CH + loff[e]] = hv[cil][e];
+#pragma unroll
+      for (int k = 0; k < C::NWU; ++k) {
+        const int i = tid + k * C::NT;
+        if (i < C::WU) wts[g][i] = wv[k];
+      }
     }
     __syncthreads();
-    if (c0 + CIS < p.cin) fetch(c0 + CIS);
+    if (!active) continue;
+    const int cn = min(CIS, p.cin - chunk * CIS);
+    if (chunk + SC_G < nch) fetch((chunk + SC_G) * CIS);
     for (int cil = 0; cil < cn; ++cil) {
-      const f32x4* wk = wts + cil * KK;
+      const f32x4* wk = wts[g] + cil * KK;
 #pragma unroll
       for (int kh = 0; kh < KS; ++kh) {
         float in[C::NV * 4];
-        const float* row = halo + cil * C::CH + (ty + kh) * C::RWP + tx * SC_PX;
+        const float* row = halo[g] + cil * C::CH + (ty + kh) * C::RWP + tx * SC_PX;
 #pragma unroll
         for (int v = 0; v < C::NV; ++v) {
           const f32x4 t = *reinterpret_cast<const f32x4*>(row + 4 * v);
@@ -522,6 +410,22 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
       }
     }
   }
+  // fixed-order combine: group 1's partial sums through LDS, added by group 0
+  __syncthreads();
+  float* red = &halo[0][0];
+  static_assert(C::NT * COUT * SC_PX <= CIS * C::CH, "reduction buffer fits");
+  if (g == 1) {
+#pragma unroll
+    for (int c = 0; c < COUT; ++c)
+#pragma unroll
+      for (int q = 0; q < SC_PX; ++q) red[(c * SC_PX + q) * C::NT + tid] = acc[c][q];
+  }
+  __syncthreads();
+  if (g == 1) return;
+#pragma unroll
+  for (int c = 0; c < COUT; ++c)
+#pragma unroll
+    for (int q = 0; q < SC_PX; ++q) acc[c][q] += red[(c * SC_PX + q) * C::NT + tid];
   const int oy = oy0 + ty;
   if (oy >= p.ho) return;
   const size_t plane = (size_t)p.ho * p.wo;
@@ -549,7 +453,9 @@ template <int KS, int TH>
 static int launch_smallc(const stx_conv_params& p, hipStream_t st) {
   const int tiles_x = cdiv(p.wo, SC_TW), tiles_y = cdiv(p.ho, TH);
   dim3 grid(tiles_x * tiles_y, 1, p.n);
-  hipLaunchKernelGGL((conv_smallc_kernel<KS, 8, TH>), grid, dim3(16 * TH), 0, st, p, tiles_x);
+  constexpr int CIS = KS == 9 ? 4 : 8;
+  hipLaunchKernelGGL((conv_smallc_kernel<KS, CIS, TH>), grid, dim3(SC_G * 16 * TH), 0, st, p,
+                     tiles_x);
   return check_launch("stx_conv2d(smallc)");
 }
 
@@ -605,6 +511,8 @@ static int dispatch_tw(const stx_conv_params& p, hipStream_t st) {
   if (p.wo > 16) return launch_fwd<KS, S, CIS, BM, 32, LM>(p, st);
   return launch_fwd<KS, S, CIS, BM, 16, LM>(p, st);
 }
+
+int conv2d_f16x3(const stx_conv_params& p, hipStream_t st);  // conv16.hip
 
 }  // namespace stx
 
@@ -685,11 +593,24 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     set_error("stx_conv2d: unpool epilogue needs up_z");
     return STX_E_INVALID;
   }
+  // fp16 hi/lo split MFMA path (conv16.hip) for the 3x3 stride-1 layers it covers;
+  // other shapes keep the fp32 MFMA kernels (wt is always required)
+  if (p.wt16 && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.cout > 4 && p.cin >= 16 &&
+      p.wt_batch_stride == 0) {
+    if (!p.w_amax || !p.in_amax) {
+      set_error("stx_conv2d: the wt16 path needs w_amax and in_amax");
+      return STX_E_INVALID;
+    }
+    return conv2d_f16x3(p, st);
+  }
+  if (p.pool_out) {
+    set_error("stx_conv2d: pool_out is only fused on the split (wt16) path");
+    return STX_E_INVALID;
+  }
   if (p.cout <= 4 && p.stride == 1 && (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) &&
-      (p.ks == 3 || p.ks == 9) && !p.p2_z && !p.up_dp) {
-    const long long blocks16 = (long long)cdiv(p.wo, SC_TW) * cdiv(p.ho, 16) * p.n;
-    if (p.ks == 3) return blocks16 >= 512 ? launch_smallc<3, 16>(p, st) : launch_smallc<3, 8>(p, st);
-    return blocks16 >= 512 ? launch_smallc<9, 16>(p, st) : launch_smallc<9, 8>(p, st);
+      (p.ks == 3 || p.ks == 9) && !p.p2_z && !p.up_dp && !p.out_amax) {
+    if (p.ks == 3) return launch_smallc<3, 8>(p, st);
+    return launch_smallc<9, 8>(p, st);
   }
   const bool big = p.cout > 64;
   if (p.in_mode == STX_IN_RELU || p.in_mode == STX_IN_RELU_POOL2) {

@@ -1,0 +1,295 @@
+// Fused epilogue shared by the implicit-GEMM conv kernels (conv.hip: fp32 MFMA,
+// conv16.hip: fp16 hi/lo split MFMA).  Both keep the same accumulator tiling:
+// 4 waves in a WM x WN grid, each wave 2 x 2 tiles of 32x32 (MI = NI = 2), so
+//   output channel  co  = co0 + wm*64 + i*32 + (r & 3) + 8*(r >> 2) + 4*h
+//   output pixel    pix = (wn*2 + j)*32 + l32   of the block's TH x TW tile
+// for accumulator register r of tile (i, j) in lane (h = lane>>5, l32 = lane&31)
+// (the C/D layout of every 32x32 MFMA on gfx950).
+//
+// Order of operations (stx_conv_params, include/stx.h):
+//   v = acc * pre_scale                      (fp16-split de-scaling; 1 for fp32)
+//   v *= *acc_scale; v *= (mask > 0)          (data-gradient ReLU mask)
+//   v += s2 * A[n] . p2_z                     (fused Gram-backward phase, 1x1 fp32 MFMA)
+//   v += bias; v += unpool(up_dp)*(up_z>0); v += aux_scale*aux; v += y; relu
+//   y = v;  *out_amax = max(*out_amax, |v|)  (next fp16-split conv's input scale)
+#pragma once
+#include "common.h"
+#include "../../include/stx.h"
+
+namespace stx {
+
+struct EpiTile {
+  int n, co0, ty0, tx0, wm, wn, h, l32;
+};
+
+// (ty, tx) inside the block tile of the pixel lane l32 of wave column wn holds in
+// N-tile j.  Default: the wave's two tiles are consecutive runs of 32 pixels in
+// row-major tile order.  ROWPAIR (TW == 64): wave column wn covers x in
+// [32*(wn&1), +32) of rows 2*(wn>>1) + {0, 1}, so every 2x2 pooling window lies in
+// one wave (tiles j = 0/1 x lanes l32, l32^1) -- the fused ReLU+MaxPool output.
+template <int TW, bool ROWPAIR>
+__device__ __forceinline__ void tile_pix(int wn, int j, int l32, int& ty, int& tx) {
+  if (ROWPAIR) {
+    static_assert(!ROWPAIR || TW == 64, "row-pair mapping needs TW == 64");
+    tx = (wn & 1) * 32 + l32;
+    ty = (wn >> 1) * 2 + j;
+  } else {
+    const int pix = (wn * 2 + j) * 32 + l32;
+    ty = pix / TW;
+    tx = pix - ty * TW;
+  }
+}
+
+__device__ __forceinline__ void atomic_max_abs(float* slot, float m) {
+  // |v| >= 0: the IEEE bit pattern orders like the value (NaN sorts above inf)
+  atomicMax(reinterpret_cast<unsigned int*>(slot), __float_as_uint(m));
+}
+
+// max over the 256-thread block (NaN wins), then ONE device atomic per block: a
+// same-address atomic per wave costs ~12 ns each chip-wide (8192 of them stalled a
+// 64 MB pass for 100 us)
+__device__ __forceinline__ void block_max_to(float* slot, float m) {
+  __shared__ float red[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float other = __shfl_xor(m, o, 64);
+    m = (other != other) ? other : fmaxf(m, other);
+  }
+  const int tid = threadIdx.x;
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) {
+    float r = red[0];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
+    atomic_max_abs(slot, fabsf(r));
+  }
+}
+
+template <int BM, int TW, int NPIX, int CIS2, bool ROWPAIR = false>
+__device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_conv_params& p,
+                                              const EpiTile& t, float pre_scale,
+                                              float* __restrict__ lds_in,
+                                              float* __restrict__ lds_w) {
+  const int tid = threadIdx.x;
+  const size_t plane = (size_t)p.ho * p.wo;
+  const int n = t.n, h = t.h, l32 = t.l32;
+  if (pre_scale != 1.f) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= pre_scale;
+  }
+  bool mask_done = false;
+  if (p.p2_z) {
+    // ---- fused second phase: acc = acc*(mask>0) + s2 * A[n] . z2 (1x1, no halo) ----
+    if (p.acc_scale) {
+      const float sc = *p.acc_scale;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
+    }
+    if (p.mask) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        int ty, tx;
+        tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
+        const int oy = min(t.ty0 + ty, p.ho - 1), ox = min(t.tx0 + tx, p.wo - 1);
+        const size_t pofs = (size_t)oy * p.wo + ox;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int co = min(t.co0 + t.wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h,
+                               p.cout - 1);
+            if (!(p.mask[((size_t)n * p.cout + co) * plane + pofs] > 0.f)) acc[i][j][r] = 0.f;
+          }
+      }
+    }
+    mask_done = true;
+    const float s2 = p.p2_scale ? *p.p2_scale : 1.f;
+    const float* __restrict__ z2 = p.p2_z + (size_t)n * p.p2_c * plane;
+    const float* __restrict__ w2 = p.p2_wt + (size_t)n * p.p2_wt_batch_stride;
+    constexpr int E2 = CIS2 * NPIX;  // staged floats per phase-2 chunk
+    constexpr int N2 = (E2 + 255) / 256;
+    constexpr int WQ2 = CIS2 * BM / 4;
+    constexpr int NW2 = (WQ2 + 255) / 256;
+    int b2_base[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int ty, tx;
+      tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
+      b2_base[j] = h * (CIS2 / 2) * NPIX + ty * TW + tx;
+    }
+    const int a2_base = h * (CIS2 / 2) * BM + t.wm * 64 + l32;
+    uint32_t off2[N2];  // chunk-invariant byte offsets of the staged Z elements
+#pragma unroll
+    for (int e = 0; e < N2; ++e) {
+      const int idx = tid + e * 256;
+      const int ci = idx / NPIX, px = idx % NPIX;
+      const int oy = t.ty0 + px / TW, ox = t.tx0 + px % TW;
+      const bool ok = idx < E2 && oy < p.ho && ox < p.wo;
+      off2[e] = ok ? (uint32_t)(ci * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
+    }
+    for (int c0 = 0; c0 < p.p2_c; c0 += CIS2) {
+      const auto rz = make_srd(z2 + (size_t)c0 * plane, (uint32_t)((p.p2_c - c0) * plane * 4));
+      float v2[N2];
+#pragma unroll
+      for (int e = 0; e < N2; ++e) v2[e] = s2 * buf_ld(rz, off2[e]);
+      f32x4 wv2[NW2];
+#pragma unroll
+      for (int e = 0; e < NW2; ++e) {
+        const int idx = tid + e * 256;
+        if (idx < WQ2) {
+          const int kr = idx / (BM / 4), c4 = idx - kr * (BM / 4);
+          wv2[e] = *reinterpret_cast<const f32x4*>(w2 + (size_t)(c0 + kr) * p.cout_pad + t.co0 +
+                                                  c4 * 4);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < N2; ++e) {
+        const int idx = tid + e * 256;
+        if (idx < E2) lds_in[idx] = v2[e];
+      }
+#pragma unroll
+      for (int e = 0; e < NW2; ++e) {
+        const int idx = tid + e * 256;
+        if (idx < WQ2) *reinterpret_cast<f32x4*>(lds_w + idx * 4) = wv2[e];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < CIS2 / 2; ++s) {
+        float a[2], b[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = lds_w[a2_base + s * BM + i * 32];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] = lds_in[b2_base[j] + s * NPIX];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // ReLU + MaxPool2d(2,2) backward (unpool(up_dp) * (up_z > 0), argmax of the
+  // relu'd window recomputed from up_z, first max in row-major order wins).  With the
+  // row-pair mapping the window is this lane's two tiles x its partner lane (l32^1):
+  // two z loads and one dp load per lane per register instead of six per element.
+  float dpv[2][16];
+  uint32_t dsel[2] = {0u, 0u};  // bit i*16+r of dsel[j]: element (i, j, r) takes dpv
+  if constexpr (ROWPAIR) {
+    if (p.up_dp) {
+      const int hp = p.ho >> 1, wp = p.wo >> 1;
+      const int ty0r = t.ty0 + (t.wn >> 1) * 2, oxr = t.tx0 + (t.wn & 1) * 32 + l32;
+      const int py = ty0r >> 1, px = oxr >> 1, par = l32 & 1;
+      const bool win = py < hp && px < wp;   // both rows, both columns exist
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = min(t.co0 + t.wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h,
+                             p.cout - 1);
+          const float* zc = p.up_z + ((size_t)n * p.cout + co) * plane;
+          const int oyc = min(ty0r, p.ho - 1), oxc = min(oxr, p.wo - 1);
+          const float za = zc[(size_t)oyc * p.wo + oxc];                      // row 2py
+          const float zb = zc[(size_t)min(oyc + 1, p.ho - 1) * p.wo + oxc];   // row 2py+1
+          const float pa = __shfl_xor(za, 1, 64), pb = __shfl_xor(zb, 1, 64);
+          const float z0 = fmaxf(par ? pa : za, 0.f), z1 = fmaxf(par ? za : pa, 0.f);
+          const float z2v = fmaxf(par ? pb : zb, 0.f), z3 = fmaxf(par ? zb : pb, 0.f);
+          int bi = 0;
+          float best = z0;
+          if (z1 > best) { best = z1; bi = 1; }
+          if (z2v > best) { best = z2v; bi = 2; }
+          if (z3 > best) { bi = 3; }
+          dpv[i][r] = win ? p.up_dp[(((size_t)n * p.cout + co) * hp + py) * wp + px] : 0.f;
+          // element (row j, column parity par) is window slot j*2 + par
+          if (win && bi == par && za > 0.f) dsel[0] |= 1u << (i * 16 + r);
+          if (win && bi == 2 + par && zb > 0.f) dsel[1] |= 1u << (i * 16 + r);
+        }
+    }
+  }
+
+  float vmax = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int ty, tx;
+    tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
+    const int oy = t.ty0 + ty, ox = t.tx0 + tx;
+    if (oy >= p.ho || ox >= p.wo) continue;
+    const size_t pofs = (size_t)oy * p.wo + ox;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = t.co0 + t.wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co >= p.cout) continue;
+        const size_t o = ((size_t)n * p.cout + co) * plane + pofs;
+        float v = acc[i][j][r];
+        if (!mask_done) {
+          if (p.acc_scale) v *= *p.acc_scale;
+          if (p.mask) v = p.mask[o] > 0.f ? v : 0.f;
+        }
+        if (p.bias) v += p.bias[co];
+        if (ROWPAIR) {
+          if ((dsel[j] >> (i * 16 + r)) & 1u) v += dpv[i][r];
+        } else if (p.up_dp) {
+          // ReLU + MaxPool2d(2,2) backward, argmax recomputed from up_z
+          const float* zc = p.up_z + ((size_t)n * p.cout + co) * plane;
+          const int hp = p.ho >> 1, wp = p.wo >> 1;
+          const int py = oy >> 1, px2 = ox >> 1;
+          if (py < hp && px2 < wp && zc[pofs] > 0.f) {
+            const float* q = zc + (size_t)(2 * py) * p.wo + 2 * px2;
+            const float z0 = fmaxf(q[0], 0.f), z1 = fmaxf(q[1], 0.f);
+            const float z2v = fmaxf(q[p.wo], 0.f), z3 = fmaxf(q[p.wo + 1], 0.f);
+            int bi = 0;
+            float best = z0;
+            if (z1 > best) { best = z1; bi = 1; }
+            if (z2v > best) { best = z2v; bi = 2; }
+            if (z3 > best) { bi = 3; }
+            if (bi == ((oy & 1) * 2 + (ox & 1)))
+              v += p.up_dp[(((size_t)n * p.cout + co) * hp + py) * wp + px2];
+          }
+        }
+        if (p.aux) v += p.aux_scale * p.aux[o];
+        if (p.accumulate) v += p.y[o];
+        if (p.relu_out) v = fmaxf(v, 0.f);
+        p.y[o] = v;
+        if (ROWPAIR) acc[i][j][r] = v;  // kept for the fused pooled output
+        vmax = fmaxf(vmax, fabsf(v)) ;
+        if (v != v) vmax = v;  // NaN: keep it (fmaxf would drop it)
+      }
+    }
+  }
+  if (ROWPAIR && p.pool_out) {
+    // relu(maxpool2x2(y)) = maxpool2x2(relu(y)) -> pool_out [n][cout][ho/2][wo/2]
+    // (torch MaxPool2d floor mode: a window needs both rows and both columns)
+    const int hp = p.ho >> 1, wp = p.wo >> 1;
+    const int py = (t.ty0 + (t.wn >> 1) * 2) >> 1;
+    const int px = (t.tx0 + (t.wn & 1) * 32 + l32) >> 1;
+    const bool ok = py < hp && px < wp && !(l32 & 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float m = fmaxf(acc[i][0][r], acc[i][1][r]);
+        if (acc[i][0][r] != acc[i][0][r]) m = acc[i][0][r];
+        const float o = __shfl_xor(m, 1, 64);
+        m = (o != o) ? o : ((m != m) ? m : fmaxf(m, o));
+        m = (m != m) ? m : fmaxf(m, 0.f);
+        const int co = t.co0 + t.wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (ok && co < p.cout)
+          p.pool_out[(((size_t)n * p.cout + co) * hp + py) * wp + px] = m;
+      }
+  }
+  if (p.out_amax) block_max_to(p.out_amax, vmax);
+}
+
+}  // namespace stx

@@ -15,7 +15,8 @@ from . import _native as N
 from ._native import ConvParams, check, lib
 
 __all__ = [
-    "conv_weight_dims", "conv_weight_prep", "conv2d", "conv_out_hw", "conv2d_wgrad",
+    "conv_weight_dims", "conv_weight_prep", "conv_weight_prep16", "split_eligible", "amax",
+    "conv2d", "conv_out_hw", "conv2d_wgrad",
     "bias_grad", "gram", "style_loss", "gram_bwd", "mse", "diff_scale", "loss_combine",
     "maxpool2x2", "maxpool2x2_bwd", "relupool_bwd", "relu", "relu_bwd", "adam_step",
     "instnorm_fwd", "instnorm_bwd", "upsample2x", "upsample2x_bwd", "tv_loss",
@@ -80,6 +81,36 @@ def conv_weight_prep(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
     return wt
 
 
+def conv_weight_prep16(w: torch.Tensor, transpose: bool = False):
+    """[cout][cin][3][3] -> (fp16 hi/lo split slab, device max|w|) for the split-MFMA
+    path of stx_conv2d (transpose=True: the data-gradient slab)."""
+    _req(w, "weight")
+    cout, cin, ks, _ = w.shape
+    L = lib()
+    nb = L.stx_conv_weight16_bytes(cin, cout, ks, int(transpose))
+    if nb == 0:
+        raise N.NativeError(f"no fp16-split slab for a {ks}x{ks} conv")
+    wt16 = torch.empty(nb, device=w.device, dtype=torch.uint8)
+    w_amax = torch.empty(1, device=w.device, dtype=torch.float32)
+    check(L.stx_conv_weight_prep16(w.data_ptr(), wt16.data_ptr(), w_amax.data_ptr(), cout, cin,
+                                   ks, int(transpose), _stream()), "conv_weight_prep16")
+    return wt16, w_amax
+
+
+def split_eligible(cin, cout, ks, stride=1):
+    """Shapes stx_conv2d runs on the fp16 hi/lo split MFMA kernel (conv16.hip)."""
+    return ks == 3 and stride == 1 and cin >= 16 and cout > 4
+
+
+def amax(x: torch.Tensor, out=None):
+    """Device scalar max|x| (stx_amax)."""
+    _req(x, "x")
+    if out is None:
+        out = torch.empty(1, device=x.device, dtype=torch.float32)
+    check(lib().stx_amax(x.data_ptr(), x.numel(), out.data_ptr(), _stream()), "stx_amax")
+    return out
+
+
 def virtual_hw(h, w, in_mode, hv=None, wv=None):
     if in_mode in (N.STX_IN_RAW, N.STX_IN_RELU):
         return h, w
@@ -97,10 +128,15 @@ def conv_out_hw(hv, wv, ks, stride, pad):
 def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=None,
            out=None, mask=None, aux=None, aux_scale=0.0, acc_scale=None, accumulate=False,
            relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
-           p2_scale=None, up_dp=None, up_z=None):
+           p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
+           pool_out=None):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
-    up_dp/up_z: fused ReLU+MaxPool2d backward epilogue."""
+    up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
+    wt16=(slab, w_amax) from conv_weight_prep16 selects the fp16 hi/lo split MFMA
+    kernel for eligible shapes; in_amax (device >= max|x|) is computed when absent;
+    out_amax (device scalar, zeroed by the caller) receives max|out|; pool_out
+    [n][cout][ho/2][wo/2] receives maxpool2x2(relu(out)) (split path, wo > 32)."""
     _req(x, "x")
     n, c, h, w = x.shape
     assert c == cin, (c, cin)
@@ -127,6 +163,16 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         p.p2_wt_batch_stride = p2_coef.shape[-1] * p2_coef.shape[-2]
     if up_dp is not None:
         p.up_dp, p.up_z = up_dp.data_ptr(), up_z.data_ptr()
+    if wt16 is not None and split_eligible(cin, cout, ks, stride) and wt_batch_stride == 0:
+        if in_amax is None:
+            in_amax = amax(x)
+        p.wt16, p.w_amax, p.in_amax = wt16[0].data_ptr(), wt16[1].data_ptr(), in_amax.data_ptr()
+    if out_amax is not None:
+        p.out_amax = out_amax.data_ptr()
+    if pool_out is not None:
+        _req(pool_out, "pool_out")
+        assert pool_out.shape == (n, cout, ho // 2, wo // 2), pool_out.shape
+        p.pool_out = pool_out.data_ptr()
     check(lib().stx_conv2d(C.byref(p), _stream()), "stx_conv2d")
     return out
 
@@ -208,13 +254,14 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
     return loss, (coef if want_coef else None)
 
 
-def gram_bwd_fused(coef, z, out=None, acc_scale=None, up_dp=None, aux=None, aux_scale=0.0):
+def gram_bwd_fused(coef, z, out=None, acc_scale=None, up_dp=None, aux=None, aux_scale=0.0,
+                   out_amax=None):
     """out = s*A[n].z[n] (+ unpool(up_dp)*(z>0)) (+ aux_scale*aux): the Gram backward
     as a 1x1 MFMA conv with the ReLU+MaxPool backward fused into its epilogue."""
     b, c = z.shape[:2]
     return conv2d(z, coef, c, c, 1, pad=0, out=out, acc_scale=acc_scale, aux=aux,
                   aux_scale=aux_scale, wt_batch_stride=coef.shape[-1] * coef.shape[-2],
-                  up_dp=up_dp, up_z=z if up_dp is not None else None)
+                  up_dp=up_dp, up_z=z if up_dp is not None else None, out_amax=out_amax)
 
 
 def gram_bwd(coef, z, dz=None, acc_scale=None, mask=None, aux=None, aux_scale=0.0,

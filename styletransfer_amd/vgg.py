@@ -74,6 +74,8 @@ class VGGFeatures:
     def __init__(self, convs, device):
         self.device = torch.device(device)
         self.w, self.b, self.wt, self.wtT = [], [], [], []
+        # fp16 hi/lo split slabs (conv16.hip) where the shape is eligible, else None
+        self.wt16, self.wtT16 = [], []
         for (w, b), (cout, cin) in zip(convs, VGG_CONV_SHAPES):
             wt = torch.as_tensor(np.ascontiguousarray(w), dtype=torch.float32).to(self.device)
             bt = torch.as_tensor(np.ascontiguousarray(b), dtype=torch.float32).to(self.device)
@@ -82,6 +84,11 @@ class VGGFeatures:
             self.b.append(bt)
             self.wt.append(ops.conv_weight_prep(wt))
             self.wtT.append(ops.conv_weight_prep(wt, transpose=True))
+            split = os.environ.get("STX_CONV_SPLIT", "1") != "0"
+            self.wt16.append(ops.conv_weight_prep16(wt) if split and
+                             ops.split_eligible(cin, cout, 3) else None)
+            self.wtT16.append(ops.conv_weight_prep16(wt, transpose=True) if split and
+                              ops.split_eligible(cout, cin, 3) else None)
 
     @classmethod
     def from_modules(cls, convs, device):
@@ -89,16 +96,46 @@ class VGGFeatures:
         return cls([(c.weight.detach().cpu().numpy(), c.bias.detach().cpu().numpy())
                     for c in convs], device)
 
-    def conv(self, l, x, out=None):
+    def conv(self, l, x, out=None, in_amax=None, out_amax=None):
         cout, cin = VGG_CONV_SHAPES[l]
         return ops.conv2d(x, self.wt[l], cin, cout, 3, in_mode=IN_MODES[l], bias=self.b[l],
-                          out=out)
+                          out=out, wt16=self.wt16[l], in_amax=in_amax, out_amax=out_amax)
 
-    def forward(self, x, upto=5, outs=None):
-        """[Z1..Z_upto] (pre-ReLU conv outputs)."""
-        zs, cur = [], x
+    def dgrad(self, l, dz, out, **kw):
+        """d/d(conv_l input, after its loader transform) of dz = d/dZ_l."""
+        cout, cin = VGG_CONV_SHAPES[l]
+        return ops.conv2d(dz, self.wtT[l], cout, cin, 3, out=out, wt16=self.wtT16[l], **kw)
+
+    def fuses_pool(self, l, wo):
+        """conv l can write relu+maxpool of its output for conv l+1 (split path)."""
+        return (l + 1 < len(IN_MODES) and IN_MODES[l + 1] == N.STX_IN_RELU_POOL2
+                and self.wt16[l] is not None and self.wt16[l + 1] is not None and wo > 32)
+
+    def forward(self, x, upto=5, outs=None, amax=None, pools=None):
+        """[Z1..Z_upto] (pre-ReLU conv outputs).  amax: device [>=5] slots, zeroed by
+        the caller; slot l+1 receives max|Z_l| (the next split conv's input scale).
+        Where fuses_pool holds, conv l also writes P = maxpool(relu(Z_l)) (into
+        pools[l] if given) and conv l+1 reads P directly."""
+        zs, cur, pin = [], x, None
         for l in range(upto):
-            cur = self.conv(l, cur, None if outs is None else outs[l])
+            cout, cin = VGG_CONV_SHAPES[l]
+            src, mode = cur, IN_MODES[l]
+            if mode == N.STX_IN_RELU_POOL2 and pin is not None:
+                src, mode = pin, N.STX_IN_RAW
+            kw = {}
+            if amax is not None:
+                kw = dict(in_amax=amax[l:l + 1] if l > 0 else None,
+                          out_amax=amax[l + 1:l + 2])
+            pin = None
+            if l + 1 < upto and self.fuses_pool(l, src.shape[3]):
+                shp = (src.shape[0], cout, src.shape[2] // 2, src.shape[3] // 2)
+                pin = pools[l] if pools is not None and pools[l] is not None else \
+                    torch.empty(shp, device=src.device, dtype=torch.float32)
+                if pools is not None:
+                    pools[l] = pin
+                kw["pool_out"] = pin
+            cur = ops.conv2d(src, self.wt[l], cin, cout, 3, in_mode=mode, bias=self.b[l],
+                             out=None if outs is None else outs[l], wt16=self.wt16[l], **kw)
             zs.append(cur)
         return zs
 
@@ -118,6 +155,8 @@ class LossState:
     fmean: torch.Tensor = None                  # [2] feature loss, its mse
     folded: bool = False                        # loss weights baked into coef
     alpha: float = 0.0
+    amax: torch.Tensor = None                   # [16] max|.| slots of split-conv inputs
+    pools: list = field(default_factory=lambda: [None] * 5)  # fused relu+pool outputs
 
 
 def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
@@ -132,7 +171,11 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     upstream gradient vector (autograd case)."""
     if st is None:
         st = LossState()
-    st.z = feat.forward(x, 5, st.z if st.z else None)
+    if st.amax is None:
+        st.amax = torch.zeros(16, device=x.device, dtype=torch.float32)
+    else:
+        st.amax.zero_()
+    st.z = feat.forward(x, 5, st.z if st.z else None, amax=st.amax, pools=st.pools)
     if st.losses is None:
         # [style x5, content, feature, feature-mse]
         st.losses = torch.empty(N_LOSSES + 1, device=x.device, dtype=torch.float32)
@@ -183,36 +226,40 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
 
     folded = st.folded
     s = (lambda i: None) if folded else (lambda i: g[i:i + 1])
+    am = st.amax  # slots 0..5: forward; 6..9: backward split-conv inputs
     # conv3_1 output: dZ5 = A5 Z5
-    dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4))
+    dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4),
+                             out_amax=am[6:7])
     # -> grad wrt pool(relu Z4)
     n4 = (B, 128, z[3].shape[2] // 2, z[3].shape[3] // 2)
-    dp2 = ops.conv2d(dz5, feat.wtT[4], 256, 128, 3, out=buf("dp2", n4))
+    dp2 = feat.dgrad(4, dz5, buf("dp2", n4), in_amax=am[6:7])
     # dZ4 = unpool(dP2)*[Z4>0] + A4 Z4 (+ content)
     dz4 = ops.gram_bwd_fused(st.coef[3], z[3], out=buf("dz4", z[3].shape), acc_scale=s(3),
-                             up_dp=dp2, aux=st.c4 if folded else None, aux_scale=-st.alpha)
+                             up_dp=dp2, aux=st.c4 if folded else None, aux_scale=-st.alpha,
+                             out_amax=am[7:8] if folded else None)
     n = z[3].numel()
+    dz4_amax = am[7:8] if folded else None
     if not folded:
         ops.diff_scale(z[3], st.c4, 2.0 / n, s1=g[5:6], out=dz4, accumulate=True)
         if feature_grad:
             ops.diff_scale(z[3], st.c4, 4.0 / (float(n) * float(n)), s1=g[6:7],
                            s2=st.fmean[1:2], relu=True, out=dz4, accumulate=True)
     # dZ3 = conv2_2^T(dZ4)*[Z3>0] + A3 Z3
-    dz3 = ops.conv2d(dz4, feat.wtT[3], 128, 128, 3, mask=z[2], out=buf("dz3", z[2].shape),
-                     p2_z=z[2], p2_coef=st.coef[2], p2_scale=s(2))
+    dz3 = feat.dgrad(3, dz4, buf("dz3", z[2].shape), mask=z[2], p2_z=z[2],
+                     p2_coef=st.coef[2], p2_scale=s(2), in_amax=dz4_amax, out_amax=am[8:9])
     # -> grad wrt pool(relu Z2)
     n2 = (B, 64, z[1].shape[2] // 2, z[1].shape[3] // 2)
-    dp1 = ops.conv2d(dz3, feat.wtT[2], 128, 64, 3, out=buf("dp1", n2))
+    dp1 = feat.dgrad(2, dz3, buf("dp1", n2), in_amax=am[8:9])
     dz2 = ops.gram_bwd_fused(st.coef[1], z[1], out=buf("dz2", z[1].shape), acc_scale=s(1),
-                             up_dp=dp1)
+                             up_dp=dp1, out_amax=am[9:10])
     # dZ1 = conv1_2^T(dZ2)*[Z1>0] + A1 Z1
-    dz1 = ops.conv2d(dz2, feat.wtT[1], 64, 64, 3, mask=z[0], out=buf("dz1", z[0].shape),
-                     p2_z=z[0], p2_coef=st.coef[0], p2_scale=s(0))
+    dz1 = feat.dgrad(1, dz2, buf("dz1", z[0].shape), mask=z[0], p2_z=z[0],
+                     p2_coef=st.coef[0], p2_scale=s(0), in_amax=am[9:10])
     # conv1_1 dgrad -> image
     xs = (B, 3, z[0].shape[2], z[0].shape[3])
     if dx is None:
         dx = torch.empty(xs, device=z[0].device, dtype=torch.float32)
-    return ops.conv2d(dz1, feat.wtT[0], 64, 3, 3, out=dx)
+    return feat.dgrad(0, dz1, dx)
 
 
 def content_target(feat: VGGFeatures, content, out=None):

@@ -257,12 +257,54 @@ def test_fast_st_trainer_matches_api(itn_case, dev):
     total.backward()
     ga = [p.grad.clone() for p in a.parameters()]
     opt.step()
+    p0 = [q.detach().clone() for q in b.parameters()]
     tr = FastStTrainer(b, style)
     tb = tr.step(batch)
     assert rel(tb, total) < 1e-5
-    for p, q, gq in zip(a.parameters(), b.parameters(), ga):
+    gmax = max(float(g.norm()) for g in ga)
+    for p, q, gq, q0 in zip(a.parameters(), b.parameters(), ga, p0):
+        if float(gq.norm()) < 1e-6 * gmax:
+            # conv biases feeding InstanceNorm: the exact gradient is 0 and both sides
+            # hold fp32 rounding noise (see test_itn_forward_backward_params)
+            assert float(q.grad.norm()) < 1e-6 * gmax
+            continue
         assert rel(q.grad, gq) < 1e-5
-        assert rel(q.detach(), p.detach()) < 1e-5
+        # Adam step 1 moves each element by ~lr*sign(g): elements whose gradient is
+        # at rounding-noise level (|g| < 1e-4 max|g|) may step either way; the rest
+        # must take the same step
+        da, db = (p.detach() - q0), (q.detach() - q0)
+        big = gq.abs() >= 1e-4 * gq.abs().max()
+        assert rel(db[big], da[big]) < 1e-4
+        assert float((db - da).abs().max()) <= 2.0001e-3
+
+
+def test_determinism(itn_case, dev):
+    """Bit-reproducible runs: no float atomics, fixed reduction orders (the split
+    convs' per-tensor scales come from atomicMax, which is order-independent)."""
+    from styletransfer_amd.train import FastStTrainer
+    d, _ = itn_case
+    style = T(d["style"], dev)
+    batch = T(d["batch"], dev)
+    sd = {k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)}
+    outs = []
+    for _ in range(2):
+        net = network.ImageTransformNet(style, 2)
+        net.load_state_dict(sd)
+        tr = FastStTrainer(net, style)
+        tr.step(batch)
+        tr.step(batch)
+        outs.append(tr.flat.detach().clone())
+    assert torch.equal(outs[0], outs[1])
+    xs = []
+    feat = V.VGGFeatures(V.load_vgg19_weights(), dev)
+    s = torch.from_numpy(W.synthetic_image(5, (1, 3, 96, 96))).to(dev)
+    c = torch.from_numpy(W.synthetic_image(6, (1, 3, 96, 96))).to(dev)
+    for _ in range(2):
+        eng = V.GatysEngine(feat, s, c)
+        for _ in range(3):
+            eng.step()
+        xs.append(eng.x.clone())
+    assert torch.equal(xs[0], xs[1])
 
 
 def test_dp_gradient_equivalence(itn_case, dev):

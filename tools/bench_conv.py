@@ -27,6 +27,7 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="", help="run only cases whose name contains this")
+    ap.add_argument("--no-split", action="store_true", help="fp32 MFMA kernels only")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -48,13 +49,21 @@ def main():
         if args.only not in name:
             continue
         x = torch.randn(n, cin, h, w, generator=g).to(dev)
-        wt = ops.conv_weight_prep(torch.randn(cout, cin, ks, ks, generator=g).to(dev) * 0.05)
+        wraw = torch.randn(cout, cin, ks, ks, generator=g).to(dev) * 0.05
+        wt = ops.conv_weight_prep(wraw)
         hv, wv = ops.virtual_hw(h, w, mode)
         ho, wo = ops.conv_out_hw(hv, wv, ks, s, ks // 2)
         out = torch.empty(n, cout, ho, wo, device=dev)
         ms = ev(lambda: ops.conv2d(x, wt, cin, cout, ks, stride=s, in_mode=mode, out=out))
         gf = 2.0 * n * cin * cout * ks * ks * ho * wo / 1e9
-        print(f"{name:32s} {ms * 1e3:9.1f} us  {gf / ms:8.2f} TFLOP/s")
+        line = f"{name:32s} fp32 {ms * 1e3:9.1f} us {gf / ms:7.2f} TF"
+        if not args.no_split and ops.split_eligible(cin, cout, ks, s):
+            w16 = ops.conv_weight_prep16(wraw)
+            am = ops.amax(x)
+            ms16 = ev(lambda: ops.conv2d(x, wt, cin, cout, ks, stride=s, in_mode=mode, out=out,
+                                         wt16=w16, in_amax=am))
+            line += f" | f16x3 {ms16 * 1e3:9.1f} us {gf / ms16:7.2f} TF"
+        print(line, flush=True)
     for name, n, c, h in (("gram C64 512^2", 1, 64, 512), ("gram C128 256^2", 1, 128, 256),
                           ("gram C256 128^2", 1, 256, 128), ("gram C64 B8 256^2", 8, 64, 256)):
         if args.only not in name:
