@@ -580,8 +580,9 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   const long long in_bytes = 4LL * p.cin * p.h * p.w;
   const long long wt_bytes = 4LL * p.cin_pad * p.ks * p.ks * p.cout_pad;
   const long long p2_bytes = p.p2_z ? 4LL * p.p2_c * p.ho * p.wo : 0;
+  const long long out_bytes = 4LL * p.cout * p.ho * p.wo;  // epilogue descriptors
   if (in_bytes >= (long long)BUF_OOB / 2 || wt_bytes >= (long long)BUF_OOB / 2 ||
-      p2_bytes >= (long long)BUF_OOB / 2) {
+      p2_bytes >= (long long)BUF_OOB / 2 || out_bytes >= (long long)BUF_OOB / 2) {
     set_error("stx_conv2d: per-image tensor too large (>= 1 GiB)");
     return STX_E_INVALID;
   }

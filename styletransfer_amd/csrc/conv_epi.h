@@ -217,57 +217,89 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_con
     }
   }
 
-  float vmax = 0.f;
+  // Final pass.  All tensor accesses go through buffer descriptors based at this
+  // wave's first output row co_w: the per-element byte offset is one VGPR add of a
+  // per-register row constant (SGPR) to a per-lane pixel offset, rows past cout
+  // fall outside num_records and pixels outside the image carry BUF_OOB, so loads
+  // read 0 and stores are dropped by the hardware -- no 64-bit address math and no
+  // per-element bounds branches.
+  const int co_w = t.co0 + t.wm * 64;
+  const uint32_t rows = (uint32_t)max(0, p.cout - co_w);
+  const size_t wofs = ((size_t)n * p.cout + co_w) * plane;
+  const uint32_t pb = (uint32_t)plane * 4u;
+  const auto ry = make_srd(p.y + wofs, rows * pb);
+  const auto rmask = make_srd(p.mask ? p.mask + wofs : p.y, rows * pb);
+  const auto raux = make_srd(p.aux ? p.aux + wofs : p.y, rows * pb);
+  uint32_t vo[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     int ty, tx;
     tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
     const int oy = t.ty0 + ty, ox = t.tx0 + tx;
-    if (oy >= p.ho || ox >= p.wo) continue;
-    const size_t pofs = (size_t)oy * p.wo + ox;
+    vo[j] = (oy < p.ho && ox < p.wo) ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u
+                                     : BUF_OOB;
+  }
+  float bias_r[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      bias_r[i][r] = (p.bias && co < p.cout) ? p.bias[co] : 0.f;
+    }
+  const float sc = (!mask_done && p.acc_scale) ? *p.acc_scale : 1.f;
+  uint32_t vmax_u = 0u;  // max |v| as IEEE bits: NaN (above inf) propagates
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = t.co0 + t.wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (co >= p.cout) continue;
-        const size_t o = ((size_t)n * p.cout + co) * plane + pofs;
+        const uint32_t o = vo[j] + (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * pb;
         float v = acc[i][j][r];
         if (!mask_done) {
-          if (p.acc_scale) v *= *p.acc_scale;
-          if (p.mask) v = p.mask[o] > 0.f ? v : 0.f;
+          v *= sc;
+          if (p.mask) v = buf_ld(rmask, o) > 0.f ? v : 0.f;
         }
-        if (p.bias) v += p.bias[co];
+        v += bias_r[i][r];
         if (ROWPAIR) {
           if ((dsel[j] >> (i * 16 + r)) & 1u) v += dpv[i][r];
         } else if (p.up_dp) {
           // ReLU + MaxPool2d(2,2) backward, argmax recomputed from up_z
-          const float* zc = p.up_z + ((size_t)n * p.cout + co) * plane;
-          const int hp = p.ho >> 1, wp = p.wo >> 1;
-          const int py = oy >> 1, px2 = ox >> 1;
-          if (py < hp && px2 < wp && zc[pofs] > 0.f) {
-            const float* q = zc + (size_t)(2 * py) * p.wo + 2 * px2;
-            const float z0 = fmaxf(q[0], 0.f), z1 = fmaxf(q[1], 0.f);
-            const float z2v = fmaxf(q[p.wo], 0.f), z3 = fmaxf(q[p.wo + 1], 0.f);
-            int bi = 0;
-            float best = z0;
-            if (z1 > best) { best = z1; bi = 1; }
-            if (z2v > best) { best = z2v; bi = 2; }
-            if (z3 > best) { bi = 3; }
-            if (bi == ((oy & 1) * 2 + (ox & 1)))
-              v += p.up_dp[(((size_t)n * p.cout + co) * hp + py) * wp + px2];
+          const int co = co_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          int ty, tx;
+          tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
+          const int oy = t.ty0 + ty, ox = t.tx0 + tx;
+          if (co < p.cout && oy < p.ho && ox < p.wo) {
+            const size_t pofs = (size_t)oy * p.wo + ox;
+            const float* zc = p.up_z + ((size_t)n * p.cout + co) * plane;
+            const int hp = p.ho >> 1, wp = p.wo >> 1;
+            const int py = oy >> 1, px2 = ox >> 1;
+            if (py < hp && px2 < wp && zc[pofs] > 0.f) {
+              const float* q = zc + (size_t)(2 * py) * p.wo + 2 * px2;
+              const float z0 = fmaxf(q[0], 0.f), z1 = fmaxf(q[1], 0.f);
+              const float z2v = fmaxf(q[p.wo], 0.f), z3 = fmaxf(q[p.wo + 1], 0.f);
+              int bi = 0;
+              float best = z0;
+              if (z1 > best) { best = z1; bi = 1; }
+              if (z2v > best) { best = z2v; bi = 2; }
+              if (z3 > best) { bi = 3; }
+              if (bi == ((oy & 1) * 2 + (ox & 1)))
+                v += p.up_dp[(((size_t)n * p.cout + co) * hp + py) * wp + px2];
+            }
           }
         }
-        if (p.aux) v += p.aux_scale * p.aux[o];
-        if (p.accumulate) v += p.y[o];
+        if (p.aux) v += p.aux_scale * buf_ld(raux, o);
+        if (p.accumulate) v += buf_ld(ry, o);
         if (p.relu_out) v = fmaxf(v, 0.f);
-        p.y[o] = v;
+        buf_st(ry, o, v);
         if (ROWPAIR) acc[i][j][r] = v;  // kept for the fused pooled output
-        vmax = fmaxf(vmax, fabsf(v)) ;
-        if (v != v) vmax = v;  // NaN: keep it (fmaxf would drop it)
+        // elements outside the output (dropped stores) must not count
+        if (o < rows * pb) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
       }
     }
   }
+  const float vmax = __uint_as_float(vmax_u);
   if (ROWPAIR && p.pool_out) {
     // relu(maxpool2x2(y)) = maxpool2x2(relu(y)) -> pool_out [n][cout][ho/2][wo/2]
     // (torch MaxPool2d floor mode: a window needs both rows and both columns)

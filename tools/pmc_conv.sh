@@ -1,8 +1,10 @@
+# PMC passes (one rocprofv3 run each) over the conv1_2 microbench: issue/wait
+# breakdown, LDS behaviour, HBM bytes.  gpurun -- 'bash tools/pmc_conv.sh [filter]'
 cd /tmp && export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-cd $R
-timeout -k 10 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc1 -- python tools/bench_conv.py --only conv1_2 > gpurun_out/pmc1.log 2>&1 &&
-timeout -k 10 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_UNALIGNED_STALL --output-format csv -d gpurun_out/pmc2 -- python tools/bench_conv.py --only conv1_2 > gpurun_out/pmc2.log 2>&1 &&
-timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc3 -- python tools/bench_conv.py --only conv1_2 > gpurun_out/pmc3.log 2>&1 &&
-timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc4 -- python tools/bench_conv.py --only conv1_2 > gpurun_out/pmc4.log 2>&1
-echo rc $?
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+F=${1:-conv1_2}
+run() { timeout -s KILL 90 rocprofv3 --pmc $2 --output-format csv -d gpurun_out/$1 -o run -- python3 tools/bench_conv.py --only "$F" > gpurun_out/$1.log 2>&1; echo "$1 rc $?"; }
+run pmc1 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" &&
+run pmc2 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES" &&
+run pmc_fetch "FETCH_SIZE" &&
+run pmc_write "WRITE_SIZE"
