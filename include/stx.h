@@ -91,6 +91,12 @@ typedef struct stx_conv_params {
    * maxpool(relu(y)) (torch floor mode), written beside y.  Split path (wt16) with
    * wo > 32 only; the next conv then reads it with STX_IN_RAW. */
   float* pool_out;
+  /* split path only: device scalar >= max|p2_z| (required with p2_z and wt16; the
+   * Gram-backward phase then also runs on the fp16 hi/lo split MFMA, A scaled per
+   * block by its own max).  A 1x1 conv with per-image weights (the Gram backward
+   * dz = s*A[n].z, stx_gram_bwd) given in_amax and wt16 = (void*)1 runs as that
+   * phase alone on the split kernel (no ReLU mask allowed there). */
+  const float* p2_amax;
 } stx_conv_params;
 
 int stx_version(void);
@@ -136,10 +142,12 @@ int stx_bias_grad(const float* dy, float* db, int n, int c, int hw, int accumula
                   void* ws, size_t ws_bytes, void* stream);
 
 /* Gram: G[b] = F_b F_b^T * scale, F_b = z[b] viewed [c][hw].  Split-K MFMA +
- * deterministic reduction. */
+ * deterministic reduction.  z_amax (optional device scalar >= max|z|, e.g. the
+ * producing conv's out_amax): with it and hw % 8 == 0 the partials run on the fp16
+ * hi/lo split MFMA (fp32-level accuracy), else on fp32 MFMA. */
 size_t stx_gram_ws(int b, int c, int hw);
 int stx_gram(const float* z, float* g, int b, int c, int hw, float scale,
-             void* ws, size_t ws_bytes, void* stream);
+             const float* z_amax, void* ws, size_t ws_bytes, void* stream);
 
 /* Style loss forward + backward coefficients (StyleLoss.forward):
  *   G = gram(z)/(c*hw);  loss = mean((G - T)^2) over b*c*c  -> *loss (device scalar)
@@ -149,7 +157,8 @@ int stx_gram(const float* z, float* g, int b, int c, int hw, float scale,
 int stx_gram_coef_pitch(int c);
 int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
                    float* loss, int b, int c, int hw, int target_batched, float weight,
-                   float diag_alpha, void* ws, size_t ws_bytes, void* stream);
+                   float diag_alpha, const float* z_amax, void* ws, size_t ws_bytes,
+                   void* stream);
 /* dz (+)= s * A[b]·z[b] (+ aux_scale*aux) — Gram backward as a 1x1 MFMA conv with
  * per-image weights; z viewed [b][c][h][w]; s = *acc_scale_dev (or 1 if NULL) */
 int stx_gram_bwd(const float* coef, const float* z, float* dz, int b, int c, int h, int w,

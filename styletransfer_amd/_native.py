@@ -35,7 +35,7 @@ class ConvParams(C.Structure):
         ("p2_z", vp), ("p2_wt", vp), ("p2_scale", vp), ("p2_c", i32), ("p2_wt_batch_stride", i64),
         ("up_dp", vp), ("up_z", vp),
         ("wt16", vp), ("w_amax", vp), ("in_amax", vp), ("out_amax", vp),
-        ("pool_out", vp),
+        ("pool_out", vp), ("p2_amax", vp),
     ]
 
 
@@ -55,9 +55,10 @@ SIGNATURES = {
     "stx_bias_grad_ws": (sz, [i32, i32]),
     "stx_bias_grad": (i32, [vp, vp, i32, i32, i32, i32, vp, sz, vp]),
     "stx_gram_ws": (sz, [i32, i32, i32]),
-    "stx_gram": (i32, [vp, vp, i32, i32, i32, f32, vp, sz, vp]),
+    "stx_gram": (i32, [vp, vp, i32, i32, i32, f32, vp, vp, sz, vp]),
     "stx_gram_coef_pitch": (i32, [i32]),
-    "stx_style_loss": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, sz, vp]),
+    "stx_style_loss": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, vp, sz,
+                             vp]),
     "stx_gram_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, f32, i32, vp]),
     "stx_mse_ws": (sz, [i64]),
     "stx_mse": (i32, [vp, vp, i64, i32, i32, vp, vp, f32, vp, sz, vp]),

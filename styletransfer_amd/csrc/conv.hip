@@ -598,11 +598,35 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   // other shapes keep the fp32 MFMA kernels (wt is always required)
   if (p.wt16 && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.cout > 4 && p.cin >= 16 &&
       p.wt_batch_stride == 0) {
-    if (!p.w_amax || !p.in_amax) {
-      set_error("stx_conv2d: the wt16 path needs w_amax and in_amax");
+    if (!p.w_amax || !p.in_amax || (p.p2_z && !p.p2_amax)) {
+      set_error("stx_conv2d: the wt16 path needs w_amax, in_amax (and p2_amax with p2_z)");
       return STX_E_INVALID;
     }
     return conv2d_f16x3(p, st);
+  }
+  // 1x1 conv with per-image weights (Gram backward) as the split phase alone
+  if (p.wt16 == (const void*)1 && p.ks == 1 && p.stride == 1 && p.pad == 0 &&
+      p.wt_batch_stride != 0 && !p.p2_z) {
+    if (!p.in_amax || p.mask || p.in_mode != STX_IN_RAW) {
+      set_error("stx_conv2d: split 1x1 mode needs in_amax, no mask, raw input");
+      return STX_E_INVALID;
+    }
+    stx_conv_params q = p;
+    q.p2_z = p.x;
+    q.p2_wt = p.wt;
+    q.p2_c = p.cin;
+    q.p2_wt_batch_stride = p.wt_batch_stride;
+    q.p2_scale = p.acc_scale;
+    q.p2_amax = p.in_amax;
+    q.acc_scale = nullptr;
+    q.cin = 0;
+    q.wt_batch_stride = 0;
+    q.pad = 1;
+    q.ks = 3;
+    q.hv = p.ho;
+    q.wv = p.wo;
+    q.wt16 = nullptr;
+    return conv2d_f16x3(q, st);
   }
   if (p.pool_out) {
     set_error("stx_conv2d: pool_out is only fused on the split (wt16) path");

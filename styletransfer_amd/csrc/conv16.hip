@@ -44,9 +44,166 @@ __device__ __forceinline__ int amax_exp(float a) {
   return min(max(e, -60), 60);
 }
 
+// Split Gram-backward phase: acc (the de-scaled, masked main result) gets
+//   + s2 * sum_c A[n][c][co] * z2[n][c][pixel]
+// on the fp16 hi/lo MFMA.  z2 is scaled by sz = 2^(15 - e(p2_amax)); A' = s2 * A
+// (small, L2 resident) by its block-wide max.  The products accumulate straight into
+// acc (no second accumulator: register budget): acc is first brought to the common
+// power-of-two scale S = 2^(30 - ea - ez) (capped so |acc| * S < 2^100), A' is
+// staged with sa = S / sz (<= 2^(15 - ea): no fp16 overflow) and acc is de-scaled
+// by 1/S at the end -- all factors are powers of two, so the only roundings are
+// those of fp32 accumulation.  Per chunk of 16
+// channels: z2 tile -> LDS [P][cg][pixel], A' -> LDS [P][cg][co] (16-B units of 8
+// channels), 3 MFMAs per 32x32 tile; the next chunk's loads are in flight meanwhile.
 template <int TW>
+__device__ __forceinline__ void phase2_f16(f32x16 (&acc)[2][2], const stx_conv_params& p, int n,
+                                           int co0, int ty0, int tx0, int wave, int h, int l32,
+                                           char* smem) {
+  constexpr int NPIX = 256, BM = 64;
+  constexpr bool RP = TW == 64;
+  const int tid = threadIdx.x;
+  const size_t plane = (size_t)p.ho * p.wo;
+  const float* __restrict__ A = p.p2_wt + (size_t)n * p.p2_wt_batch_stride;
+  const int C2 = p.p2_c;
+  const float s2 = p.p2_scale ? *p.p2_scale : 1.f;
+  // max |A[c][co0 .. co0+63]| over c < C2 (float4 rows of the padded [c][cout_pad] layout)
+  float m = 0.f;
+  for (int idx = tid; idx < C2 * (BM / 4); idx += 256) {
+    const int c = idx / (BM / 4), q4 = idx - c * (BM / 4);
+    const int co = co0 + 4 * q4;
+    if (co < p.cout_pad) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(A + (size_t)c * p.cout_pad + co);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m = fmaxf(m, fabsf(v[e]));
+    }
+  }
+  __shared__ float red2[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((tid & 63) == 0) red2[tid >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red2[0], red2[1]), fmaxf(red2[2], red2[3])) * fabsf(s2);
+  // max |acc| bounds how far acc may be scaled up (|acc| * S < 2^100)
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) am = fmaxf(am, fabsf(acc[i][j][r]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+  __syncthreads();
+  if ((tid & 63) == 0) red2[tid >> 6] = am;
+  __syncthreads();
+  am = fmaxf(fmaxf(red2[0], red2[1]), fmaxf(red2[2], red2[3]));
+  const int ea = amax_exp(m), ez = amax_exp(*p.p2_amax), eacc = amax_exp(am);
+  const int ls = min(min(30 - ea - ez, 100 - eacc), 120);  // log2 S
+  const float sz = __builtin_ldexpf(1.f, 15 - ez);
+  const float sa = __builtin_ldexpf(s2, ls - (15 - ez));  // S / sz, with s2 folded in
+  {
+    const float up = __builtin_ldexpf(1.f, ls);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= up;
+  }
+
+  char* lz = smem;                     // [P][cg][256 px] x 16 B = 16 KB
+  char* la = smem + 4 * NPIX * 16;     // [P][cg][64 co]  x 16 B = 4 KB
+  uint32_t zoff;                       // this thread's staged pixel (row-major tile order)
+  {
+    const int oy = ty0 + tid / TW, ox = tx0 + tid % TW;
+    zoff = (oy < p.ho && ox < p.wo) ? (uint32_t)(oy * p.wo + ox) * 4u : BUF_OOB;
+  }
+  const uint32_t pb = (uint32_t)plane * 4u;
+  const float* __restrict__ z2 = p.p2_z + (size_t)n * C2 * plane;
+  int bpix[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int ty, tx;
+    tile_pix<TW, RP>(wave, j, l32, ty, tx);
+    bpix[j] = ty * TW + tx;
+  }
+  const int acg = tid >> 6, aco = tid & 63;  // A' staging: threads 0..127 -> (cg, co)
+  float zv[2][8], av[8];
+  auto fetch = [&](int c0) {
+    const auto rz = make_srd(z2 + (size_t)c0 * plane, (uint32_t)(C2 - c0) * pb);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) zv[q][e] = buf_ld(rz, zoff + (uint32_t)(q * 8 + e) * pb);
+    if (tid < 128) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + acg * 8 + e, co = co0 + aco;
+        av[e] = (c < C2 && co < p.cout_pad) ? A[(size_t)c * p.cout_pad + co] : 0.f;
+      }
+    }
+  };
+  fetch(0);
+  for (int c0 = 0; c0 < C2; c0 += 16) {
+    __syncthreads();  // previous chunk's operand reads done
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      f16x8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = zv[q][e] * sz;
+        const _Float16 vh = (_Float16)v;
+        hi[e] = vh;
+        lo[e] = (_Float16)(v - (float)vh);
+      }
+      *reinterpret_cast<f16x8*>(lz + ((0 * 2 + q) * NPIX + tid) * 16) = hi;
+      *reinterpret_cast<f16x8*>(lz + ((1 * 2 + q) * NPIX + tid) * 16) = lo;
+    }
+    if (tid < 128) {
+      f16x8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = av[e] * sa;
+        const _Float16 vh = (_Float16)v;
+        hi[e] = vh;
+        lo[e] = (_Float16)(v - (float)vh);
+      }
+      *reinterpret_cast<f16x8*>(la + ((0 * 2 + acg) * BM + aco) * 16) = hi;
+      *reinterpret_cast<f16x8*>(la + ((1 * 2 + acg) * BM + aco) * 16) = lo;
+    }
+    __syncthreads();
+    if (c0 + 16 < C2) fetch(c0 + 16);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f16x8 fa[2];
+#pragma unroll
+      for (int P = 0; P < 2; ++P)
+        fa[P] = *reinterpret_cast<const f16x8*>(la + ((P * 2 + h) * BM + i * 32 + l32) * 16);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f16x8 fb[2];
+#pragma unroll
+        for (int P = 0; P < 2; ++P)
+          fb[P] = *reinterpret_cast<const f16x8*>(lz + ((P * 2 + h) * NPIX + bpix[j]) * 16);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1], fb[0], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // LDS handed back to the epilogue
+  const float down = __builtin_ldexpf(1.f, -ls);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] *= down;
+}
+
+template <int TW, int NI>
 struct C16 {
-  static constexpr int BM = 64, NPIX = 256, TH = NPIX / TW;
+  static constexpr int BM = 64, NPIX = 128 * NI, TH = NPIX / TW;
   static constexpr int RH = TH + 2, RW = TW + 2, NPOS = RH * RW;
   static constexpr int NITEM = 2 * NPOS;                   // (channel group, position)
   static constexpr int NIT = (NITEM + 255) / 256;          // items per thread
@@ -60,10 +217,14 @@ struct C16 {
 
 // DBG (profiling experiments only, tools/bench_conv.py --dbg): bit 0 skips the
 // epilogue, bit 1 skips the per-chunk restaging after chunk 0
-template <int TW, int LM, int DBG = 0>
+// P2: 0 plain conv, 1 3x3 + fused fp32 Gram-backward phase (shared epilogue),
+//     2 the split Gram-backward phase alone (1x1 mode, cin == 0)
+template <int TW, int LM, int DBG = 0, int P2 = 0, int NI = 2>
 __global__ void __launch_bounds__(256, 2)
 conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
-  using C = C16<TW>;
+  using C = C16<TW, NI>;
+  constexpr bool RP = TW == 64 && NI == 2;  // row-pair tiles (fused pool / unpool)
+  static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
   constexpr int BM = C::BM;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
   char* lds_h = smem;                       // halo, hi plane then lo plane
@@ -78,7 +239,8 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
   const int co0 = blockIdx.y * BM;
   const int n = blockIdx.z;
 
-  const int ex = amax_exp(*p.in_amax), ew = amax_exp(*p.w_amax);
+  const int nchunks = cdiv(p.cin, 16);  // 0: Gram-backward phase only (1x1 mode)
+  const int ex = nchunks ? amax_exp(*p.in_amax) : 0, ew = nchunks ? amax_exp(*p.w_amax) : 0;
   const float sx = __builtin_ldexpf(1.f, 15 - ex);
   const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
 
@@ -122,7 +284,6 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
     const int seg = u / BM, co = u - seg * BM;
     woff[q] = (uint32_t)((seg * cout64 + co0 + co) * 16);
   }
-  const int nchunks = cdiv(p.cin, 16);
   const char* __restrict__ wt16 = reinterpret_cast<const char*>(p.wt16);
 
   float hv[C::NIT][8];
@@ -168,32 +329,32 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
       *reinterpret_cast<f32x4*>(lds_w + (tid + q * 256) * 16) = wreg[q];
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][NI];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // per-lane operand bases (bytes)
-  const char* bbase[2];
+  const char* bbase[NI];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NI; ++j) {
     int ty, tx;
-    tile_pix<TW, (TW == 64)>(wave, j, l32, ty, tx);
+    tile_pix<TW, RP, NI>(wave, j, l32, ty, tx);
     bbase[j] = lds_h + (h * C::NPOS + ty * C::RW + tx) * 16;
   }
   const char* abase = lds_w + (h * BM + l32) * 16;
 
-  fetch(0);
+  if (nchunks) fetch(0);
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     __syncthreads();  // previous chunk's operand reads done
     if (!(DBG & 2) || chunk == 0) store();
     __syncthreads();
     if (chunk + 1 < nchunks && !(DBG & 2)) fetch(chunk + 1);  // in flight across the MFMA loop
-    f16x8 ra[2][2][2], rb[2][2][2];            // [slot][tile][hi/lo]
-    auto rd = [&](int tap, f16x8 (&a)[2][2], f16x8 (&b)[2][2]) {
+    f16x8 ra[2][2][2], rb[2][NI][2];           // [slot][tile][hi/lo]
+    auto rd = [&](int tap, f16x8 (&a)[2][2], f16x8 (&b)[NI][2]) {
       const int kh = tap / 3, kw = tap % 3;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -201,7 +362,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
         for (int P = 0; P < 2; ++P)
           a[i][P] = *reinterpret_cast<const f16x8*>(abase + (tap * 4 * BM + P * 2 * BM + i * 32) * 16);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int P = 0; P < 2; ++P)
           b[j][P] = *reinterpret_cast<const f16x8*>(bbase[j] +
@@ -215,19 +376,19 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][i][0], rb[s][j][0], acc[i][j],
                                                              0, 0, 0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][i][0], rb[s][j][1], acc[i][j],
                                                              0, 0, 0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][i][1], rb[s][j][0], acc[i][j],
                                                              0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
@@ -238,7 +399,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) t += acc[i][j][r];
     if (t == 12345.f) p.y[tid] = t;
@@ -246,8 +407,49 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
   }
   __syncthreads();  // the epilogue's phase 2 re-uses the LDS
   const EpiTile et{n, co0, ty0, tx0, 0, wave, h, l32};
-  conv_epilogue<BM, TW, C::NPIX, 16, (TW == 64)>(acc, p, et, descale, reinterpret_cast<float*>(smem),
-                                     reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
+  if constexpr (P2 == 1) {
+    // 3x3 data-gradient + Gram-backward phase: the phase runs on fp32 MFMA inside the
+    // shared epilogue (its z/A streams are latency-bound either way; the split phase
+    // measured slower after the 3x3 main loop)
+    conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, true>(acc, p, et, descale,
+                                                     reinterpret_cast<float*>(smem),
+                                                     reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
+    return;
+  }
+  if constexpr (P2 == 2) {
+    // main accumulator first: de-scale, *acc_scale, ReLU mask (the order of the
+    // fp32 path), then the split Gram-backward phase adds s2 * A[n] . p2_z
+    const float sc = descale * (p.acc_scale ? *p.acc_scale : 1.f);
+    const size_t plane = (size_t)p.ho * p.wo;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int ty, tx;
+      tile_pix<TW, RP>(wave, j, l32, ty, tx);
+      const int oy = min(ty0 + ty, p.ho - 1), ox = min(tx0 + tx, p.wo - 1);
+      const size_t pofs = (size_t)oy * p.wo + ox;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[i][j][r] * sc;
+          if (p.mask) {
+            const int co = min(co0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, p.cout - 1);
+            if (!(p.mask[((size_t)n * p.cout + co) * plane + pofs] > 0.f)) v = 0.f;
+          }
+          acc[i][j][r] = v;
+        }
+    }
+    phase2_f16<TW>(acc, p, n, co0, ty0, tx0, wave, h, l32, smem);
+    stx_conv_params q = p;
+    q.p2_z = nullptr;
+    q.acc_scale = nullptr;
+    q.mask = nullptr;
+    conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, false>(acc, q, et, 1.f, reinterpret_cast<float*>(smem),
+                                           reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
+    return;
+  }
+  conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, false>(acc, p, et, descale, reinterpret_cast<float*>(smem),
+                                         reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
 }
 
 static int dbg_mode() {
@@ -258,12 +460,12 @@ static int dbg_mode() {
   return m;
 }
 
-template <int TW, int LM>
+template <int TW, int LM, int NI>
 static int launch16(const stx_conv_params& p, hipStream_t st) {
-  using C = C16<TW>;
+  using C = C16<TW, NI>;
   const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
   dim3 grid(tiles_x * tiles_y, cdiv(p.cout, C::BM), p.n);
-  if constexpr (TW == 64 && LM == STX_IN_RELU) {
+  if constexpr (TW == 64 && LM == STX_IN_RELU && NI == 2) {
     switch (dbg_mode()) {
       case 1: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 1>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
       case 2: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 2>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
@@ -271,19 +473,45 @@ static int launch16(const stx_conv_params& p, hipStream_t st) {
       default: break;
     }
   }
-  hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM>), grid, dim3(256), 0, st, p, tiles_x);
+  if (p.p2_z) {
+    if constexpr (LM == STX_IN_RAW && NI == 2) {
+      if (p.cin == 0)
+        hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 0, 2>), grid, dim3(256), 0, st, p,
+                           tiles_x);
+      else
+        hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 0, 1>), grid, dim3(256), 0, st, p,
+                           tiles_x);
+    } else {
+      set_error("stx_conv2d: the fused Gram-backward phase needs a raw-input conv");
+      return STX_E_INVALID;
+    }
+    return check_launch("stx_conv2d(f16x3 + phase 2)");
+  }
+  hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 0, 0, NI>), grid, dim3(256), 0, st, p,
+                     tiles_x);
   return check_launch("stx_conv2d(f16x3)");
+}
+
+// 256-pixel tiles (NI = 2) unless that grid leaves CUs idle: then 128-pixel tiles
+// (twice the blocks; not with the fused pool output or the Gram-backward phase,
+// which rely on the 256-pixel row-pair tile)
+template <int TW, int LM>
+static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
+  const long long blocks2 = (long long)cdiv(p.wo, TW) * cdiv(p.ho, 256 / TW) *
+                            cdiv(p.cout, 64) * p.n;
+  if (blocks2 < 512 && !p.pool_out && !p.p2_z) return launch16<TW, LM, 1>(p, st);
+  return launch16<TW, LM, 2>(p, st);
 }
 
 template <int LM>
 static int dispatch16_tw(const stx_conv_params& p, hipStream_t st) {
-  if (p.wo > 32) return launch16<64, LM>(p, st);
+  if (p.wo > 32) return launch16_ni<64, LM>(p, st);
   if (p.pool_out) {
     set_error("stx_conv2d: pool_out needs wo > 32 (row-pair tile mapping)");
     return STX_E_INVALID;
   }
-  if (p.wo > 16) return launch16<32, LM>(p, st);
-  return launch16<16, LM>(p, st);
+  if (p.wo > 16) return launch16_ni<32, LM>(p, st);
+  return launch16_ni<16, LM>(p, st);
 }
 
 // ------------------------------------------------------------ weight split prep

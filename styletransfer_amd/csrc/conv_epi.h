@@ -27,14 +27,14 @@ struct EpiTile {
 // row-major tile order.  ROWPAIR (TW == 64): wave column wn covers x in
 // [32*(wn&1), +32) of rows 2*(wn>>1) + {0, 1}, so every 2x2 pooling window lies in
 // one wave (tiles j = 0/1 x lanes l32, l32^1) -- the fused ReLU+MaxPool output.
-template <int TW, bool ROWPAIR>
+template <int TW, bool ROWPAIR, int NI = 2>
 __device__ __forceinline__ void tile_pix(int wn, int j, int l32, int& ty, int& tx) {
   if (ROWPAIR) {
     static_assert(!ROWPAIR || TW == 64, "row-pair mapping needs TW == 64");
     tx = (wn & 1) * 32 + l32;
     ty = (wn >> 1) * 2 + j;
   } else {
-    const int pix = (wn * 2 + j) * 32 + l32;
+    const int pix = (wn * NI + j) * 32 + l32;
     ty = pix / TW;
     tx = pix - ty * TW;
   }
@@ -66,8 +66,10 @@ __device__ __forceinline__ void block_max_to(float* slot, float m) {
   }
 }
 
-template <int BM, int TW, int NPIX, int CIS2, bool ROWPAIR = false>
-__device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_conv_params& p,
+template <int BM, int TW, int NPIX, int CIS2, bool ROWPAIR = false, int NI = 2,
+          bool HAS_P2 = true>
+// (NI: 32-pixel N-tiles per wave; ROWPAIR needs NI == 2)
+__device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][NI], const stx_conv_params& p,
                                               const EpiTile& t, float pre_scale,
                                               float* __restrict__ lds_in,
                                               float* __restrict__ lds_w) {
@@ -78,27 +80,27 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_con
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] *= pre_scale;
   }
   bool mask_done = false;
-  if (p.p2_z) {
+  if (HAS_P2 && p.p2_z) {
     // ---- fused second phase: acc = acc*(mask>0) + s2 * A[n] . z2 (1x1, no halo) ----
     if (p.acc_scale) {
       const float sc = *p.acc_scale;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NI; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
     }
     if (p.mask) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NI; ++j) {
         int ty, tx;
-        tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
+        tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
         const int oy = min(t.ty0 + ty, p.ho - 1), ox = min(t.tx0 + tx, p.wo - 1);
         const size_t pofs = (size_t)oy * p.wo + ox;
 #pragma unroll
@@ -119,11 +121,11 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_con
     constexpr int N2 = (E2 + 255) / 256;
     constexpr int WQ2 = CIS2 * BM / 4;
     constexpr int NW2 = (WQ2 + 255) / 256;
-    int b2_base[2];
+    int b2_base[NI];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NI; ++j) {
       int ty, tx;
-      tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
+      tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
       b2_base[j] = h * (CIS2 / 2) * NPIX + ty * TW + tx;
     }
     const int a2_base = h * (CIS2 / 2) * BM + t.wm * 64 + l32;
@@ -165,15 +167,15 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_con
       __syncthreads();
 #pragma unroll
       for (int s = 0; s < CIS2 / 2; ++s) {
-        float a[2], b[2];
+        float a[2], b[NI];
 #pragma unroll
         for (int i = 0; i < 2; ++i) a[i] = lds_w[a2_base + s * BM + i * 32];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b[j] = lds_in[b2_base[j] + s * NPIX];
+        for (int j = 0; j < NI; ++j) b[j] = lds_in[b2_base[j] + s * NPIX];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NI; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
       }
     }
@@ -230,11 +232,11 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_con
   const auto ry = make_srd(p.y + wofs, rows * pb);
   const auto rmask = make_srd(p.mask ? p.mask + wofs : p.y, rows * pb);
   const auto raux = make_srd(p.aux ? p.aux + wofs : p.y, rows * pb);
-  uint32_t vo[2];
+  uint32_t vo[NI];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NI; ++j) {
     int ty, tx;
-    tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
+    tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
     const int oy = t.ty0 + ty, ox = t.tx0 + tx;
     vo[j] = (oy < p.ho && ox < p.wo) ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u
                                      : BUF_OOB;
@@ -250,7 +252,7 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_con
   const float sc = (!mask_done && p.acc_scale) ? *p.acc_scale : 1.f;
   uint32_t vmax_u = 0u;  // max |v| as IEEE bits: NaN (above inf) propagates
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NI; ++j) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -268,7 +270,7 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_con
           // ReLU + MaxPool2d(2,2) backward, argmax recomputed from up_z
           const int co = co_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           int ty, tx;
-          tile_pix<TW, ROWPAIR>(t.wn, j, l32, ty, tx);
+          tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
           const int oy = t.ty0 + ty, ox = t.tx0 + tx;
           if (co < p.cout && oy < p.ho && ox < p.wo) {
             const size_t pofs = (size_t)oy * p.wo + ox;
@@ -300,7 +302,7 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][2], const stx_con
     }
   }
   const float vmax = __uint_as_float(vmax_u);
-  if (ROWPAIR && p.pool_out) {
+  if constexpr (ROWPAIR) if (p.pool_out) {
     // relu(maxpool2x2(y)) = maxpool2x2(relu(y)) -> pool_out [n][cout][ho/2][wo/2]
     // (torch MaxPool2d floor mode: a window needs both rows and both columns)
     const int hp = p.ho >> 1, wp = p.wo >> 1;

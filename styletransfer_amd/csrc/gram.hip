@@ -237,6 +237,182 @@ gram_partial_v2_kernel(const float* __restrict__ z, float* __restrict__ ws, int 
   }
 }
 
+// fp16 hi/lo split Gram partial (hw % 8 == 0, z_amax = a device bound on max|z|).
+// Same tiling, split-K and deterministic LDS reduction as gram_partial_v2_kernel,
+// but every F element is scaled by a power of two s (s*max|z| < 2^15) and split
+// s*f = hi + lo (fp16) and each 32x32 quadrant takes hi*hi + hi*lo + lo*hi on
+// v_mfma_f32_32x32x16_f16 (fp32-level accuracy, conv16.hip): the matrix pipe does
+// 16 pixels in 3 x 32 cycles where the fp32 MFMA needs 8 x 64, so the kernel is
+// bound by reading F.  Lane (r, h) feeds pixels [8h, 8h+8) of each 16-pixel step
+// from its own rows (two float4), identical for the A (rows I) and B (rows J)
+// operands; a wave walks 32-pixel groups (two steps) with the next group's loads
+// in flight.  Partials are de-scaled by 1/s^2 (exact) before the reduction.
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int gram_amax_exp(float a) {
+  int e = 0;
+  frexpf(a, &e);
+  return min(max(e, -60), 60);
+}
+
+__device__ __forceinline__ void split8(const f32x4& x0, const f32x4& x1, float s, f16x8_t& hi,
+                                       f16x8_t& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float v = (e < 4 ? x0[e] : x1[e - 4]) * s;
+    const _Float16 vh = (_Float16)v;
+    hi[e] = vh;
+    lo[e] = (_Float16)(v - (float)vh);
+  }
+}
+
+#define MF16(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0)
+
+// One launch over all upper-triangle tiles (a block-uniform branch picks the
+// diagonal or off-diagonal body) so that small-C x large-HW and large-C x small-HW
+// layers both fill the chip with ~512 blocks.
+template <bool DIAG>
+__device__ __forceinline__ void gram_f16_tile(const float* __restrict__ z, float* __restrict__ ws,
+                                              int c, int hw, int nsplit, int split_len,
+                                              const float* __restrict__ z_amax, int I, int J,
+                                              int split, float* red);
+
+__global__ void __launch_bounds__(256, 2)
+gram_partial_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int c, int hw,
+                        int nsplit, int split_len, const float* __restrict__ z_amax) {
+  __shared__ __attribute__((aligned(16))) float red[2 * GT * GT];
+  const int nt = cdiv(c, GT);
+  const int ntu = nt * (nt + 1) / 2;
+  const int L = blockIdx.x;
+  const int xcd = L & 7, rest = L >> 3;
+  const int k = rest % ntu, split = (rest / ntu) * 8 + xcd;
+  int I, J;
+  tile_ij(k, nt, I, J);
+  if (I == J)
+    gram_f16_tile<true>(z, ws, c, hw, nsplit, split_len, z_amax, I, J, split, red);
+  else
+    gram_f16_tile<false>(z, ws, c, hw, nsplit, split_len, z_amax, I, J, split, red);
+}
+
+template <bool DIAG>
+__device__ __forceinline__ void gram_f16_tile(const float* __restrict__ z, float* __restrict__ ws,
+                                              int c, int hw, int nsplit, int split_len,
+                                              const float* __restrict__ z_amax, int I, int J,
+                                              int split, float* red) {
+  const int nt = cdiv(c, GT);
+  const int ntu = nt * (nt + 1) / 2;
+  const int tileu = tile_index(I, J, nt);
+  const int b = blockIdx.z;
+  const int p_begin = split * split_len;
+  const int p_end = min(hw, p_begin + split_len);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const float* zb = z + (size_t)b * c * hw;
+  const int ra0 = I * GT + r, ra1 = I * GT + 32 + r;
+  const int rb0 = J * GT + r, rb1 = J * GT + 32 + r;
+  const float* pa0 = zb + (size_t)min(ra0, c - 1) * hw + 8 * h;
+  const float* pa1 = zb + (size_t)min(ra1, c - 1) * hw + 8 * h;
+  const float* pb0 = zb + (size_t)min(rb0, c - 1) * hw + 8 * h;
+  const float* pb1 = zb + (size_t)min(rb1, c - 1) * hw + 8 * h;
+  const bool va0 = ra0 < c, va1 = ra1 < c, vb0 = rb0 < c, vb1 = rb1 < c;
+  const int e = gram_amax_exp(*z_amax);
+  const float sx = __builtin_ldexpf(1.f, 15 - e);
+  const float inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
+
+  f32x16 a00, a01, a10, a11;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) a00[q] = a01[q] = a10[q] = a11[q] = 0.f;
+
+  // one 32-pixel group: [step s][half of the 8 pixels] float4s per row
+  struct Grp {
+    f32x4 x[4][2][2];  // [row a0, a1, b0, b1][step][lo/hi float4]
+  };
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  auto load = [&](int p0, Grp& g) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int pp = p0 + 16 * st;       // + 8h folded into the row pointers
+      const bool ok = pp + 8 * h < p_end;  // hw % 8 == 0: a lane's 8 pixels all in or out
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        g.x[0][st][q] = (ok && va0) ? *reinterpret_cast<const f32x4*>(pa0 + pp + 4 * q) : zero;
+        g.x[1][st][q] = (ok && va1) ? *reinterpret_cast<const f32x4*>(pa1 + pp + 4 * q) : zero;
+        if (!DIAG) {
+          g.x[2][st][q] = (ok && vb0) ? *reinterpret_cast<const f32x4*>(pb0 + pp + 4 * q) : zero;
+          g.x[3][st][q] = (ok && vb1) ? *reinterpret_cast<const f32x4*>(pb1 + pp + 4 * q) : zero;
+        }
+      }
+    }
+  };
+  auto compute = [&](const Grp& g) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f16x8_t h0, l0, h1, l1;
+      split8(g.x[0][st][0], g.x[0][st][1], sx, h0, l0);
+      split8(g.x[1][st][0], g.x[1][st][1], sx, h1, l1);
+      if (DIAG) {
+        a00 = MF16(h0, h0, a00); a01 = MF16(h0, h1, a01); a11 = MF16(h1, h1, a11);
+        a00 = MF16(h0, l0, a00); a01 = MF16(h0, l1, a01); a11 = MF16(h1, l1, a11);
+        a00 = MF16(l0, h0, a00); a01 = MF16(l0, h1, a01); a11 = MF16(l1, h1, a11);
+      } else {
+        f16x8_t g0, m0, g1, m1;
+        split8(g.x[2][st][0], g.x[2][st][1], sx, g0, m0);
+        split8(g.x[3][st][0], g.x[3][st][1], sx, g1, m1);
+        a00 = MF16(h0, g0, a00); a01 = MF16(h0, g1, a01);
+        a10 = MF16(h1, g0, a10); a11 = MF16(h1, g1, a11);
+        a00 = MF16(h0, m0, a00); a01 = MF16(h0, m1, a01);
+        a10 = MF16(h1, m0, a10); a11 = MF16(h1, m1, a11);
+        a00 = MF16(l0, g0, a00); a01 = MF16(l0, g1, a01);
+        a10 = MF16(l1, g0, a10); a11 = MF16(l1, g1, a11);
+      }
+    }
+  };
+  // waves interleave 32-pixel groups: wave w takes p_begin + 32*(w + 4*i)
+  int p0 = p_begin + wave * 32;
+  if (p0 < p_end) {
+    Grp cur, nxt;
+    load(p0, cur);
+    for (; p0 < p_end; p0 += 128) {
+      if (p0 + 128 < p_end) load(p0 + 128, nxt);
+      compute(cur);
+      cur = nxt;
+    }
+  }
+  // 4 wave partials -> 2 LDS images (32 KB): waves 2,3 store, waves 0,1 add, then sum
+  auto put = [&](float* img, bool add) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+      float* q00 = img + row * GT + r;
+      float* q01 = img + row * GT + 32 + r;
+      float* q11 = img + (32 + row) * GT + 32 + r;
+      float* q10 = img + (32 + row) * GT + r;
+      *q00 = add ? *q00 + a00[q] : a00[q];
+      *q01 = add ? *q01 + a01[q] : a01[q];
+      *q11 = add ? *q11 + a11[q] : a11[q];
+      if (!DIAG) *q10 = add ? *q10 + a10[q] : a10[q];
+    }
+  };
+  if (wave >= 2) put(red + (wave - 2) * GT * GT, false);
+  __syncthreads();
+  if (wave < 2) put(red + wave * GT * GT, true);
+  __syncthreads();
+  float* out = ws + (((size_t)b * ntu + tileu) * nsplit + split) * (GT * GT);
+#pragma unroll
+  for (int q = 0; q < (GT * GT) / 256; ++q) {
+    const int el = q * 256 + tid;
+    int row = el / GT, col = el % GT;
+    if (DIAG && row >= 32 && col < 32) {  // mirrored quadrant of a diagonal tile
+      const int t = row;
+      row = col;
+      col = t;
+    }
+    const int o = row * GT + col;
+    out[el] = (red[o] + red[GT * GT + o]) * inv2;
+  }
+}
+#undef MF16
+
 // grid (ntu * 16, B); one thread per tile element (256 elements per block).  The
 // split partials are summed in a fixed order (bit-reproducible); loads are
 // independent and unrolled so a block streams its slab column at full rate.
@@ -342,22 +518,42 @@ static void gram_geometry(int c, int hw, int b, int& nsplit, int& split_len, int
   nsplit = cdiv(hw, split_len);
 }
 
+// split geometry of the fp16 split kernel: 32-pixel groups interleaved over 4 waves,
+// splits in multiples of 256 pixels (whole groups) and of 8 (XCD grouping), each
+// wave >= 2 groups, ~640 blocks (2-3 per CU: enough bytes in flight)
+static void gram_geometry16(int c, int hw, int b, int& nsplit, int& split_len, int& ntu) {
+  const int nt = cdiv(c, GT);
+  ntu = nt * (nt + 1) / 2;
+  int want = rup(cdiv(640, ntu * b), 8);
+  const int max_splits = std::max(1, cdiv(hw, 256));
+  want = std::max(8, std::min(want, rup(max_splits, 8)));
+  split_len = rup(cdiv(hw, want), 256);
+  nsplit = rup(cdiv(hw, split_len), 8);
+}
+
 static size_t gram_ws_bytes(int b, int c, int hw) {
-  int nsplit, split_len, ntu;
+  int nsplit, split_len, ntu, ns16, sl16;
   gram_geometry(c, hw, b, nsplit, split_len, ntu);
+  gram_geometry16(c, hw, b, ns16, sl16, ntu);
+  nsplit = std::max(nsplit, ns16);
   // partial slabs + loss parts
   return ((size_t)b * ntu * nsplit * GT * GT + (size_t)b * ntu * FSUB + 64) * sizeof(float);
 }
 
 static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_out,
                     const float* target, long long t_bstride, float* coef, float cA, float alpha, float* loss,
-                    float loss_inv, void* ws, size_t ws_bytes, hipStream_t st) {
+                    float loss_inv, const float* z_amax, void* ws, size_t ws_bytes,
+                    hipStream_t st) {
   if (b <= 0 || c <= 0 || hw <= 0 || !z) {
     set_error("gram: invalid dims");
     return STX_E_INVALID;
   }
+  const bool f16 = z_amax && hw % 8 == 0 && (reinterpret_cast<uintptr_t>(z) & 15) == 0;
   int nsplit, split_len, ntu;
-  gram_geometry(c, hw, b, nsplit, split_len, ntu);
+  if (f16)
+    gram_geometry16(c, hw, b, nsplit, split_len, ntu);
+  else
+    gram_geometry(c, hw, b, nsplit, split_len, ntu);
   const size_t need = gram_ws_bytes(b, c, hw);
   if (!ws || ws_bytes < need) {
     set_error("gram: workspace %zu < %zu", ws_bytes, need);
@@ -365,7 +561,10 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
   }
   float* slabs = (float*)ws;
   float* parts = slabs + (size_t)b * ntu * nsplit * GT * GT;
-  if (hw % 4 == 0) {
+  if (f16) {
+    hipLaunchKernelGGL(gram_partial_f16_kernel, dim3(nsplit * ntu, 1, b), dim3(256), 0, st, z,
+                       slabs, c, hw, nsplit, split_len, z_amax);
+  } else if (hw % 4 == 0) {
     const int nt = cdiv(c, GT);
     hipLaunchKernelGGL(gram_partial_v2_kernel<true>, dim3(nsplit * nt, 1, b), dim3(256), 0, st,
                        z, slabs, c, hw, nsplit, split_len);
@@ -392,15 +591,16 @@ extern "C" size_t stx_gram_ws(int b, int c, int hw) { return gram_ws_bytes(b, c,
 
 extern "C" int stx_gram_coef_pitch(int c) { return c <= 64 ? rup(c, 64) : rup(c, 128); }
 
-extern "C" int stx_gram(const float* z, float* g, int b, int c, int hw, float scale, void* ws,
-                        size_t ws_bytes, void* stream) {
-  return gram_run(z, b, c, hw, scale, g, nullptr, 0, nullptr, 0.f, 0.f, nullptr, 0.f, ws, ws_bytes,
+extern "C" int stx_gram(const float* z, float* g, int b, int c, int hw, float scale,
+                        const float* z_amax, void* ws, size_t ws_bytes, void* stream) {
+  return gram_run(z, b, c, hw, scale, g, nullptr, 0, nullptr, 0.f, 0.f, nullptr, 0.f, z_amax, ws,
+                  ws_bytes,
                   (hipStream_t)stream);
 }
 
 extern "C" int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
                               float* loss, int b, int c, int hw, int target_batched, float weight, float diag_alpha,
-                              void* ws, size_t ws_bytes, void* stream) {
+                              const float* z_amax, void* ws, size_t ws_bytes, void* stream) {
   if (!target || !loss) {
     set_error("stx_style_loss: target and loss are required");
     return STX_E_INVALID;
@@ -417,7 +617,7 @@ extern "C" int stx_style_loss(const float* z, const float* target, float* g_out,
                        dim3(256), 0, st, coef, cnt);
   }
   return gram_run(z, b, c, hw, scale, g_out, target, target_batched ? (long long)c * c : 0, coef, cA, diag_alpha, loss,
-                  (float)(1.0 / ((double)b * c * c)), ws, ws_bytes, st);
+                  (float)(1.0 / ((double)b * c * c)), z_amax, ws, ws_bytes, st);
 }
 
 extern "C" int stx_gram_bwd(const float* coef, const float* z, float* dz, int b, int c, int h,

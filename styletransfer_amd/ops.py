@@ -129,7 +129,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
            out=None, mask=None, aux=None, aux_scale=0.0, acc_scale=None, accumulate=False,
            relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
            p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
-           pool_out=None):
+           pool_out=None, p2_amax=None, split_1x1=False):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
     up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
@@ -167,6 +167,13 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         if in_amax is None:
             in_amax = amax(x)
         p.wt16, p.w_amax, p.in_amax = wt16[0].data_ptr(), wt16[1].data_ptr(), in_amax.data_ptr()
+        if p2_z is not None:
+            p.p2_amax = (p2_amax if p2_amax is not None else amax(p2_z)).data_ptr()
+    elif split_1x1:
+        # Gram backward as the split phase alone (per-image weights, include/stx.h)
+        assert ks == 1 and wt_batch_stride and mask is None and p2_z is None
+        p.wt16 = 1
+        p.in_amax = (in_amax if in_amax is not None else amax(x)).data_ptr()
     if out_amax is not None:
         p.out_amax = out_amax.data_ptr()
     if pool_out is not None:
@@ -211,8 +218,9 @@ def bias_grad(dy, db=None, accumulate=False):
 
 
 # ----------------------------------------------------------------------- gram
-def gram(z, scale=None):
-    """G[b] = F F^T * scale (default 1/(C*H*W), StyleLoss.gram_matrix)."""
+def gram(z, scale=None, z_amax=None):
+    """G[b] = F F^T * scale (default 1/(C*H*W), StyleLoss.gram_matrix).  z_amax
+    (device >= max|z|) selects the fp16 hi/lo split MFMA partials."""
     _req(z, "z")
     b, c = z.shape[:2]
     hw = z[0, 0].numel()
@@ -221,7 +229,8 @@ def gram(z, scale=None):
     g = torch.empty((b, c, c), device=z.device, dtype=torch.float32)
     L = lib()
     wp, wn = WS.get(L.stx_gram_ws(b, c, hw), z.device)
-    check(L.stx_gram(z.data_ptr(), g.data_ptr(), b, c, hw, float(scale), wp, wn, _stream()),
+    check(L.stx_gram(z.data_ptr(), g.data_ptr(), b, c, hw, float(scale), _p(z_amax), wp, wn,
+                     _stream()),
           "stx_gram")
     return g
 
@@ -231,7 +240,7 @@ def coef_pitch(c):
 
 
 def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None, loss=None,
-               coef=None):
+               coef=None, z_amax=None):
     """mean((gram(z) - target)^2) -> 0-d loss; coef = d(weight*loss)/dz operator."""
     _req(z, "z")
     _req(target, "target")
@@ -250,18 +259,20 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
     wp, wn = WS.get(L.stx_gram_ws(b, c, hw), z.device)
     check(L.stx_style_loss(z.data_ptr(), target.data_ptr(), _p(g_out), _p(coef) if want_coef
                            else None, loss.data_ptr(), b, c, hw, int(tb), float(weight),
-                           float(diag_alpha), wp, wn, _stream()), "stx_style_loss")
+                           float(diag_alpha), _p(z_amax), wp, wn, _stream()), "stx_style_loss")
     return loss, (coef if want_coef else None)
 
 
 def gram_bwd_fused(coef, z, out=None, acc_scale=None, up_dp=None, aux=None, aux_scale=0.0,
-                   out_amax=None):
+                   out_amax=None, z_amax=None):
     """out = s*A[n].z[n] (+ unpool(up_dp)*(z>0)) (+ aux_scale*aux): the Gram backward
-    as a 1x1 MFMA conv with the ReLU+MaxPool backward fused into its epilogue."""
+    as a 1x1 MFMA conv with the ReLU+MaxPool backward fused into its epilogue.
+    z_amax (device >= max|z|) runs it on the fp16 hi/lo split MFMA."""
     b, c = z.shape[:2]
     return conv2d(z, coef, c, c, 1, pad=0, out=out, acc_scale=acc_scale, aux=aux,
                   aux_scale=aux_scale, wt_batch_stride=coef.shape[-1] * coef.shape[-2],
-                  up_dp=up_dp, up_z=z if up_dp is not None else None, out_amax=out_amax)
+                  up_dp=up_dp, up_z=z if up_dp is not None else None, out_amax=out_amax,
+                  in_amax=z_amax, split_1x1=z_amax is not None)
 
 
 def gram_bwd(coef, z, dz=None, acc_scale=None, mask=None, aux=None, aux_scale=0.0,

@@ -190,10 +190,12 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         sw = float(folded_weights[0])
         alpha = float(folded_weights[1]) * 2.0 / z4.numel()
     st.alpha = alpha
+    split = os.environ.get("STX_GRAM_SPLIT", "1") != "0"
     for i, l in enumerate(STYLE_CONVS):
         _, st.coef[i] = ops.style_loss(st.z[l], targets[i], weight=sw,
                                        diag_alpha=alpha if l == CONTENT_CONV else 0.0,
-                                       loss=st.losses[i], coef=st.coef[i])
+                                       loss=st.losses[i], coef=st.coef[i],
+                                       z_amax=st.amax[l + 1:l + 2] if split else None)
     st.c4 = c4
     ops.mse(z4, c4, mode=2, out=st.losses[5:8])  # content, feature, feature-mse: one pass
     return st
@@ -228,15 +230,17 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
     s = (lambda i: None) if folded else (lambda i: g[i:i + 1])
     am = st.amax  # slots 0..5: forward; 6..9: backward split-conv inputs
     # conv3_1 output: dZ5 = A5 Z5
+    sp = feat.wt16[1] is not None  # split kernels in use
     dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4),
-                             out_amax=am[6:7])
+                             out_amax=am[6:7], z_amax=am[5:6] if sp else None)
     # -> grad wrt pool(relu Z4)
     n4 = (B, 128, z[3].shape[2] // 2, z[3].shape[3] // 2)
     dp2 = feat.dgrad(4, dz5, buf("dp2", n4), in_amax=am[6:7])
     # dZ4 = unpool(dP2)*[Z4>0] + A4 Z4 (+ content)
     dz4 = ops.gram_bwd_fused(st.coef[3], z[3], out=buf("dz4", z[3].shape), acc_scale=s(3),
                              up_dp=dp2, aux=st.c4 if folded else None, aux_scale=-st.alpha,
-                             out_amax=am[7:8] if folded else None)
+                             out_amax=am[7:8] if folded else None,
+                             z_amax=am[4:5] if sp else None)
     n = z[3].numel()
     dz4_amax = am[7:8] if folded else None
     if not folded:
@@ -246,15 +250,16 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
                            s2=st.fmean[1:2], relu=True, out=dz4, accumulate=True)
     # dZ3 = conv2_2^T(dZ4)*[Z3>0] + A3 Z3
     dz3 = feat.dgrad(3, dz4, buf("dz3", z[2].shape), mask=z[2], p2_z=z[2],
-                     p2_coef=st.coef[2], p2_scale=s(2), in_amax=dz4_amax, out_amax=am[8:9])
+                     p2_coef=st.coef[2], p2_scale=s(2), in_amax=dz4_amax, out_amax=am[8:9],
+                     p2_amax=am[3:4])
     # -> grad wrt pool(relu Z2)
     n2 = (B, 64, z[1].shape[2] // 2, z[1].shape[3] // 2)
     dp1 = feat.dgrad(2, dz3, buf("dp1", n2), in_amax=am[8:9])
     dz2 = ops.gram_bwd_fused(st.coef[1], z[1], out=buf("dz2", z[1].shape), acc_scale=s(1),
-                             up_dp=dp1, out_amax=am[9:10])
+                             up_dp=dp1, out_amax=am[9:10], z_amax=am[2:3] if sp else None)
     # dZ1 = conv1_2^T(dZ2)*[Z1>0] + A1 Z1
     dz1 = feat.dgrad(1, dz2, buf("dz1", z[0].shape), mask=z[0], p2_z=z[0],
-                     p2_coef=st.coef[0], p2_scale=s(0), in_amax=am[9:10])
+                     p2_coef=st.coef[0], p2_scale=s(0), in_amax=am[9:10], p2_amax=am[1:2])
     # conv1_1 dgrad -> image
     xs = (B, 3, z[0].shape[2], z[0].shape[3])
     if dx is None:

@@ -171,3 +171,45 @@ def test_vgg_fused_pool_matches_unfused(dev):
         ref.append(cur)
     for a, b in zip(zs, ref):
         assert rel(a, b) < 1e-6
+
+
+@pytest.mark.parametrize("shape", [(1, 64, 64, 64), (2, 128, 24, 40), (1, 256, 16, 16),
+                                   (1, 96, 9, 24), (3, 64, 8, 7), (1, 64, 512, 512)])
+def test_split_gram(dev, shape):
+    """fp16 hi/lo split Gram partials (z_amax given) vs fp64, and the style loss /
+    backward coefficients they feed vs the fp32 MFMA path."""
+    b, c, h, w = shape
+    z = rnd(b, c, h, w, dev=dev, seed=41, scale=2, shift=-1)
+    am = ops.amax(z)
+    g16 = ops.gram(z, z_amax=am)
+    f = z.double().cpu().reshape(b, c, h * w)
+    ref = torch.bmm(f, f.transpose(1, 2)) / (c * h * w)
+    assert rel(g16, ref) < TOL64
+    t = rnd(c, c, dev=dev, seed=42, scale=0.02)
+    l16, a16 = ops.style_loss(z, t, weight=3.0, z_amax=am)
+    l32, a32 = ops.style_loss(z, t, weight=3.0)
+    assert rel(l16, l32) < 1e-5
+    assert rel(a16, a32) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 20, 70), (1, 128, 34, 64), (1, 256, 16, 16),
+                                   (1, 64, 9, 13)])
+def test_split_gram_bwd(dev, shape):
+    """Gram backward dz = s*A.z + unpool(dp)*(z>0) + aux as the split phase alone
+    (1x1 mode) vs the fp32 MFMA 1x1 conv."""
+    n, c, h, w = shape
+    z = rnd(n, c, h, w, dev=dev, seed=51, scale=2, shift=-1)
+    t = rnd(c, c, dev=dev, seed=52, scale=0.02)
+    _, coef = ops.style_loss(z, t, weight=5.0)
+    dp = rnd(n, c, h // 2, w // 2, dev=dev, seed=53, scale=2, shift=-1)
+    aux = rnd(n, c, h, w, dev=dev, seed=54)
+    s = torch.tensor(0.75, device=dev)
+    a16 = ops.gram_bwd_fused(coef, z, acc_scale=s, up_dp=dp, aux=aux, aux_scale=-0.25,
+                             z_amax=ops.amax(z))
+    a32 = ops.gram_bwd_fused(coef, z, acc_scale=s, up_dp=dp, aux=aux, aux_scale=-0.25)
+    assert rel(a16, a32) < 2e-6
+    b16 = ops.gram_bwd_fused(coef, z, z_amax=ops.amax(z))
+    f = z.double().cpu().reshape(n, c, h * w)
+    A = coef.double().cpu()[:, :c, :c]
+    ref = torch.bmm(A.transpose(1, 2), f).reshape(n, c, h, w)
+    assert rel(b16, ref) < TOL64

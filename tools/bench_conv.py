@@ -45,6 +45,14 @@ def main():
         ("itn up conv B8 128->64 @128", 8, 128, 64, 64, 64, 3, 1, N.STX_IN_UPSAMPLE2),
         ("itn down s2 B8 32->64", 8, 32, 64, 256, 256, 3, 2, N.STX_IN_RAW),
     ]
+    if not args.only or "hbm" in args.only:
+        # HBM calibration: 64 MiB write (fill) and 64 MiB copy (read + write)
+        a = torch.empty(16 << 20, device=dev)
+        bb = torch.empty_like(a)
+        ms = ev(lambda: a.fill_(1.0))
+        ms2 = ev(lambda: bb.copy_(a))
+        print(f"{'hbm fill 64MiB':32s} {ms * 1e3:9.1f} us {64 * 1.048576 / ms / 1e3:7.2f} TB/s | "
+              f"copy {ms2 * 1e3:9.1f} us {2 * 64 * 1.048576 / ms2 / 1e3:7.2f} TB/s", flush=True)
     for name, n, cin, cout, h, w, ks, s, mode in cases:
         if args.only not in name:
             continue
