@@ -143,8 +143,8 @@ def gatys_leg(args, world, rank, dev):
     # fused ReLU+MaxPool output for conv2_1, max|Z2| for conv2_1's input scale
     z1 = eng.st.z[0]
     out = torch.empty_like(z1)
-    am = eng.st.amax[1:2].clone()
-    am_out = torch.zeros(1, device=dev)
+    am = V.slot(eng.st.amax, 1).clone()
+    am_out = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
     pool = torch.empty_like(eng.st.pools[1])
     fwd_ms = event_avg_ms(lambda: ops.conv2d(z1, feat.wt[1], 64, 64, 3, in_mode=N.STX_IN_RELU,
                                              bias=feat.b[1], out=out, wt16=feat.wt16[1],

@@ -29,6 +29,11 @@
 extern "C" {
 #endif
 
+/* Every max|.| bound in this API ("amax": in_amax, w_amax, out_amax, p2_amax,
+ * z_amax, stx_amax's out) is a group of STX_AMAX_SLOTS floats whose maximum is the
+ * value; producers spread their atomics over the group, a zeroed group reads 0. */
+#define STX_AMAX_SLOTS 32
+
 #define STX_OK 0
 #define STX_E_INVALID 1001   /* bad argument / unsupported shape */
 #define STX_E_WORKSPACE 1002 /* workspace too small */

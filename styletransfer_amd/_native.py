@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STX_LIB", os.path.join(_HERE, "libstx.so"))
 
 STX_IN_RAW, STX_IN_RELU, STX_IN_RELU_POOL2, STX_IN_UPSAMPLE2, STX_IN_DILATE2 = range(5)
+STX_AMAX_SLOTS = 32  # an "amax" is a group of 32 floats whose max is the value (stx.h)
 
 vp = C.c_void_p
 i32 = C.c_int

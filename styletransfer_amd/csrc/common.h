@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/stx.h"
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -57,6 +59,17 @@ __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte
 
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, 0);
+}
+
+// A max|.| bound ("amax") is a group of STX_AMAX_SLOTS floats whose maximum is the
+// value: producers atomicMax into slot (block id % 32) so a 1024-block kernel does
+// not serialise 1024 same-address atomics at its tail; consumers take the max of
+// the group (wave-uniform loads).
+__device__ __forceinline__ float read_amax(const float* __restrict__ g) {
+  uint32_t m = 0u;
+#pragma unroll
+  for (int i = 0; i < STX_AMAX_SLOTS; ++i) m = max(m, __float_as_uint(g[i]) & 0x7fffffffu);
+  return __uint_as_float(m);
 }
 
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -97,7 +97,7 @@ __device__ __forceinline__ void phase2_f16(f32x16 (&acc)[2][2], const stx_conv_p
   if ((tid & 63) == 0) red2[tid >> 6] = am;
   __syncthreads();
   am = fmaxf(fmaxf(red2[0], red2[1]), fmaxf(red2[2], red2[3]));
-  const int ea = amax_exp(m), ez = amax_exp(*p.p2_amax), eacc = amax_exp(am);
+  const int ea = amax_exp(m), ez = amax_exp(read_amax(p.p2_amax)), eacc = amax_exp(am);
   const int ls = min(min(30 - ea - ez, 100 - eacc), 120);  // log2 S
   const float sz = __builtin_ldexpf(1.f, 15 - ez);
   const float sa = __builtin_ldexpf(s2, ls - (15 - ez));  // S / sz, with s2 folded in
@@ -240,7 +240,8 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
   const int n = blockIdx.z;
 
   const int nchunks = cdiv(p.cin, 16);  // 0: Gram-backward phase only (1x1 mode)
-  const int ex = nchunks ? amax_exp(*p.in_amax) : 0, ew = nchunks ? amax_exp(*p.w_amax) : 0;
+  const int ex = nchunks ? amax_exp(read_amax(p.in_amax)) : 0;
+  const int ew = nchunks ? amax_exp(read_amax(p.w_amax)) : 0;
   const float sx = __builtin_ldexpf(1.f, 15 - ex);
   const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
 
@@ -475,7 +476,11 @@ static int launch16(const stx_conv_params& p, hipStream_t st) {
   }
   if (p.p2_z) {
     if constexpr (LM == STX_IN_RAW && NI == 2) {
-      if (p.cin == 0)
+      static const bool split_p2 = [] {
+        const char* e = getenv("STX_P2_SPLIT");
+        return e && atoi(e) != 0;
+      }();
+      if (p.cin == 0 || split_p2)
         hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 0, 2>), grid, dim3(256), 0, st, p,
                            tiles_x);
       else
@@ -520,7 +525,7 @@ __global__ void weight_prep16_kernel(const float* __restrict__ w, _Float16* __re
                                      const float* __restrict__ w_amax, int cout, int cin,
                                      int transpose, int gin16, int gout64) {
   const long long total = (long long)gin16 * 9 * 2 * gout64;
-  const float sw = __builtin_ldexpf(1.f, 15 - amax_exp(*w_amax));
+  const float sw = __builtin_ldexpf(1.f, 15 - amax_exp(read_amax(w_amax)));
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int e = (int)(i & 7);
@@ -599,7 +604,7 @@ extern "C" int stx_amax(const float* x, long long n, float* out, void* stream) {
     set_error("stx_amax: x must be 16-byte aligned");
     return STX_E_INVALID;
   }
-  hipError_t e = hipMemsetAsync(out, 0, sizeof(float), st);
+  hipError_t e = hipMemsetAsync(out, 0, STX_AMAX_SLOTS * sizeof(float), st);
   if (e != hipSuccess) {
     set_error("stx_amax: %s", hipGetErrorString(e));
     return (int)e;

@@ -45,10 +45,11 @@ __device__ __forceinline__ void atomic_max_abs(float* slot, float m) {
   atomicMax(reinterpret_cast<unsigned int*>(slot), __float_as_uint(m));
 }
 
-// max over the 256-thread block (NaN wins), then ONE device atomic per block: a
-// same-address atomic per wave costs ~12 ns each chip-wide (8192 of them stalled a
-// 64 MB pass for 100 us)
-__device__ __forceinline__ void block_max_to(float* slot, float m) {
+// max over the 256-thread block (NaN wins), then ONE device atomic per block into
+// one of the group's STX_AMAX_SLOTS slots: same-address atomics serialise at
+// ~12-15 ns each chip-wide (8192 of them stalled a 64 MB pass for 100 us; 1024 at a
+// conv's tail cost ~15 us)
+__device__ __forceinline__ void block_max_to(float* group, float m) {
   __shared__ float red[4];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -62,7 +63,8 @@ __device__ __forceinline__ void block_max_to(float* slot, float m) {
     float r = red[0];
 #pragma unroll
     for (int i = 1; i < 4; ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
-    atomic_max_abs(slot, fabsf(r));
+    const int bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    atomic_max_abs(group + (bid & (STX_AMAX_SLOTS - 1)), fabsf(r));
   }
 }
 

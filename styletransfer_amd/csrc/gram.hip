@@ -315,7 +315,7 @@ __device__ __forceinline__ void gram_f16_tile(const float* __restrict__ z, float
   const float* pb0 = zb + (size_t)min(rb0, c - 1) * hw + 8 * h;
   const float* pb1 = zb + (size_t)min(rb1, c - 1) * hw + 8 * h;
   const bool va0 = ra0 < c, va1 = ra1 < c, vb0 = rb0 < c, vb1 = rb1 < c;
-  const int e = gram_amax_exp(*z_amax);
+  const int e = gram_amax_exp(read_amax(z_amax));
   const float sx = __builtin_ldexpf(1.f, 15 - e);
   const float inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
 

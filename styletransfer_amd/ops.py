@@ -91,7 +91,7 @@ def conv_weight_prep16(w: torch.Tensor, transpose: bool = False):
     if nb == 0:
         raise N.NativeError(f"no fp16-split slab for a {ks}x{ks} conv")
     wt16 = torch.empty(nb, device=w.device, dtype=torch.uint8)
-    w_amax = torch.empty(1, device=w.device, dtype=torch.float32)
+    w_amax = torch.empty(N.STX_AMAX_SLOTS, device=w.device, dtype=torch.float32)
     check(L.stx_conv_weight_prep16(w.data_ptr(), wt16.data_ptr(), w_amax.data_ptr(), cout, cin,
                                    ks, int(transpose), _stream()), "conv_weight_prep16")
     return wt16, w_amax
@@ -103,10 +103,10 @@ def split_eligible(cin, cout, ks, stride=1):
 
 
 def amax(x: torch.Tensor, out=None):
-    """Device scalar max|x| (stx_amax)."""
+    """max|x| as an amax group (STX_AMAX_SLOTS floats whose max is the value)."""
     _req(x, "x")
     if out is None:
-        out = torch.empty(1, device=x.device, dtype=torch.float32)
+        out = torch.empty(N.STX_AMAX_SLOTS, device=x.device, dtype=torch.float32)
     check(lib().stx_amax(x.data_ptr(), x.numel(), out.data_ptr(), _stream()), "stx_amax")
     return out
 

@@ -111,9 +111,10 @@ class VGGFeatures:
         return (l + 1 < len(IN_MODES) and IN_MODES[l + 1] == N.STX_IN_RELU_POOL2
                 and self.wt16[l] is not None and self.wt16[l + 1] is not None and wo > 32)
 
-    def forward(self, x, upto=5, outs=None, amax=None, pools=None):
+    def forward(self, x, upto=5, outs=None, amax=None, pools=None, on_layer=None):
         """[Z1..Z_upto] (pre-ReLU conv outputs).  amax: device [>=5] slots, zeroed by
-        the caller; slot l+1 receives max|Z_l| (the next split conv's input scale).
+        the caller; slot l+1 receives max|Z_l| (the next split conv's input scale);
+        each slot is an amax group of N.STX_AMAX_SLOTS floats (slot(amax, k)).
         Where fuses_pool holds, conv l also writes P = maxpool(relu(Z_l)) (into
         pools[l] if given) and conv l+1 reads P directly."""
         zs, cur, pin = [], x, None
@@ -124,8 +125,8 @@ class VGGFeatures:
                 src, mode = pin, N.STX_IN_RAW
             kw = {}
             if amax is not None:
-                kw = dict(in_amax=amax[l:l + 1] if l > 0 else None,
-                          out_amax=amax[l + 1:l + 2])
+                kw = dict(in_amax=slot(amax, l) if l > 0 else None,
+                          out_amax=slot(amax, l + 1))
             pin = None
             if l + 1 < upto and self.fuses_pool(l, src.shape[3]):
                 shp = (src.shape[0], cout, src.shape[2] // 2, src.shape[3] // 2)
@@ -137,6 +138,8 @@ class VGGFeatures:
             cur = ops.conv2d(src, self.wt[l], cin, cout, 3, in_mode=mode, bias=self.b[l],
                              out=None if outs is None else outs[l], wt16=self.wt16[l], **kw)
             zs.append(cur)
+            if on_layer is not None:
+                on_layer(l, cur)
         return zs
 
     def style_targets(self, style_image):
@@ -171,34 +174,90 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     upstream gradient vector (autograd case)."""
     if st is None:
         st = LossState()
+    dev = x.device
     if st.amax is None:
-        st.amax = torch.zeros(16, device=x.device, dtype=torch.float32)
+        st.amax = torch.zeros(16 * N.STX_AMAX_SLOTS, device=dev, dtype=torch.float32)
     else:
         st.amax.zero_()
-    st.z = feat.forward(x, 5, st.z if st.z else None, amax=st.amax, pools=st.pools)
     if st.losses is None:
         # [style x5, content, feature, feature-mse]
-        st.losses = torch.empty(N_LOSSES + 1, device=x.device, dtype=torch.float32)
+        st.losses = torch.empty(N_LOSSES + 1, device=dev, dtype=torch.float32)
         st.fmean = st.losses[6:8]
     if not st.coef:
         st.coef = [None] * 5
-    z4 = st.z[CONTENT_CONV]
-    assert c4.shape == z4.shape, (c4.shape, z4.shape)
+    B, _, H, W = x.shape
+    z4_shape = (B, 128, H // 2, W // 2)
+    assert tuple(c4.shape) == z4_shape, (c4.shape, z4_shape)
     sw, alpha = 1.0, 0.0
     st.folded = folded_weights is not None
     if st.folded:
         sw = float(folded_weights[0])
-        alpha = float(folded_weights[1]) * 2.0 / z4.numel()
+        alpha = float(folded_weights[1]) * 2.0 / (B * 128 * (H // 2) * (W // 2))
     st.alpha = alpha
-    split = os.environ.get("STX_GRAM_SPLIT", "1") != "0"
-    for i, l in enumerate(STYLE_CONVS):
-        _, st.coef[i] = ops.style_loss(st.z[l], targets[i], weight=sw,
-                                       diag_alpha=alpha if l == CONTENT_CONV else 0.0,
-                                       loss=st.losses[i], coef=st.coef[i],
-                                       z_amax=st.amax[l + 1:l + 2] if split else None)
     st.c4 = c4
-    ops.mse(z4, c4, mode=2, out=st.losses[5:8])  # content, feature, feature-mse: one pass
+    split = os.environ.get("STX_GRAM_SPLIT", "1") != "0"
+    overlap = os.environ.get("STX_LOSS_STREAM", "0") != "0"  # measured slower (A/B)
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev) if overlap else main
+    capturing = False
+    if overlap:
+        # the side stream never grows the shared scratch buffer: size it here, on main
+        L = N.lib()
+        hw = [(64, H * W), (64, H * W), (128, (H // 2) * (W // 2)),
+              (128, (H // 2) * (W // 2)), (256, (H // 4) * (W // 4))]
+        need = max([L.stx_gram_ws(B, c, n) for c, n in hw] +
+                   [L.stx_mse_ws(B * 128 * (H // 2) * (W // 2))])
+        ops.WS.get(need, dev)
+        side.wait_stream(main)
+        capturing = torch.cuda.is_current_stream_capturing()
+        if not capturing:
+            for t in [st.losses, st.amax, c4] + [c for c in st.coef if c is not None]:
+                t.record_stream(side)
+
+    def on_layer(l, z):
+        # the style loss of layer l (and the content/feature losses at conv2_2) run on
+        # the side stream while the next conv runs: memory-bound reductions under
+        # compute-bound convs, joined before the backward
+        if overlap:
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            if not capturing:
+                z.record_stream(side)
+        with torch.cuda.stream(side):
+            i = STYLE_CONVS.index(l)
+            _, st.coef[i] = ops.style_loss(z, targets[i], weight=sw,
+                                           diag_alpha=alpha if l == CONTENT_CONV else 0.0,
+                                           loss=st.losses[i], coef=st.coef[i],
+                                           z_amax=slot(st.amax, l + 1) if split else None)
+            if l == CONTENT_CONV:  # content, feature, feature-mse: one pass
+                ops.mse(z, c4, mode=2, out=st.losses[5:8])
+
+    st.z = feat.forward(x, 5, st.z if st.z else None, amax=st.amax, pools=st.pools,
+                        on_layer=on_layer)
+    if overlap:
+        main.wait_stream(side)
+        if not capturing:
+            for c in st.coef:
+                c.record_stream(main)
     return st
+
+
+_SIDE = {}
+
+
+def slot(amax, k):
+    """The k-th amax group of a slot vector (include/stx.h STX_AMAX_SLOTS)."""
+    return amax[k * N.STX_AMAX_SLOTS:(k + 1) * N.STX_AMAX_SLOTS]
+
+
+def _side_stream(dev):
+    """Per-device secondary stream for the loss reductions (loss_forward)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _SIDE.get(key)
+    if s is None:
+        s = _SIDE[key] = torch.cuda.Stream(torch.device("cuda", key))
+    return s
 
 
 def loss_values(st: LossState):
@@ -232,17 +291,17 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
     # conv3_1 output: dZ5 = A5 Z5
     sp = feat.wt16[1] is not None  # split kernels in use
     dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4),
-                             out_amax=am[6:7], z_amax=am[5:6] if sp else None)
+                             out_amax=slot(am, 6), z_amax=slot(am, 5) if sp else None)
     # -> grad wrt pool(relu Z4)
     n4 = (B, 128, z[3].shape[2] // 2, z[3].shape[3] // 2)
-    dp2 = feat.dgrad(4, dz5, buf("dp2", n4), in_amax=am[6:7])
+    dp2 = feat.dgrad(4, dz5, buf("dp2", n4), in_amax=slot(am, 6))
     # dZ4 = unpool(dP2)*[Z4>0] + A4 Z4 (+ content)
     dz4 = ops.gram_bwd_fused(st.coef[3], z[3], out=buf("dz4", z[3].shape), acc_scale=s(3),
                              up_dp=dp2, aux=st.c4 if folded else None, aux_scale=-st.alpha,
-                             out_amax=am[7:8] if folded else None,
-                             z_amax=am[4:5] if sp else None)
+                             out_amax=slot(am, 7) if folded else None,
+                             z_amax=slot(am, 4) if sp else None)
     n = z[3].numel()
-    dz4_amax = am[7:8] if folded else None
+    dz4_amax = slot(am, 7) if folded else None
     if not folded:
         ops.diff_scale(z[3], st.c4, 2.0 / n, s1=g[5:6], out=dz4, accumulate=True)
         if feature_grad:
@@ -250,16 +309,16 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
                            s2=st.fmean[1:2], relu=True, out=dz4, accumulate=True)
     # dZ3 = conv2_2^T(dZ4)*[Z3>0] + A3 Z3
     dz3 = feat.dgrad(3, dz4, buf("dz3", z[2].shape), mask=z[2], p2_z=z[2],
-                     p2_coef=st.coef[2], p2_scale=s(2), in_amax=dz4_amax, out_amax=am[8:9],
-                     p2_amax=am[3:4])
+                     p2_coef=st.coef[2], p2_scale=s(2), in_amax=dz4_amax, out_amax=slot(am, 8),
+                     p2_amax=slot(am, 3))
     # -> grad wrt pool(relu Z2)
     n2 = (B, 64, z[1].shape[2] // 2, z[1].shape[3] // 2)
-    dp1 = feat.dgrad(2, dz3, buf("dp1", n2), in_amax=am[8:9])
+    dp1 = feat.dgrad(2, dz3, buf("dp1", n2), in_amax=slot(am, 8))
     dz2 = ops.gram_bwd_fused(st.coef[1], z[1], out=buf("dz2", z[1].shape), acc_scale=s(1),
-                             up_dp=dp1, out_amax=am[9:10], z_amax=am[2:3] if sp else None)
+                             up_dp=dp1, out_amax=slot(am, 9), z_amax=slot(am, 2) if sp else None)
     # dZ1 = conv1_2^T(dZ2)*[Z1>0] + A1 Z1
     dz1 = feat.dgrad(1, dz2, buf("dz1", z[0].shape), mask=z[0], p2_z=z[0],
-                     p2_coef=st.coef[0], p2_scale=s(0), in_amax=am[9:10], p2_amax=am[1:2])
+                     p2_coef=st.coef[0], p2_scale=s(0), in_amax=slot(am, 9), p2_amax=slot(am, 1))
     # conv1_1 dgrad -> image
     xs = (B, 3, z[0].shape[2], z[0].shape[3])
     if dx is None:

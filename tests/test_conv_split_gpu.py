@@ -57,7 +57,7 @@ def test_split_conv_fwd(dev, case):
     b = rnd(cout, dev=dev, seed=3)
     wt = ops.conv_weight_prep(wgt)
     w16 = ops.conv_weight_prep16(wgt)
-    amax = torch.zeros(1, device=dev)
+    amax = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
     y = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=b, wt16=w16, out_amax=amax)
     y32 = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=b)
     ref = F.conv2d(vinput(x.double().cpu(), mode), wgt.double().cpu(), b.double().cpu(),
@@ -66,7 +66,7 @@ def test_split_conv_fwd(dev, case):
     assert y.shape == ref.shape
     e16, e32 = rel(y, ref), rel(y32, ref)
     assert e16 < TOL64, (e16, e32)
-    assert float(amax) == float(y.abs().max())
+    assert float(amax.max()) == float(y.abs().max())
 
 
 @pytest.mark.parametrize("scale", [1e-9, 1.0, 3e4])
@@ -138,8 +138,12 @@ def test_split_conv_fused_epilogue(dev):
 def test_amax(dev):
     x = rnd(3, 5, 7, 11, dev=dev, seed=7, scale=4, shift=-2)
     x.view(-1)[123] = -9.5
-    assert float(ops.amax(x)) == 9.5
-    assert float(ops.amax(torch.zeros(0, device=dev))) == 0.0
+    assert float(ops.amax(x).max()) == 9.5
+    assert float(ops.amax(torch.zeros(0, device=dev)).max()) == 0.0
+    big = rnd(1 << 22, dev=dev, seed=8, scale=2, shift=-1)
+    big[777777] = 3.25
+    g = ops.amax(big)
+    assert g.numel() == N.STX_AMAX_SLOTS and float(g.max()) == 3.25
 
 
 @pytest.mark.parametrize("shape", [(2, 64, 64, 20, 70), (1, 128, 128, 17, 99)])

@@ -71,7 +71,7 @@ def main():
             kw = {}
             if "conv1_2" in name:  # the Gatys launch: + relu/pool output, out_amax
                 kw = dict(pool_out=torch.empty(n, cout, ho // 2, wo // 2, device=dev),
-                          out_amax=torch.zeros(1, device=dev))
+                          out_amax=torch.zeros(N.STX_AMAX_SLOTS, device=dev))
             ms16 = ev(lambda: ops.conv2d(x, wt, cin, cout, ks, stride=s, in_mode=mode, out=out,
                                          wt16=w16, in_amax=am, **kw))
             line += f" | f16x3 {ms16 * 1e3:9.1f} us {gf / ms16:7.2f} TF"
