@@ -83,6 +83,7 @@ def parse():
     ap.add_argument("--fast-batch", type=int, default=8, help="fast_st images per GPU")
     ap.add_argument("--fast-steps", type=int, default=0, help="default: max(2, steps//10)")
     ap.add_argument("--skip-fast", action="store_true")
+    ap.add_argument("--fast-only", action="store_true", help="profiling: fast_st leg only")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=4)
     ap.add_argument("--no-graph", action="store_true")
@@ -216,6 +217,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     N.lib()
+    if args.fast_only:
+        fs = fast_st_leg(args, world, rank, dev)
+        if rank == 0:
+            print(json.dumps({"fast_st_images_per_s": round(fs["rate"], 3),
+                              "ms_per_step": round(1e3 * fs["dt"] / fs["steps"], 3)}))
+        return
     g = gatys_leg(args, world, rank, dev)
     fs = None if args.skip_fast else fast_st_leg(args, world, rank, dev)
     cpu = None
