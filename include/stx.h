@@ -141,6 +141,15 @@ int stx_conv2d_wgrad(const float* x, const float* dy, float* dw, int accumulate,
                      int n, int cin, int h, int w, int cout, int ks, int stride, int pad,
                      int in_mode, int hv, int wv, int ho, int wo,
                      void* ws, size_t ws_bytes, void* stream);
+/* Weight gradient of a 3x3 stride-1 pad-1 conv on the fp16 hi/lo split MFMA
+ * (in_mode RAW / RELU / UPSAMPLE2, hv x wv = dy's spatial size with wv % 16 == 0,
+ * cin and cout >= 16); x_amax / dy_amax are amax groups of x and dy.  Split-K
+ * partials in ws (stx_conv2d_wgrad16_ws, 0 = unsupported shape), fixed-order sum. */
+size_t stx_conv2d_wgrad16_ws(int n, int cin, int cout, int in_mode, int hv, int wv);
+int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, int accumulate, int n,
+                       int cin, int h, int w, int cout, int in_mode, int hv, int wv,
+                       const float* x_amax, const float* dy_amax, void* ws, size_t ws_bytes,
+                       void* stream);
 /* db[c] (+)= sum_{n,p} dy[n][c][p]  (conv bias gradient) */
 size_t stx_bias_grad_ws(int n, int c);
 int stx_bias_grad(const float* dy, float* db, int n, int c, int hw, int accumulate,

@@ -53,6 +53,9 @@ SIGNATURES = {
     "stx_conv2d_wgrad_ws": (sz, [i32, i32, i32, i32, i32, i32, i32]),
     "stx_conv2d_wgrad": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                i32, i32, i32, i32, vp, sz, vp]),
+    "stx_conv2d_wgrad16_ws": (sz, [i32, i32, i32, i32, i32, i32]),
+    "stx_conv2d_wgrad16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                                 vp, sz, vp]),
     "stx_bias_grad_ws": (sz, [i32, i32]),
     "stx_bias_grad": (i32, [vp, vp, i32, i32, i32, i32, vp, sz, vp]),
     "stx_gram_ws": (sz, [i32, i32, i32]),

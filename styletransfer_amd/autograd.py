@@ -14,19 +14,28 @@ def _c(t):
     return t.contiguous() if t is not None and not t.is_contiguous() else t
 
 
+def _split_on():
+    import os
+    return os.environ.get("STX_CONV_SPLIT", "1") != "0"
+
+
 # ----------------------------------------------------------------------- conv
 class Conv2dFn(torch.autograd.Function):
     """y = conv2d(V(x), w) + b with V = identity / relu / nearest-upsample-x2.
     (nn.Conv2d of VGG-19 and ImageTransformNet; zero padding.)"""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, in_mode, wt=None):
+    def forward(ctx, x, w, b, stride, pad, in_mode, wt=None, wt16=None):
         x = _c(x)
         cout, cin, ks, _ = w.shape
         if wt is None:
             wt = ops.conv_weight_prep(w.detach().contiguous())
+        # 3x3 stride-1 layers with cin >= 16 run on the fp16 hi/lo split MFMA kernel
+        split = _split_on() and pad == 1 and ops.split_eligible(cin, cout, ks, stride)
+        if split and wt16 is None:
+            wt16 = ops.conv_weight_prep16(w.detach().contiguous())
         y = ops.conv2d(x, wt, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
-                       bias=None if b is None else b.detach())
+                       bias=None if b is None else b.detach(), wt16=wt16 if split else None)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, in_mode, b is not None)
         return y
@@ -43,7 +52,10 @@ class Conv2dFn(torch.autograd.Function):
             h, wd = x.shape[2], x.shape[3]
             hv, wv = ops.virtual_hw(h, wd, in_mode)
             if stride == 1:
-                dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad)
+                wtT16 = None
+                if _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1):
+                    wtT16 = ops.conv_weight_prep16(w.detach().contiguous(), transpose=True)
+                dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16)
             elif stride == 2:
                 dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad,
                                 in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv)
@@ -61,12 +73,12 @@ class Conv2dFn(torch.autograd.Function):
             dw = ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode)
         if has_b and ctx.needs_input_grad[2]:
             db = ops.bias_grad(dy)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
-def conv2d(x, w, b=None, stride=1, pad=None, in_mode=N.STX_IN_RAW, wt=None):
+def conv2d(x, w, b=None, stride=1, pad=None, in_mode=N.STX_IN_RAW, wt=None, wt16=None):
     ks = w.shape[-1]
-    return Conv2dFn.apply(x, w, b, stride, ks // 2 if pad is None else pad, in_mode, wt)
+    return Conv2dFn.apply(x, w, b, stride, ks // 2 if pad is None else pad, in_mode, wt, wt16)
 
 
 # ----------------------------------------------------------------------- relu / pool

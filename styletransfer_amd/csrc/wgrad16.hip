@@ -1,0 +1,302 @@
+// 3x3 stride-1 convolution weight gradient on the fp16 hi/lo split MFMA
+// (v_mfma_f32_32x32x16_f16; numerics as conv16.hip: both operands scaled by a
+// per-tensor power of two and split s*v = hi + lo, hi*hi + hi*lo + lo*hi in fp32).
+//
+//   dW[co][ci][kh][kw] = sum_{n,y,x} dY[n][co][y][x] * V[n][ci][y+kh-1][x+kw-1]
+//
+// For each tap row kh this is three GEMMs (kw = 0,1,2) with M = cout, N = cin and
+// K = every output pixel, whose B operands are the same input row shifted by one
+// pixel.  A wave owns one (32 couts, 32 cins, kh) unit over one K split and keeps
+// the three kw accumulators: per 16-pixel step each lane loads 8 pixels of its dY
+// row (two float4) and 10 pixels of its V row (two float4 + the two neighbours),
+// splits them once and forms the three shifted B fragments in registers -- no LDS,
+// no im2col.  The four waves of a block take four consecutive cin tiles of the
+// same (cout tile, kh, split), so their identical dY loads hit L1.  Each wave
+// writes its partial [split][kh][kw][co][ci]; a second kernel sums the splits in a
+// fixed order (bit-reproducible; no float atomics).
+//
+// Reference: autograd of the ImageTransformNet 3x3 convs trained by static_train
+// (stransfer/network.py:468-481, 525-609, :690-765).
+#include "common.h"
+#include "../../include/stx.h"
+
+namespace stx {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int wg_amax_exp(float a) {
+  int e = 0;
+  frexpf(a, &e);
+  return min(max(e, -60), 60);
+}
+
+struct Wg16 {
+  int n, cin, h, w, cout, mode, hv, wv;  // x physical [n][cin][h][w]; V/dY are hv x wv
+  int ncot, ncit, nsplit, steps, steps_per_split;
+  int cout32, cin32;
+};
+
+__global__ void __launch_bounds__(256)
+wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ ws,
+               const float* __restrict__ x_amax, const float* __restrict__ dy_amax, Wg16 g) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  int unit = blockIdx.x * 4 + wave;
+  const int cit = unit % g.ncit;
+  unit /= g.ncit;
+  const int cot = unit % g.ncot;  // pair of 32-cout tiles (64 couts)
+  unit /= g.ncot;
+  const int kh = unit % 3;
+  const int split = unit / 3;
+  if (split >= g.nsplit) return;  // (no barriers in this kernel)
+
+  const int ex = wg_amax_exp(read_amax(x_amax)), ed = wg_amax_exp(read_amax(dy_amax));
+  const float sv = __builtin_ldexpf(1.f, 15 - ex), sd = __builtin_ldexpf(1.f, 15 - ed);
+  const float descale = __builtin_ldexpf(1.f, ex + ed - 30);
+
+  const int co = cot * 64 + l32, ci = cit * 32 + l32;
+  const bool co_ok = co < g.cout, co2_ok = co + 32 < g.cout, ci_ok = ci < g.cin;
+  const int H = g.hv, W = g.wv, wsteps = W / 16;
+  const bool relu = g.mode == STX_IN_RELU, up = g.mode == STX_IN_UPSAMPLE2;
+
+  f32x16 acc[2][3];  // [cout tile][kw]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
+
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  struct Step {
+    f32x4 a0, a1;   // dY[co][y][x0+8h .. +7]
+    f32x4 c0, c1;   // dY[co+32][y][x0+8h .. +7]
+    f32x4 b0, b1;   // V[ci][vy][x0+8h .. +7] (b1 unused for the upsample loader)
+    float bl, br;   // V at x0+8h-1 and x0+8h+8
+  };
+  // running (image, row, 16-pixel column step) of the next load: loads are issued in
+  // step order, so no integer division per step
+  int ln, ly, lxs;
+  auto load = [&](Step& t) {
+    const int n = ln, y = ly, x0 = lxs * 16 + 8 * h;
+    if (++lxs == wsteps) {
+      lxs = 0;
+      if (++ly == H) {
+        ly = 0;
+        ++ln;
+      }
+    }
+    const float* pa = dy + (((size_t)n * g.cout + co) * H + y) * W + x0;
+    if (co_ok) {
+      t.a0 = *reinterpret_cast<const f32x4*>(pa);
+      t.a1 = *reinterpret_cast<const f32x4*>(pa + 4);
+    } else {
+      t.a0 = t.a1 = zero4;
+    }
+    if (co2_ok) {
+      const float* pc = pa + (size_t)32 * H * W;
+      t.c0 = *reinterpret_cast<const f32x4*>(pc);
+      t.c1 = *reinterpret_cast<const f32x4*>(pc + 4);
+    } else {
+      t.c0 = t.c1 = zero4;
+    }
+    const int vy = y + kh - 1;
+    t.b0 = t.b1 = zero4;
+    t.bl = t.br = 0.f;
+    if (ci_ok && vy >= 0 && vy < H) {
+      if (!up) {
+        const float* pb = x + (((size_t)n * g.cin + ci) * g.h + vy) * g.w + x0;
+        t.b0 = *reinterpret_cast<const f32x4*>(pb);
+        t.b1 = *reinterpret_cast<const f32x4*>(pb + 4);
+        if (x0 > 0) t.bl = pb[-1];
+        if (x0 + 8 < W) t.br = pb[8];
+      } else {  // V[vy][vx] = x[vy/2][vx/2]; x0 is even
+        const float* pb = x + (((size_t)n * g.cin + ci) * g.h + (vy >> 1)) * g.w + (x0 >> 1);
+        t.b0 = *reinterpret_cast<const f32x4*>(pb);
+        if (x0 > 0) t.bl = pb[-1];
+        if (x0 + 8 < W) t.br = pb[4];
+      }
+    }
+  };
+  auto compute = [&](const Step& t) {
+    float av[8] = {t.a0[0], t.a0[1], t.a0[2], t.a0[3], t.a1[0], t.a1[1], t.a1[2], t.a1[3]};
+    float bv[10];
+    bv[0] = t.bl;
+    bv[9] = t.br;
+    if (!up) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bv[1 + e] = t.b0[e];
+        bv[5 + e] = t.b1[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[1 + 2 * e] = bv[2 + 2 * e] = t.b0[e];
+    }
+    float cv[8] = {t.c0[0], t.c0[1], t.c0[2], t.c0[3], t.c1[0], t.c1[1], t.c1[2], t.c1[3]};
+    h8 ah[2], al[2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = av[e] * sd, w2 = cv[e] * sd;
+      const _Float16 vh = (_Float16)v, wh = (_Float16)w2;
+      ah[0][e] = vh;
+      al[0][e] = (_Float16)(v - (float)vh);
+      ah[1][e] = wh;
+      al[1][e] = (_Float16)(w2 - (float)wh);
+    }
+    _Float16 bh[10], bl[10];
+#pragma unroll
+    for (int e = 0; e < 10; ++e) {
+      float v = bv[e];
+      if (relu) v = fmaxf(v, 0.f);
+      v *= sv;
+      bh[e] = (_Float16)v;
+      bl[e] = (_Float16)(v - (float)bh[e]);
+    }
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      h8 fh, fl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        fh[e] = bh[e + kw];
+        fl[e] = bl[e + kw];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], fh, acc[i][kw], 0, 0, 0);
+        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], fl, acc[i][kw], 0, 0, 0);
+        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], fh, acc[i][kw], 0, 0, 0);
+      }
+    }
+  };
+
+  // four steps of loads in flight (HBM latency >> one step of 9 MFMAs)
+  const int s0 = split * g.steps_per_split;
+  const int s1 = min(g.steps, s0 + g.steps_per_split);
+  constexpr int PF = 4;
+  {
+    const int r0 = s0 / wsteps;
+    lxs = s0 - r0 * wsteps;
+    ln = r0 / H;
+    ly = r0 - ln * H;
+  }
+  Step ring[PF];
+#pragma unroll
+  for (int k = 0; k < PF; ++k)
+    if (s0 + k < s1) load(ring[k]);
+  for (int s = s0; s < s1; s += PF) {
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      if (s + k < s1) {
+        compute(ring[k]);
+        if (s + k + PF < s1) load(ring[k]);
+      }
+    }
+  }
+  // partial [split][kh*3+kw][co (cout32)][ci (cin32)], descaled (exact)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      float* out = ws + (((size_t)split * 9 + kh * 3 + kw) * g.cout32 + cot * 64 + i * 32) *
+                            g.cin32 + cit * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[(size_t)row * g.cin32] = acc[i][kw][r] * descale;
+      }
+    }
+}
+
+// dW[co][ci][kh][kw] (+)= sum over splits (fixed order); thread -> (tap, co, ci), ci fastest
+__global__ void wgrad16_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
+                                      Wg16 g, int accumulate) {
+  const long long per = (long long)g.cout * g.cin;
+  const long long total = per * 9;
+  const size_t sstride = (size_t)9 * g.cout32 * g.cin32;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int tap = (int)(i / per);
+    const long long rem = i - tap * per;
+    const int co = (int)(rem / g.cin), ci = (int)(rem - (long long)co * g.cin);
+    const float* src = ws + ((size_t)tap * g.cout32 + co) * g.cin32 + ci;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    for (; k + 7 < g.nsplit; k += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += src[(size_t)(k + u) * sstride];
+    }
+    for (int u = 0; k < g.nsplit; ++k, ++u) a[u] += src[(size_t)k * sstride];
+    const float s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    float* d = dw + ((size_t)co * g.cin + ci) * 9 + tap;
+    *d = accumulate ? *d + s : s;
+  }
+}
+
+static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg16& g) {
+  if (wv % 16 != 0 || cin < 16 || cout < 16 || n <= 0 || hv <= 0) return false;
+  if (in_mode != STX_IN_RAW && in_mode != STX_IN_RELU && in_mode != STX_IN_UPSAMPLE2) return false;
+  g.n = n;
+  g.cin = cin;
+  g.cout = cout;
+  g.mode = in_mode;
+  g.hv = hv;
+  g.wv = wv;
+  g.ncot = cdiv(cout, 64);  // a wave takes 64 couts (two 32-row MFMA tiles)
+  g.ncit = cdiv(cin, 32);
+  g.cout32 = g.ncot * 64;
+  g.cin32 = g.ncit * 32;
+  g.steps = n * hv * (wv / 16);
+  const int units = 3 * g.ncot * g.ncit;
+  int ns = cdiv(1024, units);                     // ~1024 waves
+  ns = std::max(1, std::min(ns, cdiv(g.steps, 8)));  // >= 8 steps per wave
+  g.steps_per_split = cdiv(g.steps, ns);
+  g.nsplit = cdiv(g.steps, g.steps_per_split);
+  return true;
+}
+
+}  // namespace stx
+
+using namespace stx;
+
+extern "C" size_t stx_conv2d_wgrad16_ws(int n, int cin, int cout, int in_mode, int hv, int wv) {
+  Wg16 g;
+  if (!wg16_plan(n, cin, cout, in_mode, hv, wv, g)) return 0;
+  return (size_t)g.nsplit * 9 * g.cout32 * g.cin32 * sizeof(float);
+}
+
+extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, int accumulate,
+                                  int n, int cin, int h, int w, int cout, int in_mode, int hv,
+                                  int wv, const float* x_amax, const float* dy_amax, void* ws,
+                                  size_t ws_bytes, void* stream) {
+  Wg16 g;
+  if (!x || !dy || !dw || !x_amax || !dy_amax || !wg16_plan(n, cin, cout, in_mode, hv, wv, g)) {
+    set_error("stx_conv2d_wgrad16: unsupported shape/mode or NULL argument");
+    return STX_E_INVALID;
+  }
+  g.h = h;
+  g.w = w;
+  if ((in_mode == STX_IN_UPSAMPLE2 && (hv != 2 * h || wv != 2 * w)) ||
+      (in_mode != STX_IN_UPSAMPLE2 && (hv != h || wv != w))) {
+    set_error("stx_conv2d_wgrad16: virtual dims do not match the input mode");
+    return STX_E_INVALID;
+  }
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy)) & 15) {
+    set_error("stx_conv2d_wgrad16: 16-byte aligned tensors required");
+    return STX_E_INVALID;
+  }
+  const size_t need = stx_conv2d_wgrad16_ws(n, cin, cout, in_mode, hv, wv);
+  if (!ws || ws_bytes < need) {
+    set_error("stx_conv2d_wgrad16: workspace %zu < %zu", ws_bytes, need);
+    return STX_E_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int units = g.nsplit * 3 * g.ncot * g.ncit;
+  hipLaunchKernelGGL(wgrad16_kernel, dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy, (float*)ws,
+                     x_amax, dy_amax, g);
+  const long long total = (long long)cout * cin * 9;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(wgrad16_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, dw,
+                     g, accumulate);
+  return check_launch("stx_conv2d_wgrad16");
+}

@@ -31,17 +31,26 @@ class Conv2d(nn.Conv2d):
         self._wt_cache = None
 
     def prepped(self):
-        """Cached GEMM slab of a frozen weight (re-prepped when the weight changes)."""
+        """Cached GEMM slabs (fp32, and the fp16 hi/lo split slab where the shape
+        takes the split kernel) of a frozen weight; re-prepped when it changes."""
         w = self.weight
         key = (w.data_ptr(), w._version, w.device)
         if self._wt_cache is None or self._wt_cache[0] != key:
             from . import ops
-            self._wt_cache = (key, ops.conv_weight_prep(w.detach().contiguous()))
-        return self._wt_cache[1]
+            wd = w.detach().contiguous()
+            cout, cin, ks, _ = wd.shape
+            w16 = ops.conv_weight_prep16(wd) if (A._split_on() and self.padding[0] == 1 and
+                                                 ops.split_eligible(cin, cout, ks, self.stride[0])) \
+                else None
+            self._wt_cache = (key, ops.conv_weight_prep(wd), w16)
+        return self._wt_cache[1], self._wt_cache[2]
 
     def forward(self, x, in_mode=N.STX_IN_RAW):
-        wt = None if self.weight.requires_grad else self.prepped()
-        return A.conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], in_mode, wt)
+        wt = wt16 = None
+        if not self.weight.requires_grad:
+            wt, wt16 = self.prepped()
+        return A.conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], in_mode, wt,
+                        wt16)
 
 
 class ReLU(nn.ReLU):

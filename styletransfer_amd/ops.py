@@ -185,7 +185,9 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
 
 
 def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, dw=None,
-                 accumulate=False):
+                 accumulate=False, split=True):
+    """dW (+)= sum dy * V(x); 3x3 stride-1 shapes run on the fp16 hi/lo split MFMA
+    (stx_conv2d_wgrad16) unless split=False or STX_CONV_SPLIT=0."""
     _req(x, "x")
     _req(dy, "dy")
     n, _, h, w = x.shape
@@ -196,6 +198,19 @@ def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW,
     if dw is None:
         dw = torch.empty((cout, cin, ks, ks), device=x.device, dtype=torch.float32)
     L = lib()
+    import os
+    if (split and ks == 3 and stride == 1 and pad == 1 and
+            os.environ.get("STX_CONV_SPLIT", "1") != "0"):
+        need16 = L.stx_conv2d_wgrad16_ws(n, cin, cout, in_mode, ho, wo)
+        if need16:
+            _req(dy, "dy")
+            xa, da = amax(x), amax(dy)
+            wp, wn = WS.get(need16, x.device)
+            check(L.stx_conv2d_wgrad16(x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
+                                       int(accumulate), n, cin, h, w, cout, in_mode, ho, wo,
+                                       xa.data_ptr(), da.data_ptr(), wp, wn, _stream()),
+                  "stx_conv2d_wgrad16")
+            return dw
     need = L.stx_conv2d_wgrad_ws(n, cin, cout, ks, stride, ho, wo)
     wp, wn = WS.get(need, x.device)
     check(L.stx_conv2d_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(accumulate), n, cin,

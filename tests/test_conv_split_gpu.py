@@ -217,3 +217,24 @@ def test_split_gram_bwd(dev, shape):
     A = coef.double().cpu()[:, :c, :c]
     ref = torch.bmm(A.transpose(1, 2), f).reshape(n, c, h, w)
     assert rel(b16, ref) < TOL64
+
+
+@pytest.mark.parametrize("case", [(8, 128, 128, 16, 32, N.STX_IN_RAW),
+                                  (2, 64, 32, 20, 16, N.STX_IN_RELU),
+                                  (2, 128, 64, 8, 16, N.STX_IN_UPSAMPLE2),
+                                  (3, 40, 24, 9, 48, N.STX_IN_RAW)])
+def test_split_wgrad(dev, case):
+    """3x3 weight gradient on the split MFMA vs fp64 (and the fp32 MFMA kernel)."""
+    n, cin, cout, h, w, mode = case
+    x = rnd(n, cin, h, w, dev=dev, seed=61, scale=2, shift=-1)
+    xv = vinput(x.double().cpu(), mode)
+    wgt = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(xv, wgt, padding=1)
+    dy = rnd(*y.shape, dev=dev, seed=62, scale=2e-3, shift=-1e-3)
+    (ref,) = torch.autograd.grad(y, wgt, dy.double().cpu())
+    dw16 = ops.conv2d_wgrad(x, dy, cin, cout, 3, in_mode=mode)
+    dw32 = ops.conv2d_wgrad(x, dy, cin, cout, 3, in_mode=mode, split=False)
+    assert rel(dw16, ref) < TOL64, (rel(dw16, ref), rel(dw32, ref))
+    acc = dw16.clone()
+    ops.conv2d_wgrad(x, dy, cin, cout, 3, in_mode=mode, dw=acc, accumulate=True)
+    assert rel(acc, 2 * ref) < TOL64

@@ -104,9 +104,13 @@ def main():
         x = torch.randn(n, cin, h, h, generator=g).to(dev)
         ho = (h + 2 * (ks // 2) - ks) // s + 1
         dy = torch.randn(n, cout, ho, ho, generator=g).to(dev)
-        ms = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s), reps=10)
+        ms = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s, split=False), reps=10)
         gf = 2.0 * n * cin * cout * ks * ks * ho * ho / 1e9
-        print(f"{name:32s} {ms * 1e3:9.1f} us  {gf / ms:8.2f} TFLOP/s")
+        line = f"{name:32s} fp32 {ms * 1e3:9.1f} us {gf / ms:7.2f} TF"
+        if ks == 3 and s == 1:
+            ms16 = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s), reps=10)
+            line += f" | f16x3 {ms16 * 1e3:9.1f} us {gf / ms16:7.2f} TF (incl. 2 amax passes)"
+        print(line, flush=True)
 
 
 if __name__ == "__main__":
