@@ -153,9 +153,15 @@ def gatys_leg(args, world, rank, dev):
                           reps=20)
     gf = conv_gflop(64, 64, H, H)
     achieved = gf / (fwd_ms * 1e-3) / 1e3  # TFLOP/s
+    # the style-loss Gram of conv1_2's output (C=64, HW=H^2): split partials + finalize
+    z2 = eng.st.z[1]
+    zam = V.slot(eng.st.amax, 2).clone()
+    gram_ms = event_avg_ms(lambda: ops.gram(z2, z_amax=zam), reps=20)
     loss = float(eng.total)
     return dict(rate=rate, dt=dt, loss=loss, kernel=dict(fwd_ms=fwd_ms, gflop=gf,
-                                                         tflops=achieved))
+                                                         tflops=achieved),
+                gram=dict(ms=gram_ms, gflop=2.0 * 64 * 64 * H * H / 1e9,
+                          bytes=64 * H * H * 4))
 
 
 def fast_st_leg(args, world, rank, dev):
@@ -268,6 +274,19 @@ def main():
                 "algorithmic_bytes": CONV1_2_BYTES if args.size == 512 else None,
                 "iteration_tflops": round(GATYS_GFLOP.get(args.size, float("nan")) * g["rate"]
                                           / world / 1e3, 3),
+            },
+            "gram_roofline": {
+                "kernel": "gram_partial_f16_kernel + gram_finalize_kernel (StyleLoss.gram_matrix "
+                          f"of conv1_2's output, C=64, HW={args.size}^2)",
+                "ms": round(g["gram"]["ms"], 4),
+                "achieved_tflops_fp32eq": round(g["gram"]["gflop"] / g["gram"]["ms"], 2),
+                "mfma_bf16_peak_frac": round(3 * g["gram"]["gflop"] / g["gram"]["ms"]
+                                             / PEAK_F16_MFMA_TFLOPS, 4),
+                "hbm_gbs": round(g["gram"]["bytes"] / (g["gram"]["ms"] * 1e-3) / 1e9, 1),
+                "hbm_frac": round(g["gram"]["bytes"] / (g["gram"]["ms"] * 1e-3) / 1e9
+                                  / PEAK_HBM_GBS, 4),
+                "note": "HBM-bound: 2*C^2*HW FLOPs over C*HW*4 bytes = 32 FLOP/B; the MFMA "
+                        "fraction counts the 3 fp16 products per fp32 product",
             },
             "cpu_baseline": cpu,
             "gatys_loss": g["loss"],

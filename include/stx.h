@@ -197,6 +197,22 @@ int stx_diff_scale(const float* a, const float* b, float* grad, long long n, flo
 /* *out = sum_i w_host[i] * s[i]   (k <= 16 device scalars, fixed order) */
 int stx_loss_combine(const float* s, int k, const float* w_host, float* out, void* stream);
 
+/* Vector kernels of the on-device L-BFGS (StyleNetwork.train_gatys' optimiser,
+ * stransfer/network.py:435; torch.optim.LBFGS semantics):
+ *   stx_vec_reduce: r = dot(a,b) (op 0), sum|a| (op 1) or max|a| (op 2) over n floats
+ *     (fixed-order two-stage reduction, ws >= stx_vec_ws()), then
+ *     *out = (add ? *add : 0) + sgn * r * (mul ? *mul : 1)   (device scalars)
+ *   stx_vec_axpby: y = alpha*x + b*y, alpha = a_dev ? a_sgn * (*a_dev) * a : a
+ *   stx_scalar_op: s[k] = s[i] op s[j]  (0 div, 1 mul, 2 sub, 3 add, 4 1/s[i],
+ *     5 min(s[j], 1/s[i])) on a device scalar array */
+size_t stx_vec_ws(void);
+int stx_vec_reduce(const float* a, const float* b, long long n, int op, float* out,
+                   const float* mul, const float* add, float sgn, void* ws, size_t ws_bytes,
+                   void* stream);
+int stx_vec_axpby(float* y, const float* x, long long n, float a, const float* a_dev,
+                  float a_sgn, float b, void* stream);
+int stx_scalar_op(float* s, int op, int i, int j, int k, void* stream);
+
 /* MaxPool2d(2,2) on (optionally relu'd) input; idx = flat y*w+x argmax per plane,
  * torch CPU semantics (first max in row-major window order; NaN propagates). idx may be NULL. */
 int stx_maxpool2x2_fwd(const float* x, float* y, long long* idx, int nc, int h, int w,

@@ -318,6 +318,8 @@ class StyleNetwork(nn.Module):
         """stransfer/network.py:403-409 (optim.Adam -> the HIP Adam)."""
         if optt is None or optt is optim.Adam:
             optt = stx_optim.Adam
+        elif optt is optim.LBFGS:
+            optt = stx_optim.LBFGS
         return optt([input_img.requires_grad_()])
 
     def train_gatys(self, style_image: torch.Tensor, content_image: torch.Tensor, steps=550,
@@ -327,7 +329,7 @@ class StyleNetwork(nn.Module):
         assert isinstance(content_image, torch.Tensor), "Images need to be already loaded"
         content_image = _dev(content_image)
         image = content_image.clone()
-        opt = self.get_content_optimizer(image, optt=optim.LBFGS)
+        opt = self.get_content_optimizer(image, optt=optim.LBFGS)  # -> the HIP L-BFGS
 
         def closure():
             opt.zero_grad()

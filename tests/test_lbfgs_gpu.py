@@ -1,0 +1,75 @@
+"""On-device L-BFGS (styletransfer_amd.optim.LBFGS) vs torch.optim.LBFGS.
+
+StyleNetwork.train_gatys runs `optim.LBFGS` with its defaults
+(stransfer/network.py:435); our LBFGS restates torch's algorithm on libstx vector
+kernels.  Same closure, same inputs: trajectories must agree to reduction-order
+rounding (dot products are summed in a different order)."""
+import pytest
+import torch
+
+from styletransfer_amd import network
+from styletransfer_amd import optim as stx_optim
+from styletransfer_amd import weights as W
+
+pytestmark = pytest.mark.gpu
+
+
+def quad_problem(dev, n=4096, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    m = (torch.randn(n, generator=g).abs() + 0.5).to(dev)     # diagonal curvature
+    b = torch.randn(n, generator=g).to(dev)
+    x0 = torch.randn(n, generator=g).to(dev)
+    return m, b, x0
+
+
+@pytest.mark.parametrize("history", [100, 3])
+def test_lbfgs_matches_torch_on_quadratic(dev, history):
+    m, b, x0 = quad_problem(dev)
+    xs = []
+    for cls in (torch.optim.LBFGS, stx_optim.LBFGS):
+        x = x0.clone().view(1, -1).requires_grad_()
+        opt = cls([x], history_size=history)
+
+        def closure():
+            opt.zero_grad()
+            f = 0.5 * ((m * x.view(-1) - b) ** 2).sum() + 0.1 * (x ** 4).sum()
+            f.backward()
+            return f
+
+        for _ in range(4):
+            opt.step(closure)
+        xs.append(x.detach().clone())
+    err = float((xs[0] - xs[1]).norm() / xs[0].norm())
+    assert err < 1e-4, err
+
+
+def test_lbfgs_gatys(dev):
+    """train_gatys (L-BFGS) on the HIP closure: the native optimiser and torch's give
+    the same losses after two outer steps."""
+    s = torch.from_numpy(W.synthetic_image(21, (1, 3, 64, 64))).to(dev)
+    c = torch.from_numpy(W.synthetic_image(22, (1, 3, 64, 64))).to(dev)
+    finals = []
+    for cls in (torch.optim.LBFGS, stx_optim.LBFGS):
+        net = network.StyleNetwork(s, c)
+        x = c.clone()
+        opt = cls([x.requires_grad_()])
+
+        def closure():
+            opt.zero_grad()
+            net(x, c)
+            tot = net.get_total_current_style_loss(100_000) + net.get_total_current_content_loss(1)
+            tot.backward()
+            return tot
+
+        def value():
+            with torch.no_grad():
+                net(x, c)
+                return float(net.get_total_current_style_loss(100_000)
+                             + net.get_total_current_content_loss(1))
+
+        first = value()
+        for _ in range(2):
+            opt.step(closure)
+        finals.append(value())
+    assert finals[1] < 0.5 * first
+    assert abs(finals[0] - finals[1]) <= 2e-3 * abs(finals[0]), finals
