@@ -85,6 +85,7 @@ def parse():
     ap.add_argument("--skip-fast", action="store_true")
     ap.add_argument("--fast-only", action="store_true", help="profiling: fast_st leg only")
     ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--skip-infer", action="store_true", help="skip the video/convert legs")
     ap.add_argument("--cpu-iters", type=int, default=4)
     ap.add_argument("--no-graph", action="store_true")
     return ap.parse_args()
@@ -181,6 +182,43 @@ def fast_st_leg(args, world, rank, dev):
     return dict(rate=ips, dt=dt, steps=steps, batch=B)
 
 
+def video_leg(args, world, rank, dev):
+    """BASELINE config 5: video_st per-frame step at IMSIZE^2 (frames are conditioned to
+    IMSIZE before the network, stransfer/dataset.py:280-310), one hipGraph replay per
+    frame incl. the temporal-loss norms; frames resident in HBM (decode/resize excluded)."""
+    from styletransfer_amd import network, video
+    H = 256
+    net = network.VideoTransformNet(torch.rand([3, H, H])).to(dev)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.itn_synthetic(4322, in_channels=6)})
+    frames = torch.from_numpy(W.synthetic_image(5000 + rank, (8, 3, H, H))).to(dev)
+    eng = video.FrameEngine(net, (1, 3, H, H), dev, graph=not args.no_graph)
+    i = [0]
+
+    def step():
+        eng.step(frames[i[0] % 8:i[0] % 8 + 1])
+        i[0] += 1
+    for _ in range(3):
+        step()
+    n = max(10, args.steps)
+    dt = timed(step, n, world, dev)
+    return dict(rate=world * n / dt, dt=dt, steps=n, size=H, tl=eng.temporal_loss())
+
+
+def convert_leg(args, world, rank, dev):
+    """BASELINE config 3: fast_st convert-image, batch 32 at 256^2 (ITN forward)."""
+    from styletransfer_amd import network
+    B, H = 32, 256
+    itn = network.ImageTransformNet(torch.rand([3, H, H]), batch_size=B).to(dev)
+    itn.load_state_dict({k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)})
+    x = torch.from_numpy(W.synthetic_image(6000 + rank, (B, 3, H, H))).to(dev)
+    with torch.no_grad():
+        for _ in range(2):
+            itn(x)
+        n = max(3, args.steps // 5)
+        dt = timed(lambda: itn(x), n, world, dev)
+    return dict(rate=world * B * n / dt, dt=dt, steps=n, batch=B)
+
+
 def cpu_baseline(args):
     """The oracle (torch-CPU restatement of the reference schedule) on host cores."""
     from oracle import reference_cpu as O
@@ -231,6 +269,10 @@ def main():
         return
     g = gatys_leg(args, world, rank, dev)
     fs = None if args.skip_fast else fast_st_leg(args, world, rank, dev)
+    vid = conv = None
+    if not args.skip_infer:
+        vid = video_leg(args, world, rank, dev)
+        conv = convert_leg(args, world, rank, dev)
     cpu = None
     if rank == 0 and world == 1 and not args.skip_cpu:
         cpu = cpu_baseline(args)
@@ -301,6 +343,20 @@ def main():
                               if world > 1 else None,
                 "tflops_per_gpu": round(FAST_ST_GFLOP_PER_IMAGE * fs["rate"] / world / 1e3, 3),
             }
+        if vid:
+            res["video_st"] = {
+                "value": round(vid["rate"], 2), "unit": "frames/s", "frame": vid["size"],
+                "ms_per_frame": round(1e3 * vid["dt"] / vid["steps"], 4),
+                "steps": vid["steps"], "graph": not args.no_graph, "parallelism":
+                f"replicas{world}", "note": "BASELINE config 5: per-frame 6-channel "
+                "ImageTransformNet step + temporal-loss norms, one hipGraph replay; frames "
+                "resident in HBM (decode and resize to IMSIZE excluded)"}
+        if conv:
+            res["fast_st_convert"] = {
+                "value": round(conv["rate"], 2), "unit": "images/s", "batch": conv["batch"],
+                "ms_per_batch": round(1e3 * conv["dt"] / conv["steps"], 3),
+                "steps": conv["steps"], "note": "BASELINE config 3: ImageTransformNet "
+                "forward, batch 32 at 256x256, eager"}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

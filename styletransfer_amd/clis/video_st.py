@@ -37,6 +37,12 @@ def train(style_image_path, epochs, batch_size, content_weight, style_weight, te
 @click.option("-o", "--out-dir", default="results/")
 @click.option("--fps", default=24.0)
 def convert_video(video_path, style_name, out_dir, fps):
-    """Convert a video with a pretrained video network."""
-    _need_imageio()
-    raise click.ClickException("video_st convert-video is not implemented yet (SURVEY.md §8f)")
+    """Convert a video with a pretrained video network (stransfer/clis/video_st.py).
+    VIDEO_PATH: a video file (needs imageio), a directory of frames or a .npy array."""
+    import torch
+
+    from .. import network
+    sty = network.VideoTransformNet(torch.rand([3, 255, 255]))  # as the reference CLI
+    out = sty.process_video(video_path=video_path, style_name=style_name, out_dir=out_dir,
+                            fps=fps)
+    click.echo(f"stylised video: {out}")

@@ -602,6 +602,8 @@ __global__ void weight_prep16_kernel(const float* __restrict__ w, _Float16* __re
 }
 
 // -------------------------------------------------------------------- amax
+__global__ void amax_zero_kernel(float* __restrict__ out) { out[threadIdx.x] = 0.f; }
+
 __global__ void amax_kernel(const float* __restrict__ x, long long n, float* __restrict__ out) {
   float m = 0.f;
   const long long n4 = n >> 2;
@@ -652,12 +654,10 @@ extern "C" int stx_amax(const float* x, long long n, float* out, void* stream) {
     set_error("stx_amax: x must be 16-byte aligned");
     return STX_E_INVALID;
   }
-  hipError_t e = hipMemsetAsync(out, 0, STX_AMAX_SLOTS * sizeof(float), st);
-  if (e != hipSuccess) {
-    set_error("stx_amax: %s", hipGetErrorString(e));
-    return (int)e;
-  }
-  if (n == 0) return STX_OK;
+  // the slots are cleared by a kernel, not hipMemsetAsync: a memset node captured into a
+  // hipGraph was observed to run out of order with the amax kernel on replay
+  hipLaunchKernelGGL(amax_zero_kernel, dim3(1), dim3(STX_AMAX_SLOTS), 0, st, out);
+  if (n == 0) return check_launch("stx_amax");
   const int blocks = (int)std::min<long long>(std::max<long long>(1, (n / 4 + 255) / 256), 512);
   hipLaunchKernelGGL(amax_kernel, dim3(blocks), dim3(256), 0, st, x, n, out);
   return check_launch("stx_amax");

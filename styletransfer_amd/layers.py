@@ -47,8 +47,8 @@ class Conv2d(nn.Conv2d):
 
     def forward(self, x, in_mode=N.STX_IN_RAW):
         wt = wt16 = None
-        if not self.weight.requires_grad:
-            wt, wt16 = self.prepped()
+        if not self.weight.requires_grad or not torch.is_grad_enabled():
+            wt, wt16 = self.prepped()  # frozen or inference: slabs cached per weight version
         return A.conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], in_mode, wt,
                         wt16)
 

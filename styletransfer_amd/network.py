@@ -511,8 +511,8 @@ class ImageTransformNet(nn.Sequential):
 
 class VideoTransformNet(ImageTransformNet):
     """stransfer/network.py:835-903: 6-channel first conv ([frame, previous
-    stylised frame]); temporal loss.  video_train / process_video need imageio
-    (absent from this image) and are a "next" row."""
+    stylised frame]); temporal loss; process_video on the graph-captured per-frame
+    engine (video.py).  video_train (COCO-like video dataset) stays a next row."""
 
     def __init__(self, style_image: torch.Tensor, batch_size=4, fast_transfer_dict=None):
         super().__init__(style_image, batch_size)
@@ -530,6 +530,16 @@ class VideoTransformNet(ImageTransformNet):
             self.has_external_weights = True
         else:
             self.has_external_weights = False
+
+    def process_video(self, video_path: str, style_name="nsp", working_dir="workdir/",
+                      out_dir="results/", fps=24.0):
+        """stransfer/network.py:1071-1158 on the graph-captured per-frame engine
+        (styletransfer_amd/video.py); frames come from imageio when installed, or from
+        a directory of frames / a .npy frame array."""
+        from . import video
+        self.load_state_dict(_load_latest_model_weigths(model_name="video_st",
+                                                        style_name=style_name))
+        return video.process_video(self, video_path, style_name, working_dir, out_dir, fps)
 
     def get_temporal_loss(self, old_content, old_stylized, current_content, current_stylized,
                           temporal_weight=1) -> torch.Tensor:

@@ -111,6 +111,17 @@ def amax(x: torch.Tensor, out=None):
     return out
 
 
+def vdot(a, b, out, mul=None, add=None, sgn=1.0, op=0):
+    """*out = add + sgn * mul * r, r = dot(a, b) (op 0), sum|a| (1), max|a| (2); a
+    fixed-order reduction (stx_vec_reduce).  out/mul/add: 1-element device tensors."""
+    _req(a, "a")
+    L = lib()
+    wp, wn = WS.get(L.stx_vec_ws(), a.device)
+    check(L.stx_vec_reduce(a.data_ptr(), _p(b), a.numel(), op, out.data_ptr(), _p(mul), _p(add),
+                           float(sgn), wp, wn, _stream()), "stx_vec_reduce")
+    return out
+
+
 def virtual_hw(h, w, in_mode, hv=None, wv=None):
     if in_mode in (N.STX_IN_RAW, N.STX_IN_RELU):
         return h, w

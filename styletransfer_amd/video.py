@@ -1,0 +1,162 @@
+"""video_st per-frame path on libstx (BASELINE.json config 5).
+
+Reference: `VideoTransformNet.process_video` (stransfer/network.py:1071-1158): every
+decoded frame is conditioned like an image (`dataset.iterate_on_video_batches`,
+stransfer/dataset.py:280-310 -> `img_utils.image_loader_transform`: centre crop,
+resize to IMSIZE, ImageNet normalisation), concatenated with the previous stylised
+frame along channels (`torch.cat([frame, old], dim=1)`, the first frame with
+itself) and run through the 6-channel ImageTransformNet; the output becomes the
+next frame's `old`.  `get_temporal_loss` (:885-903) is ||dy|| / (||dx|| + 1).
+
+`FrameEngine` makes one frame one hipGraph replay: the frame is copied into
+channels 0-2 of a static [1, 6, H, W] input whose channels 3-5 hold the previous
+output, the ITN forward runs on the HIP kernels, the output is copied back into
+channels 3-5, and the temporal-loss norms of the step are reduced on the device
+(the reference computes them only in training; here they are the per-frame
+"temporal loss" of BASELINE config 5).
+"""
+from __future__ import annotations
+
+import os
+from typing import Iterator
+
+import numpy as np
+import torch
+
+from . import constants, img_utils, ops
+
+VIDEO_EXTS = (".mp4", ".avi", ".mov", ".mkv", ".gif", ".webm")
+FRAME_EXTS = (".png", ".jpg", ".jpeg", ".bmp")
+
+
+def iterate_frames(source, max_frames=90 * 24, imsize=None) -> Iterator[torch.Tensor]:
+    """Conditioned frames [1, 3, IMSIZE, IMSIZE] of a video (stransfer/dataset.py:280-310).
+
+    `source`: a video file (decoded with imageio when it is installed, as the
+    reference does), a directory of frame images (sorted by the integer in their
+    name, then by name), a `.npy` array [T, H, W, 3] uint8 (loaded with
+    allow_pickle=False), or an in-memory uint8 array of that shape."""
+    from PIL import Image
+    if isinstance(source, np.ndarray):
+        frames = (Image.fromarray(f) for f in source)
+    elif isinstance(source, str) and source.endswith(".npy"):
+        arr = np.load(source, allow_pickle=False, mmap_mode="r")
+        frames = (Image.fromarray(np.ascontiguousarray(f)) for f in arr)
+    elif isinstance(source, str) and os.path.isdir(source):
+        def key(name):
+            stem = os.path.splitext(name)[0]
+            digits = "".join(ch for ch in stem if ch.isdigit())
+            return (int(digits) if digits else -1, name)
+        names = sorted((n for n in os.listdir(source) if n.lower().endswith(FRAME_EXTS)), key=key)
+        frames = (Image.open(os.path.join(source, n)).convert("RGB") for n in names)
+    elif isinstance(source, str) and source.lower().endswith(VIDEO_EXTS):
+        try:
+            import imageio
+        except ImportError as e:
+            raise RuntimeError(f"decoding {source} needs imageio (not installed); pass a "
+                               "directory of frames or a .npy frame array instead") from e
+        reader = imageio.get_reader(source)
+
+        def gen():
+            try:
+                while True:
+                    yield Image.fromarray(reader.get_next_data())
+            except IndexError:
+                return
+        frames = gen()
+    else:
+        raise ValueError(f"unsupported video source {source!r}")
+    for i, im in enumerate(frames):
+        if i >= max_frames:
+            break
+        yield img_utils.image_loader_transform(im, imsize)
+
+
+class FrameEngine:
+    """One stylised frame = one hipGraph replay of the VideoTransformNet forward."""
+
+    def __init__(self, net, shape, device=None, graph=True):
+        self.net = net
+        self.dev = torch.device(device or constants.DEVICE)
+        n, c, h, w = shape
+        assert c == 3 and n == 1, shape  # the reference converts one video (batch 1)
+        self.x6 = torch.zeros((n, 6, h, w), device=self.dev, dtype=torch.float32)
+        self.frame = self.x6[:, :3]
+        self.prev = self.x6[:, 3:]
+        self.prev_frame = torch.zeros((n, 3, h, w), device=self.dev, dtype=torch.float32)
+        self.out = None
+        # device scalars: ||y_t - y_{t-1}||^2, ||x_t - x_{t-1}||^2, temporal loss
+        self.scal = torch.zeros(4, device=self.dev, dtype=torch.float32)
+        self.graph = None
+        self.use_graph = graph
+        self.started = False
+
+    def _forward(self):
+        with torch.no_grad():
+            y = self.net(self.x6)
+        if self.out is None:
+            self.out = torch.empty_like(y)
+            self.dy = torch.empty_like(y)
+            self.dx = torch.empty_like(y)
+        # temporal-loss terms of this step (stransfer/network.py:885-903)
+        ops.diff_scale(y, self.prev, 1.0, out=self.dy)
+        ops.diff_scale(self.frame, self.prev_frame, 1.0, out=self.dx)
+        ops.vdot(self.dy, self.dy, self.scal[0:1])
+        ops.vdot(self.dx, self.dx, self.scal[1:2])
+        self.out.copy_(y)
+        self.prev.copy_(y)                 # next step's "old stylised" channels
+        self.prev_frame.copy_(self.frame)
+
+    def step(self, frame: torch.Tensor) -> torch.Tensor:
+        """Stylise one conditioned frame [n, 3, H, W]; returns the (static) output."""
+        self.frame.copy_(frame)
+        if not self.started:
+            self.prev.copy_(frame)         # first frame: old = the frame itself
+            self.prev_frame.copy_(frame)
+            self.started = True
+        if self.graph is not None:
+            self.graph.replay()
+        elif self.use_graph and self.out is not None:
+            # the first frame ran eagerly (allocations, prepped-weight caches); capture
+            # records without executing, then replay runs this frame
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._forward()
+            self.graph.replay()
+        else:
+            self._forward()
+        return self.out
+
+    def temporal_loss(self, temporal_weight=1.0) -> float:
+        """||y_t - y_{t-1}|| / (||x_t - x_{t-1}|| + 1) * w of the last step."""
+        dy, dx = float(self.scal[0]), float(self.scal[1])
+        return float(np.sqrt(dy) / (np.sqrt(dx) + 1.0) * temporal_weight)
+
+
+def process_video(net, video_path, style_name="nsp", working_dir="workdir/", out_dir="results/",
+                  fps=24.0, graph=True, max_frames=90 * 24) -> str:
+    """VideoTransformNet.process_video (stransfer/network.py:1071-1158) on FrameEngine."""
+    working_dir = os.path.join(constants.PROJECT_ROOT_PATH, working_dir)
+    out_dir = os.path.join(constants.PROJECT_ROOT_PATH, out_dir)
+    import shutil
+    shutil.rmtree(working_dir, ignore_errors=True)
+    os.makedirs(working_dir, exist_ok=True)
+    os.makedirs(out_dir, exist_ok=True)
+    eng = None
+    for i, frame in enumerate(iterate_frames(video_path, max_frames)):
+        if eng is None:
+            eng = FrameEngine(net, tuple(frame.shape), frame.device, graph=graph)
+        y = eng.step(frame)
+        img_utils.imshow(y[0], path=os.path.join(working_dir, f"{i}.png"))
+    final = os.path.join(out_dir, f"video_st_{style_name}.mp4")
+    try:
+        import imageio
+    except ImportError:
+        return working_dir  # frames only: no encoder in this image
+    from PIL import Image
+    writer = imageio.get_writer(final, fps=fps)
+    names = sorted(os.listdir(working_dir), key=lambda x: int(x.split(".")[0]))
+    for nm in names:
+        writer.append_data(np.array(Image.open(os.path.join(working_dir, nm))))
+    writer.close()
+    return final
