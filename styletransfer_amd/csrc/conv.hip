@@ -21,6 +21,7 @@
 // of padding_mode='reflection').
 #include "common.h"
 #include "conv_epi.h"
+#include "gbwd16.h"
 #include "../../include/stx.h"
 
 namespace stx {
@@ -610,6 +611,13 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     if (!p.in_amax || p.mask || p.in_mode != STX_IN_RAW) {
       set_error("stx_conv2d: split 1x1 mode needs in_amax, no mask, raw input");
       return STX_E_INVALID;
+    }
+    if ((p.cin == 64 || p.cin == 128) && p.cout == p.cin && p.cout_pad >= p.cin &&
+        p.ho % 2 == 0 && p.wo % 16 == 0 && !p.bias && !p.accumulate && !p.relu_out &&
+        (!p.up_dp || p.up_z == p.x) && (uint64_t)p.cin * p.ho * p.wo * 4 < (1ull << 31)) {
+      Gb16 g{p.wt, p.wt_batch_stride, p.cout_pad, p.x, p.in_amax, p.acc_scale, p.up_dp,
+             p.aux, p.aux_scale, p.y, p.out_amax, p.ho, p.wo, 0};
+      return gram_bwd16_launch(g, p.n, p.cin, st);
     }
     stx_conv_params q = p;
     q.p2_z = p.x;

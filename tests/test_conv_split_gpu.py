@@ -197,7 +197,8 @@ def test_split_gram(dev, shape):
 
 
 @pytest.mark.parametrize("shape", [(2, 64, 20, 70), (1, 128, 34, 64), (1, 256, 16, 16),
-                                   (1, 64, 9, 13)])
+                                   (1, 64, 9, 13), (1, 64, 128, 256), (3, 128, 32, 96),
+                                   (2, 64, 2, 32)])
 def test_split_gram_bwd(dev, shape):
     """Gram backward dz = s*A.z + unpool(dp)*(z>0) + aux as the split phase alone
     (1x1 mode) vs the fp32 MFMA 1x1 conv."""
@@ -217,6 +218,29 @@ def test_split_gram_bwd(dev, shape):
     A = coef.double().cpu()[:, :c, :c]
     ref = torch.bmm(A.transpose(1, 2), f).reshape(n, c, h, w)
     assert rel(b16, ref) < TOL64
+
+
+@pytest.mark.parametrize("c", [64, 128])
+def test_split_gram_bwd_window_ties(dev, c):
+    """Quantised z: many 2x2 windows with tied maxima and exact zeros -- the pooled
+    gradient must go to the first maximum in row-major order (max_pool2d backward)
+    exactly as the fp32 path routes it (streaming kernel for C = 64/128)."""
+    n, h, w = 2, 16, 64
+    z = (rnd(n, c, h, w, dev=dev, seed=61, scale=4, shift=-2) * 2).round() / 2
+    t = rnd(c, c, dev=dev, seed=62, scale=0.02)
+    _, coef = ops.style_loss(z, t, weight=5.0)
+    dp = rnd(n, c, h // 2, w // 2, dev=dev, seed=63, scale=2, shift=-1)
+    zero = torch.zeros_like(coef)
+    a16 = ops.gram_bwd_fused(zero, z, up_dp=dp, z_amax=ops.amax(z))
+    a32 = ops.gram_bwd_fused(zero, z, up_dp=dp)
+    assert torch.equal(a16, a32)
+    # reference: autograd of max_pool2d(relu(z))
+    zz = z.detach().cpu().double().requires_grad_(True)
+    F.max_pool2d(F.relu(zz), 2, 2).backward(dp.cpu().double())
+    assert torch.equal(a16.cpu().double(), zz.grad)
+    b16 = ops.gram_bwd_fused(coef, z, up_dp=dp, z_amax=ops.amax(z))
+    b32 = ops.gram_bwd_fused(coef, z, up_dp=dp)
+    assert rel(b16, b32) < 2e-6
 
 
 @pytest.mark.parametrize("case", [(8, 128, 128, 16, 32, N.STX_IN_RAW),

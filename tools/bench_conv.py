@@ -87,11 +87,13 @@ def main():
         _, coef = ops.style_loss(z, t)
         dz = torch.empty_like(z)
         ms2 = ev(lambda: ops.gram_bwd(coef, z, dz, accumulate=True))
-        if n == 1 and c == 64:  # the Gatys dz2 launch: split 1x1 mode + unpool epilogue
+        if n == 1 and c in (64, 128):  # the Gatys dz2/dz4 launches: split 1x1 + unpool
             dp = torch.randn(n, c, h // 2, h // 2, generator=g).to(dev)
             zam = ops.amax(z)
             ms3 = ev(lambda: ops.gram_bwd_fused(coef, z, out=dz, up_dp=dp, z_amax=zam))
-            print(f"{'gram bwd 1x1 split+unpool C64':32s} {ms3 * 1e3:9.1f} us", flush=True)
+            mb = (2.25 * c * h * h * 4) / 1e6
+            print(f"{'gram bwd split+unpool C%d' % c:32s} {ms3 * 1e3:9.1f} us "
+                  f"{mb / (ms3 * 1e3):6.2f} TB/s ({mb:.0f} MB)", flush=True)
         gf = 2.0 * n * c * c * h * h / 1e9
         print(f"{name:32s} fwd {ms * 1e3:8.1f} us {gf / ms:7.2f} TF | bwd {ms2 * 1e3:8.1f} us "
               f"{gf / ms2:7.2f} TF")

@@ -16,7 +16,7 @@ timeout -k 10 300 python bench.py --steps 50 --warmup 3 > gpurun_out/bench.json 
 cat gpurun_out/bench.json
 step rocprof-stats
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-  -- python3 bench.py --steps 50 --warmup 3 --skip-cpu --skip-fast > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
+  -- python3 bench.py --steps 50 --warmup 3 --skip-cpu --skip-fast --skip-infer > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
 step pmc-fetch
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \
   -- python3 tools/bench_conv.py --only "conv1_2" > gpurun_out/pmc_fetch.log 2>&1 || { tail -20 gpurun_out/pmc_fetch.log; exit 1; }
