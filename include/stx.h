@@ -48,7 +48,8 @@ extern "C" {
 
 typedef struct stx_conv_params {
   const float* x;     /* physical input [n][cin][h][w] */
-  const float* wt;    /* prepped weights [cin_pad*ks*ks][cout_pad] (stx_conv_weight_prep) */
+  const float* wt;    /* prepped weights [cin_pad*ks*ks][cout_pad] (stx_conv_weight_prep);
+                         may be NULL when wt16 selects the split path */
   const float* bias;  /* [cout] or NULL */
   float* y;           /* output [n][cout][ho][wo] */
   const float* mask;  /* NULL or [n][cout][ho][wo]: value *= (mask > 0)   (ReLU backward) */
@@ -150,6 +151,17 @@ int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, int accumulat
                        int cin, int h, int w, int cout, int in_mode, int hv, int wv,
                        const float* x_amax, const float* dy_amax, void* ws, size_t ws_bytes,
                        void* stream);
+
+/* dW of the ImageTransformNet 9x9 stride-1 pad-4 layers whose one side has 1..3
+ * channels and the other 32 (conv0 3->32, conv22 32->3; stransfer/network.py:525-527,
+ * 605-609, trained by static_train :690-765) on the fp16 hi/lo split MFMA: the
+ * 3-channel tensor is expanded per tap row in LDS, the 32-channel one streamed.
+ * x_amax / dy_amax: amax groups (>= max|x|, max|dy|).  ws: per-block partials
+ * (stx_conv2d_wgrad_few16_ws, 0 = unsupported shape), summed in a fixed order. */
+size_t stx_conv2d_wgrad_few16_ws(int n, int cin, int cout, int ks, int h, int w);
+int stx_conv2d_wgrad_few16(const float* x, const float* dy, float* dw, int accumulate, int n,
+                           int cin, int h, int w, int cout, int ks, int pad, const float* x_amax,
+                           const float* dy_amax, void* ws, size_t ws_bytes, void* stream);
 /* db[c] (+)= sum_{n,p} dy[n][c][p]  (conv bias gradient) */
 size_t stx_bias_grad_ws(int n, int c);
 int stx_bias_grad(const float* dy, float* db, int n, int c, int hw, int accumulate,

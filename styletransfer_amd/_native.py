@@ -56,6 +56,9 @@ SIGNATURES = {
     "stx_conv2d_wgrad16_ws": (sz, [i32, i32, i32, i32, i32, i32]),
     "stx_conv2d_wgrad16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                  vp, sz, vp]),
+    "stx_conv2d_wgrad_few16_ws": (sz, [i32, i32, i32, i32, i32, i32]),
+    "stx_conv2d_wgrad_few16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                                     vp, sz, vp]),
     "stx_vec_ws": (sz, []),
     "stx_vec_reduce": (i32, [vp, vp, i64, i32, vp, vp, vp, f32, vp, sz, vp]),
     "stx_vec_axpby": (i32, [vp, vp, i64, f32, vp, f32, f32, vp]),

@@ -19,6 +19,19 @@ def _split_on():
     return os.environ.get("STX_CONV_SPLIT", "1") != "0"
 
 
+def _grad_into(param, g, accumulate_fn):
+    """Parameter gradients straight into an existing `param.grad` (e.g. the flat
+    gradient buffer of train.FastStTrainer): `accumulate_fn(dst)` adds the gradient
+    into dst and the Function returns None for it, which is exactly autograd's
+    `param.grad += g` without the extra add launch.  Without a .grad (or for a
+    non-leaf) the gradient is returned as usual."""
+    if param is not None and param.is_leaf and param.grad is not None and \
+            param.grad.is_contiguous() and param.grad.dtype == torch.float32:
+        accumulate_fn(param.grad)
+        return None
+    return g() if callable(g) else g
+
+
 # ----------------------------------------------------------------------- conv
 class Conv2dFn(torch.autograd.Function):
     """y = conv2d(V(x), w) + b with V = identity / relu / nearest-upsample-x2.
@@ -28,15 +41,22 @@ class Conv2dFn(torch.autograd.Function):
     def forward(ctx, x, w, b, stride, pad, in_mode, wt=None, wt16=None):
         x = _c(x)
         cout, cin, ks, _ = w.shape
-        if wt is None:
-            wt = ops.conv_weight_prep(w.detach().contiguous())
         # 3x3 stride-1 layers with cin >= 16 run on the fp16 hi/lo split MFMA kernel
+        # (no fp32 slab needed); max|x| is computed once and kept for the wgrad
         split = _split_on() and pad == 1 and ops.split_eligible(cin, cout, ks, stride)
-        if split and wt16 is None:
-            wt16 = ops.conv_weight_prep16(w.detach().contiguous())
+        x_amax = None
+        if split:
+            if wt16 is None:
+                wt16 = ops.conv_weight_prep16(w.detach().contiguous())
+            x_amax = ops.amax(x)
+        elif wt is None:
+            wt = ops.conv_weight_prep(w.detach().contiguous())
         y = ops.conv2d(x, wt, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
-                       bias=None if b is None else b.detach(), wt16=wt16 if split else None)
+                       bias=None if b is None else b.detach(), wt16=wt16 if split else None,
+                       in_amax=x_amax)
         ctx.save_for_backward(x, w)
+        ctx.x_amax = x_amax
+        ctx.b_ref = b
         ctx.cfg = (stride, pad, in_mode, b is not None)
         return y
 
@@ -47,16 +67,25 @@ class Conv2dFn(torch.autograd.Function):
         dy = _c(dy)
         cout, cin, ks, _ = w.shape
         dx = dw = db = None
+        # max|dy| once for the split dgrad and the split wgrad
+        dy_amax = None
+        split_d = stride == 1 and _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1)
+        if (split_d and ctx.needs_input_grad[0]) or (ctx.needs_input_grad[1] and _split_on() and (
+                (ks == 3 and stride == 1 and pad == 1) or ks == 9)):
+            dy_amax = ops.amax(dy)
         if ctx.needs_input_grad[0]:
-            wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
             h, wd = x.shape[2], x.shape[3]
             hv, wv = ops.virtual_hw(h, wd, in_mode)
             if stride == 1:
-                wtT16 = None
-                if _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1):
+                wtT = wtT16 = None
+                if split_d:
                     wtT16 = ops.conv_weight_prep16(w.detach().contiguous(), transpose=True)
-                dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16)
+                else:
+                    wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
+                dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16,
+                                in_amax=dy_amax)
             elif stride == 2:
+                wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
                 dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad,
                                 in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv)
             else:
@@ -70,9 +99,17 @@ class Conv2dFn(torch.autograd.Function):
             else:
                 raise NotImplementedError("in_mode backward")
         if ctx.needs_input_grad[1]:
-            dw = ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode)
+            dw = _grad_into(w, lambda: ops.conv2d_wgrad(
+                x, dy, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
+                x_amax=ctx.x_amax, dy_amax=dy_amax),
+                lambda dst: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=stride, pad=pad,
+                                             in_mode=in_mode, dw=dst.view(w.shape),
+                                             accumulate=True, x_amax=ctx.x_amax,
+                                             dy_amax=dy_amax))
         if has_b and ctx.needs_input_grad[2]:
-            db = ops.bias_grad(dy)
+            b = ctx.b_ref
+            db = _grad_into(b, lambda: ops.bias_grad(dy),
+                            lambda dst: ops.bias_grad(dy, db=dst, accumulate=True))
         return dx, dw, db, None, None, None, None, None
 
 
@@ -132,6 +169,7 @@ class InstanceNormFn(torch.autograd.Function):
                                          None if beta is None else beta.detach(), res=res,
                                          eps=eps, relu=relu)
         ctx.save_for_backward(x, res, gamma, y, mean, rstd)
+        ctx.beta_ref = beta
         ctx.relu = relu
         ctx.has_res = res is not None
         return y
@@ -140,10 +178,22 @@ class InstanceNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, res, gamma, y, mean, rstd = ctx.saved_tensors
         c = x.shape[1]
-        dg = torch.empty(c, device=x.device) if gamma is not None else None
-        db = torch.empty(c, device=x.device) if gamma is not None else None
+        beta = ctx.beta_ref
+        dg = db = None
+        acc = False
+        if gamma is not None:
+            # straight into existing .grad buffers (FastStTrainer's flat gradient)
+            direct = all(p is not None and p.is_leaf and p.grad is not None and
+                         p.grad.is_contiguous() for p in (gamma, beta))
+            if direct:
+                dg, db, acc = gamma.grad, beta.grad, True
+            else:
+                dg = torch.empty(c, device=x.device)
+                db = torch.empty(c, device=x.device)
         du = ops.instnorm_bwd(_c(dy), y, x, res, None if gamma is None else gamma.detach(),
-                              mean, rstd, relu=ctx.relu, dgamma=dg, dbeta=db)
+                              mean, rstd, relu=ctx.relu, dgamma=dg, dbeta=db, accumulate=acc)
+        if acc:
+            dg = db = None
         return du, (du if ctx.has_res else None), dg, db, None, None
 
 

@@ -278,9 +278,9 @@ conv_fwd_kernel(stx_conv_params p, int tiles_x) {
 // ds_read_b128) and the chunk's weights are prefetched into registers during the
 // previous chunk's FMAs and staged in LDS; every FMA takes one LDS value re-used KS
 // times across kw and COUT times across output channels; weights are LDS broadcasts.
-constexpr int SC_TW = 64, SC_PX = 4, SC_G = 2;
+constexpr int SC_TW = 64, SC_PX = 4;
 
-template <int KS, int CIS, int TH>
+template <int KS, int CIS, int TH, int SC_G>
 struct SmallCfg {
   static constexpr int NT = 16 * TH;                   // threads per channel group
   static constexpr int RH = TH + KS - 1;
@@ -294,10 +294,12 @@ struct SmallCfg {
   static constexpr int NWU = (WU + NT - 1) / NT;
 };
 
-template <int KS, int CIS, int TH>
+// SC_G channel groups per block split the input channels (chunk c0 = (SC_G*k + g)*CIS)
+// and combine their partial sums in a fixed order at the end
+template <int KS, int CIS, int TH, int SC_G>
 __global__ void __launch_bounds__(SC_G * 16 * TH)
 conv_smallc_kernel(stx_conv_params p, int tiles_x) {
-  using C = SmallCfg<KS, CIS, TH>;
+  using C = SmallCfg<KS, CIS, TH, SC_G>;
   constexpr int COUT = 4;
   __shared__ __attribute__((aligned(16))) float halo[SC_G][CIS * C::CH];
   __shared__ __attribute__((aligned(16))) f32x4 wts[SC_G][C::WU];  // [ci][tap] -> 4 couts
@@ -411,22 +413,27 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
       }
     }
   }
-  // fixed-order combine: group 1's partial sums through LDS, added by group 0
+  // fixed-order combine: groups 1..SC_G-1 pass partial sums through LDS, group 0
+  // adds them in group order
   __syncthreads();
   float* red = &halo[0][0];
-  static_assert(C::NT * COUT * SC_PX <= CIS * C::CH, "reduction buffer fits");
-  if (g == 1) {
+  static_assert(C::NT * COUT * SC_PX * (SC_G - 1) <= SC_G * CIS * C::CH, "reduction buffer fits");
+  if (g > 0) {
 #pragma unroll
     for (int c = 0; c < COUT; ++c)
 #pragma unroll
-      for (int q = 0; q < SC_PX; ++q) red[(c * SC_PX + q) * C::NT + tid] = acc[c][q];
+      for (int q = 0; q < SC_PX; ++q)
+        red[((g - 1) * COUT * SC_PX + c * SC_PX + q) * C::NT + tid] = acc[c][q];
   }
   __syncthreads();
-  if (g == 1) return;
+  if (g > 0) return;
 #pragma unroll
-  for (int c = 0; c < COUT; ++c)
+  for (int gg = 1; gg < SC_G; ++gg)
 #pragma unroll
-    for (int q = 0; q < SC_PX; ++q) acc[c][q] += red[(c * SC_PX + q) * C::NT + tid];
+    for (int c = 0; c < COUT; ++c)
+#pragma unroll
+      for (int q = 0; q < SC_PX; ++q)
+        acc[c][q] += red[((gg - 1) * COUT * SC_PX + c * SC_PX + q) * C::NT + tid];
   const int oy = oy0 + ty;
   if (oy >= p.ho) return;
   const size_t plane = (size_t)p.ho * p.wo;
@@ -455,7 +462,36 @@ static int launch_smallc(const stx_conv_params& p, hipStream_t st) {
   const int tiles_x = cdiv(p.wo, SC_TW), tiles_y = cdiv(p.ho, TH);
   dim3 grid(tiles_x * tiles_y, 1, p.n);
   constexpr int CIS = KS == 9 ? 4 : 8;
-  hipLaunchKernelGGL((conv_smallc_kernel<KS, CIS, TH>), grid, dim3(SC_G * 16 * TH), 0, st, p,
+  if constexpr (KS == 3) {
+    static const int cfg = [] {
+      const char* e = getenv("STX_SMALLC");
+      return e ? atoi(e) : 0;
+    }();
+    if (cfg == 1) {
+      const int ty = cdiv(p.ho, 4);
+      hipLaunchKernelGGL((conv_smallc_kernel<KS, 4, 4, 4>), dim3(tiles_x * ty, 1, p.n),
+                         dim3(4 * 16 * 4), 0, st, p, tiles_x);
+      return check_launch("stx_conv2d(smallc)");
+    }
+    if (cfg == 2) {
+      hipLaunchKernelGGL((conv_smallc_kernel<KS, 4, TH, 4>), grid, dim3(4 * 16 * TH), 0, st, p,
+                         tiles_x);
+      return check_launch("stx_conv2d(smallc)");
+    }
+    if (cfg == 3) {
+      const int ty = cdiv(p.ho, 4);
+      hipLaunchKernelGGL((conv_smallc_kernel<KS, 8, 4, 2>), dim3(tiles_x * ty, 1, p.n),
+                         dim3(2 * 16 * 4), 0, st, p, tiles_x);
+      return check_launch("stx_conv2d(smallc)");
+    }
+    if (cfg == 4) {
+      const int ty = cdiv(p.ho, 4);
+      hipLaunchKernelGGL((conv_smallc_kernel<KS, 8, 4, 4>), dim3(tiles_x * ty, 1, p.n),
+                         dim3(4 * 16 * 4), 0, st, p, tiles_x);
+      return check_launch("stx_conv2d(smallc)");
+    }
+  }
+  hipLaunchKernelGGL((conv_smallc_kernel<KS, CIS, TH, 2>), grid, dim3(2 * 16 * TH), 0, st, p,
                      tiles_x);
   return check_launch("stx_conv2d(smallc)");
 }
@@ -554,7 +590,8 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   int cinp, coutp;
   if (stx_conv_weight_dims(p.cin, p.cout, p.ks, &cinp, &coutp)) return STX_E_INVALID;
   if (p.cin_pad != cinp || p.cout_pad != coutp || p.n <= 0 || p.ho <= 0 || p.wo <= 0 ||
-      p.pad < 0 || p.in_mode < 0 || p.in_mode > 4 || !p.x || !p.wt || !p.y) {
+      p.pad < 0 || p.in_mode < 0 || p.in_mode > 4 || !p.x || !p.y ||
+      (!p.wt && (!p.wt16 || p.wt16 == (const void*)1))) {
     set_error("stx_conv2d: invalid params (cin_pad %d/%d cout_pad %d/%d n %d ho %d wo %d)",
               p.cin_pad, cinp, p.cout_pad, coutp, p.n, p.ho, p.wo);
     return STX_E_INVALID;
@@ -638,6 +675,10 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   }
   if (p.pool_out) {
     set_error("stx_conv2d: pool_out is only fused on the split (wt16) path");
+    return STX_E_INVALID;
+  }
+  if (!p.wt) {  // only the split path may run without the fp32 slab
+    set_error("stx_conv2d: this shape runs on the fp32 kernels and needs wt");
     return STX_E_INVALID;
   }
   if (p.cout <= 4 && p.stride == 1 && (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) &&

@@ -161,7 +161,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         _req(out, "out")
         assert out.shape == (n, cout, ho, wo), (out.shape, (n, cout, ho, wo))
     cp, op = conv_weight_dims(cin, cout, ks)
-    p = ConvParams(x=x.data_ptr(), wt=wt.data_ptr(), bias=_p(bias), y=out.data_ptr(),
+    p = ConvParams(x=x.data_ptr(), wt=_p(wt), bias=_p(bias), y=out.data_ptr(),
                    mask=_p(mask), aux=_p(aux), aux_scale=float(aux_scale),
                    acc_scale=_p(acc_scale), accumulate=int(accumulate), relu_out=int(relu_out),
                    n=n, cin=cin, h=h, w=w, cout=cout, ks=ks, stride=stride, pad=pad,
@@ -196,7 +196,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
 
 
 def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, dw=None,
-                 accumulate=False, split=True):
+                 accumulate=False, split=True, x_amax=None, dy_amax=None):
     """dW (+)= sum dy * V(x); 3x3 stride-1 shapes run on the fp16 hi/lo split MFMA
     (stx_conv2d_wgrad16) unless split=False or STX_CONV_SPLIT=0."""
     _req(x, "x")
@@ -210,12 +210,25 @@ def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW,
         dw = torch.empty((cout, cin, ks, ks), device=x.device, dtype=torch.float32)
     L = lib()
     import os
-    if (split and ks == 3 and stride == 1 and pad == 1 and
-            os.environ.get("STX_CONV_SPLIT", "1") != "0"):
+    split = split and os.environ.get("STX_CONV_SPLIT", "1") != "0"
+    if split and ks == 9 and stride == 1 and pad == 4 and in_mode == N.STX_IN_RAW:
+        # ITN conv0 / conv22: the 3-channel side expanded per tap row (wgrad9.hip)
+        need9 = L.stx_conv2d_wgrad_few16_ws(n, cin, cout, ks, h, w)
+        if need9 and ho == h and wo == w:
+            xa = x_amax if x_amax is not None else amax(x)
+            da = dy_amax if dy_amax is not None else amax(dy)
+            wp, wn = WS.get(need9, x.device)
+            check(L.stx_conv2d_wgrad_few16(x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
+                                           int(accumulate), n, cin, h, w, cout, ks, pad,
+                                           xa.data_ptr(), da.data_ptr(), wp, wn, _stream()),
+                  "stx_conv2d_wgrad_few16")
+            return dw
+    if split and ks == 3 and stride == 1 and pad == 1:
         need16 = L.stx_conv2d_wgrad16_ws(n, cin, cout, in_mode, ho, wo)
         if need16:
             _req(dy, "dy")
-            xa, da = amax(x), amax(dy)
+            xa = x_amax if x_amax is not None else amax(x)
+            da = dy_amax if dy_amax is not None else amax(dy)
             wp, wn = WS.get(need16, x.device)
             check(L.stx_conv2d_wgrad16(x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
                                        int(accumulate), n, cin, h, w, cout, in_mode, ho, wo,

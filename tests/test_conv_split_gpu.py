@@ -262,3 +262,22 @@ def test_split_wgrad(dev, case):
     acc = dw16.clone()
     ops.conv2d_wgrad(x, dy, cin, cout, 3, in_mode=mode, dw=acc, accumulate=True)
     assert rel(acc, 2 * ref) < TOL64
+
+
+@pytest.mark.parametrize("case", [(2, 3, 32, 64, 64), (2, 32, 3, 48, 80), (1, 1, 32, 20, 272),
+                                  (3, 32, 2, 9, 16)])
+def test_split_wgrad_9x9_few(dev, case):
+    """ITN conv0 / conv22 weight gradient (9x9 pad 4, 3 <-> 32 channels, wgrad9.hip)
+    vs fp64 autograd and the fp32 MFMA kernel; accumulate mode."""
+    n, cin, cout, h, w = case
+    x = rnd(n, cin, h, w, dev=dev, seed=71, scale=2, shift=-1)
+    wgt = torch.zeros(cout, cin, 9, 9, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x.double().cpu(), wgt, padding=4)
+    dy = rnd(*y.shape, dev=dev, seed=72, scale=2e-3, shift=-1e-3)
+    (ref,) = torch.autograd.grad(y, wgt, dy.double().cpu())
+    dw16 = ops.conv2d_wgrad(x, dy, cin, cout, 9)
+    dw32 = ops.conv2d_wgrad(x, dy, cin, cout, 9, split=False)
+    assert rel(dw16, ref) < TOL64, (rel(dw16, ref), rel(dw32, ref))
+    acc = dw16.clone()
+    ops.conv2d_wgrad(x, dy, cin, cout, 9, dw=acc, accumulate=True)
+    assert rel(acc, 2 * ref) < TOL64

@@ -109,7 +109,7 @@ def main():
         ms = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s, split=False), reps=10)
         gf = 2.0 * n * cin * cout * ks * ks * ho * ho / 1e9
         line = f"{name:32s} fp32 {ms * 1e3:9.1f} us {gf / ms:7.2f} TF"
-        if ks == 3 and s == 1:
+        if s == 1:
             ms16 = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s), reps=10)
             line += f" | f16x3 {ms16 * 1e3:9.1f} us {gf / ms16:7.2f} TF (incl. 2 amax passes)"
         print(line, flush=True)
