@@ -550,6 +550,7 @@ static int dispatch_tw(const stx_conv_params& p, hipStream_t st) {
 }
 
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st);  // conv16.hip
+int conv2d_fewin(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
 
 }  // namespace stx
 
@@ -680,6 +681,14 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   if (!p.wt) {  // only the split path may run without the fp32 slab
     set_error("stx_conv2d: this shape runs on the fp32 kernels and needs wt");
     return STX_E_INVALID;
+  }
+  {  // 3 input channels (VGG conv1_1, ITN conv0, conv22's data gradient)
+    static const bool few_off = [] {
+      const char* e = getenv("STX_FEWIN");
+      return e && atoi(e) == 0;
+    }();
+    const int rc = few_off ? -1 : conv2d_fewin(p, st);
+    if (rc >= 0) return rc;
   }
   if (p.cout <= 4 && p.stride == 1 && (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) &&
       (p.ks == 3 || p.ks == 9) && !p.p2_z && !p.up_dp && !p.out_amax) {

@@ -269,3 +269,23 @@ def test_conv_fused_gram_phase_and_unpool(dev):
     out2 = ops.gram_bwd_fused(coef, z, acc_scale=s2, up_dp=dp, aux=aux, aux_scale=-0.25)
     ref2 = 0.5 * ops.gram_bwd(coef, z) + ops.relupool_bwd(dp, z) - 0.25 * aux
     assert rel(out2, ref2) < TOL
+
+
+@pytest.mark.parametrize("case", [(1, 64, 3, 37, 70), (2, 64, 3, 16, 64), (2, 32, 9, 24, 20),
+                                  (1, 32, 9, 9, 130), (3, 32, 3, 8, 8)])
+def test_conv_fewin(dev, case):
+    """3-input-channel convs (convfew.hip: VGG conv1_1, ITN conv0 / conv22 dgrad) vs
+    fp64, ragged tiles, bias + relu_out + out_amax epilogue; equal to the generic
+    fp32 kernel path (STX_FEWIN=0 is not needed: compare with F.conv2d in fp64)."""
+    n, cout, ks, h, w = case
+    x = rnd(n, 3, h, w, dev=dev, seed=21, scale=2, shift=-1)
+    wgt = rnd(cout, 3, ks, ks, dev=dev, seed=22, scale=0.2, shift=-0.1)
+    b = rnd(cout, dev=dev, seed=23)
+    wt = ops.conv_weight_prep(wgt)
+    am = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    y = ops.conv2d(x, wt, 3, cout, ks, bias=b, out_amax=am)
+    ref = F.conv2d(x.double(), wgt.double(), b.double(), padding=ks // 2)
+    assert rel(y, ref) < 1e-6
+    assert float(am.max()) == float(y.abs().max())
+    yr = ops.conv2d(x, wt, 3, cout, ks, bias=b, relu_out=True)
+    assert rel(yr, F.relu(ref)) < 1e-6
