@@ -85,9 +85,16 @@ class Conv2dFn(torch.autograd.Function):
                 dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16,
                                 in_amax=dy_amax)
             elif stride == 2:
-                wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
-                dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad,
-                                in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv)
+                # stride-1 conv over the zero-dilated dy; the split kernel takes it too
+                if _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1):
+                    wtT16 = ops.conv_weight_prep16(w.detach().contiguous(), transpose=True)
+                    dv = ops.conv2d(dy, None, cout, cin, ks, pad=ks - 1 - pad,
+                                    in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv, wt16=wtT16,
+                                    in_amax=dy_amax if dy_amax is not None else ops.amax(dy))
+                else:
+                    wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
+                    dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad,
+                                    in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv)
             else:
                 raise NotImplementedError("stride > 2")
             if in_mode == N.STX_IN_UPSAMPLE2:

@@ -337,18 +337,22 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
 
   float hv[CIS][C::NE];
   f32x4 wv[C::NWU];
+  // branch-free fetch: out-of-tile / padding elements read 0 through the buffer
+  // descriptor's range check, weights come from a clamped valid address and are
+  // selected after the load (a predicated load is a branch + vmcnt(0) per element)
+  const auto rx = make_srd(xn, (uint32_t)p.cin * (uint32_t)plane_in * 4u);
   auto fetch = [&](int c0) {
     const int cn = min(CIS, p.cin - c0);
 #pragma unroll
     for (int cil = 0; cil < CIS; ++cil) {
-      const float* src = xn + (size_t)(c0 + cil) * plane_in;
+      const uint32_t cofs = (uint32_t)(c0 + cil) * (uint32_t)plane_in;
 #pragma unroll
       for (int e = 0; e < C::NE; ++e) {
-        float v = 0.f;
-        if (cil < cn && ((evalid >> e) & 1)) {
-          v = src[eoff[e]];
-          if (relu_in) v = fmaxf(v, 0.f);
-        }
+        const bool ok = cil < cn && ((evalid >> e) & 1);
+        float v = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rx, ok ? (cofs + eoff[e]) * 4u : BUF_OOB,
+                                                        0, 0));
+        if (relu_in) v = fmaxf(v, 0.f);
         hv[cil][e] = v;
       }
     }
@@ -356,11 +360,11 @@ conv_smallc_kernel(stx_conv_params p, int tiles_x) {
     for (int k = 0; k < C::NWU; ++k) {
       const int i = tid + k * C::NT;
       const int cil = i / KK;
+      const int ic = min(i, C::WU - 1), cc = min(c0 + ic / KK, p.cin - 1);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(wt + (size_t)(cc * KK + (ic - (ic / KK) * KK)) *
+                                                               p.cout_pad);
       const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-      wv[k] = (i < C::WU && cil < cn)
-                  ? *reinterpret_cast<const f32x4*>(wt + (size_t)((c0 + cil) * KK + (i - cil * KK)) *
-                                                             p.cout_pad)
-                  : zero;
+      wv[k] = (i < C::WU && cil < cn) ? v : zero;
     }
   };
   // chunks of this group: c0 = (2k + g) * CIS
@@ -551,6 +555,7 @@ static int dispatch_tw(const stx_conv_params& p, hipStream_t st) {
 
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st);  // conv16.hip
 int conv2d_fewin(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
+int conv2d_fewout(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
 
 }  // namespace stx
 
@@ -687,7 +692,9 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
       const char* e = getenv("STX_FEWIN");
       return e && atoi(e) == 0;
     }();
-    const int rc = few_off ? -1 : conv2d_fewin(p, st);
+    int rc = few_off ? -1 : conv2d_fewin(p, st);
+    if (rc >= 0) return rc;
+    rc = few_off ? -1 : conv2d_fewout(p, st);
     if (rc >= 0) return rc;
   }
   if (p.cout <= 4 && p.stride == 1 && (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) &&

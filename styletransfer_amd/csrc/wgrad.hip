@@ -209,6 +209,8 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, float* __restr
     const int cob = co / bm, row = co % bm, cc = ci / cis, cil = ci % cis;
     const size_t o = ((size_t)cob * ncc + cc) * slab + (size_t)row * bn + cil * kk + r;
     float s = 0.f;
+    // same (split) order; unrolled so the independent loads are in flight together
+#pragma unroll 8
     for (int k = 0; k < nsplit; ++k) s += ws[(size_t)k * split_stride + o];
     dw[i] = accumulate ? dw[i] + s : s;
   }

@@ -289,3 +289,23 @@ def test_conv_fewin(dev, case):
     assert float(am.max()) == float(y.abs().max())
     yr = ops.conv2d(x, wt, 3, cout, ks, bias=b, relu_out=True)
     assert rel(yr, F.relu(ref)) < 1e-6
+
+
+@pytest.mark.parametrize("case", [(1, 3, 37, 70, N.STX_IN_RAW), (2, 3, 16, 64, N.STX_IN_RELU),
+                                  (2, 1, 9, 130, N.STX_IN_RAW), (1, 2, 64, 64, N.STX_IN_RAW)])
+def test_conv_fewout(dev, case):
+    """<= 3-output-channel 3x3 convs (convfew.hip GEMM + col2im: VGG conv1_1's data
+    gradient to the image) vs fp64, ragged tiles, bias/accumulate/relu_out."""
+    n, cout, h, w, mode = case
+    x = rnd(n, 64, h, w, dev=dev, seed=31, scale=2, shift=-1)
+    wgt = rnd(cout, 64, 3, 3, dev=dev, seed=32, scale=0.2, shift=-0.1)
+    b = rnd(cout, dev=dev, seed=33)
+    old = rnd(n, cout, h, w, dev=dev, seed=34)
+    wt = ops.conv_weight_prep(wgt)
+    ref = F.conv2d(vinput(x, mode).double(), wgt.double(), b.double(), padding=1)
+    y = ops.conv2d(x, wt, 64, cout, 3, in_mode=mode, bias=b)
+    assert rel(y, ref) < 1e-6
+    out = old.clone()
+    ops.conv2d(x, wt, 64, cout, 3, in_mode=mode, bias=b, out=out, accumulate=True,
+               relu_out=True)
+    assert rel(out, F.relu(ref + old.double())) < 1e-6
