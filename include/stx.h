@@ -249,17 +249,20 @@ int stx_adam_step(float* p, const float* g, float* m, float* v, long long n, flo
 
 /* InstanceNorm2d(affine) forward, per (n,c) plane over hw (biased var, eps):
  *   u = x (+ res);  y = (u-mean)*rstd*gamma + beta;  y = max(y,0) if relu.
- * mean/rstd [n*c] saved for the backward (may be NULL). */
+ * mean/rstd [n*c] saved for the backward (may be NULL).  out_amax (amax group, zeroed
+ * by the caller, may be NULL) receives max|y| -- the next split conv's input scale. */
 int stx_instnorm_fwd(const float* x, const float* res, const float* gamma, const float* beta,
                      float* y, float* mean, float* rstd, int n, int c, int hw, float eps,
-                     int relu, void* stream);
+                     int relu, float* out_amax, void* stream);
 /* backward: dy = grad wrt y; y needed when relu (mask).  du = grad wrt u (= grad of x
- * and of res).  dgamma/dbeta (may be NULL) (+)= sums over n (fixed order). */
+ * and of res).  dgamma/dbeta (may be NULL) (+)= sums over n (fixed order).  out_amax
+ * (amax group or NULL) receives max|du| -- the split dgrad/wgrad scale of du. */
 size_t stx_instnorm_bwd_ws(int n, int c);
 int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
                      const float* gamma, const float* mean, const float* rstd, float* du,
                      float* dgamma, float* dbeta, int n, int c, int hw, int relu,
-                     int accumulate_params, void* ws, size_t ws_bytes, void* stream);
+                     int accumulate_params, float* out_amax, void* ws, size_t ws_bytes,
+                     void* stream);
 
 /* nearest x2 upsample: y [nc][2h][2w];  backward dx[y][x] = sum of dy's 2x2 block */
 int stx_upsample2x_fwd(const float* x, float* y, int nc, int h, int w, void* stream);

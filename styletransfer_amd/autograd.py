@@ -48,7 +48,9 @@ class Conv2dFn(torch.autograd.Function):
         if split:
             if wt16 is None:
                 wt16 = ops.conv_weight_prep16(w.detach().contiguous())
-            x_amax = ops.amax(x)
+            x_amax = ops.ARENA.lookup(x)  # annotated by the producer (InstanceNorm)
+            if x_amax is None:
+                x_amax = ops.amax(x)
         elif wt is None:
             wt = ops.conv_weight_prep(w.detach().contiguous())
         y = ops.conv2d(x, wt, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
@@ -72,7 +74,9 @@ class Conv2dFn(torch.autograd.Function):
         split_d = stride == 1 and _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1)
         if (split_d and ctx.needs_input_grad[0]) or (ctx.needs_input_grad[1] and _split_on() and (
                 (ks == 3 and stride == 1 and pad == 1) or ks == 9)):
-            dy_amax = ops.amax(dy)
+            dy_amax = ops.ARENA.lookup(dy)
+            if dy_amax is None:
+                dy_amax = ops.amax(dy)
         if ctx.needs_input_grad[0]:
             h, wd = x.shape[2], x.shape[3]
             hv, wv = ops.virtual_hw(h, wd, in_mode)
@@ -172,9 +176,11 @@ class InstanceNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, gamma, beta, eps, relu):
         x, res = _c(x), _c(res)
+        g = ops.ARENA.take(x.device)
         y, mean, rstd = ops.instnorm_fwd(x, None if gamma is None else gamma.detach(),
                                          None if beta is None else beta.detach(), res=res,
-                                         eps=eps, relu=relu)
+                                         eps=eps, relu=relu, out_amax=g)
+        ops.ARENA.annotate(y, g)
         ctx.save_for_backward(x, res, gamma, y, mean, rstd)
         ctx.beta_ref = beta
         ctx.relu = relu
@@ -197,8 +203,11 @@ class InstanceNormFn(torch.autograd.Function):
             else:
                 dg = torch.empty(c, device=x.device)
                 db = torch.empty(c, device=x.device)
+        ga = ops.ARENA.take(x.device)
         du = ops.instnorm_bwd(_c(dy), y, x, res, None if gamma is None else gamma.detach(),
-                              mean, rstd, relu=ctx.relu, dgamma=dg, dbeta=db, accumulate=acc)
+                              mean, rstd, relu=ctx.relu, dgamma=dg, dbeta=db, accumulate=acc,
+                              out_amax=ga)
+        ops.ARENA.annotate(du, ga)
         if acc:
             dg = db = None
         return du, (du if ctx.has_res else None), dg, db, None, None

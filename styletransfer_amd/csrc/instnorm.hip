@@ -11,6 +11,7 @@
 // two-pass CPU kernel), then y = (u-mean)*rstd*gamma + beta (relu).  The plane
 // (<= 256 KB at 256x256) stays L2-resident between the passes.
 #include "common.h"
+#include "conv_epi.h"
 #include "../../include/stx.h"
 
 namespace stx {
@@ -21,7 +22,8 @@ __global__ void __launch_bounds__(NB)
 instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
                     const float* __restrict__ gamma, const float* __restrict__ beta,
                     float* __restrict__ y, float* __restrict__ mean_out,
-                    float* __restrict__ rstd_out, int c, int hw, float eps, int relu) {
+                    float* __restrict__ rstd_out, int c, int hw, float eps, int relu,
+                    float* __restrict__ out_amax) {
   __shared__ float red[NB / 64];
   const size_t base = (size_t)blockIdx.x * hw;
   const int ch = blockIdx.x % c;
@@ -58,6 +60,7 @@ instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
   const float gsc = gamma ? gamma[ch] * rstd : rstd;
   const float sh = (beta ? beta[ch] : 0.f) - mean * gsc;
   float* yp = y + base;
+  uint32_t om = 0u;  // max |y| as IEEE bits (NaN sorts above inf)
   if (vec) {
     for (int i = threadIdx.x * 4; i < hw; i += NB * 4) {
       f32x4 v = *reinterpret_cast<const f32x4*>(xp + i);
@@ -67,15 +70,19 @@ instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
       for (int k = 0; k < 4; ++k) {
         o[k] = v[k] * gsc + sh;
         if (relu) o[k] = fmaxf(o[k], 0.f);
+        om = max(om, __float_as_uint(o[k]) & 0x7fffffffu);
       }
       *reinterpret_cast<f32x4*>(yp + i) = o;
     }
   } else {
     for (int i = threadIdx.x; i < hw; i += NB) {
       float o = (xp[i] + (rp ? rp[i] : 0.f)) * gsc + sh;
-      yp[i] = relu ? fmaxf(o, 0.f) : o;
+      o = relu ? fmaxf(o, 0.f) : o;
+      yp[i] = o;
+      om = max(om, __float_as_uint(o) & 0x7fffffffu);
     }
   }
+  if (out_amax) block_max_to(out_amax, __uint_as_float(om));
   if (threadIdx.x == 0) {
     if (mean_out) mean_out[blockIdx.x] = mean;
     if (rstd_out) rstd_out[blockIdx.x] = rstd;
@@ -90,7 +97,8 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                     const float* __restrict__ x, const float* __restrict__ res,
                     const float* __restrict__ gamma, const float* __restrict__ mean,
                     const float* __restrict__ rstd, float* __restrict__ du,
-                    float* __restrict__ parts, int c, int hw, int relu) {
+                    float* __restrict__ parts, int c, int hw, int relu,
+                    float* __restrict__ out_amax) {
   __shared__ float red[NB / 64];
   const size_t base = (size_t)blockIdx.x * hw;
   const int ch = blockIdx.x % c;
@@ -135,6 +143,7 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
   const float gm = gamma ? gamma[ch] : 1.f;
   const float k = gm * rs / (float)hw;
   float* dup = du + base;
+  uint32_t om = 0u;  // max |du| as IEEE bits
   if (vec) {
     for (int i = threadIdx.x * 4; i < hw; i += NB * 4) {
       const f32x4 d4 = ld4(dyp, i);
@@ -147,6 +156,7 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
         const float g = (relu && !(y4[e] > 0.f)) ? 0.f : d4[e];
         const float xh = (x4[e] + r4[e] - mu) * rs;
         o[e] = k * ((float)hw * g - sg - xh * sgx);
+        om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
       }
       *reinterpret_cast<f32x4*>(dup + i) = o;
     }
@@ -155,13 +165,16 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
       float g = dyp[i];
       if (relu && !(yp[i] > 0.f)) g = 0.f;
       const float xh = (xp[i] + (rp ? rp[i] : 0.f) - mu) * rs;
-      dup[i] = k * ((float)hw * g - sg - xh * sgx);
+      const float o = k * ((float)hw * g - sg - xh * sgx);
+      dup[i] = o;
+      om = max(om, __float_as_uint(o) & 0x7fffffffu);
     }
   }
   if (threadIdx.x == 0) {
     parts[2 * blockIdx.x] = sgx;
     parts[2 * blockIdx.x + 1] = sg;
   }
+  if (out_amax) block_max_to(out_amax, __uint_as_float(om));
 }
 
 __global__ void instnorm_param_grad_kernel(const float* __restrict__ parts, int n, int c,
@@ -184,7 +197,8 @@ using namespace stx;
 
 extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* gamma,
                                 const float* beta, float* y, float* mean, float* rstd, int n,
-                                int c, int hw, float eps, int relu, void* stream) {
+                                int c, int hw, float eps, int relu, float* out_amax,
+                                void* stream) {
   if (n <= 0 || c <= 0 || hw <= 0 || !x || !y) {
     set_error("stx_instnorm_fwd: invalid args");
     return STX_E_INVALID;
@@ -194,7 +208,7 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
     return STX_E_INVALID;
   }
   hipLaunchKernelGGL(instnorm_fwd_kernel, dim3(n * c), dim3(NB), 0, (hipStream_t)stream, x, res,
-                     gamma, beta, y, mean, rstd, c, hw, eps, relu);
+                     gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
   return check_launch("stx_instnorm_fwd");
 }
 
@@ -205,8 +219,8 @@ extern "C" size_t stx_instnorm_bwd_ws(int n, int c) {
 extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
                                 const float* gamma, const float* mean, const float* rstd,
                                 float* du, float* dgamma, float* dbeta, int n, int c, int hw,
-                                int relu, int accumulate_params, void* ws, size_t ws_bytes,
-                                void* stream) {
+                                int relu, int accumulate_params, float* out_amax, void* ws,
+                                size_t ws_bytes, void* stream) {
   if (n <= 0 || c <= 0 || hw <= 0 || !dy || !x || !du || !mean || !rstd || (relu && !y)) {
     set_error("stx_instnorm_bwd: invalid args");
     return STX_E_INVALID;
@@ -217,7 +231,7 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
   }
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(instnorm_bwd_kernel, dim3(n * c), dim3(NB), 0, st, dy, y, x, res, gamma, mean,
-                     rstd, du, (float*)ws, c, hw, relu);
+                     rstd, du, (float*)ws, c, hw, relu, out_amax);
   if (dgamma || dbeta)
     hipLaunchKernelGGL(instnorm_param_grad_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st,
                        (const float*)ws, n, c, dgamma, dbeta, accumulate_params);

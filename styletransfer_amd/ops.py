@@ -62,6 +62,56 @@ class _Workspace:
 WS = _Workspace()
 
 
+class AmaxArena:
+    """Pre-zeroed amax groups for producers that annotate their outputs (InstanceNorm
+    forward/backward -> the next split conv's input scale).  A training step calls
+    begin() (one fill of all groups) and end(); outside a step take() returns None
+    and consumers compute max|x| themselves.  Annotations carry the arena epoch, so a
+    tensor kept across steps is never trusted with a re-zeroed group."""
+
+    def __init__(self, groups=128):
+        self.groups = groups
+        self.buf = None
+        self.i = 0
+        self.epoch = 0
+        self.active = False
+
+    def begin(self, device):
+        dev = torch.device(device)
+        if self.buf is None or self.buf.device != dev:
+            self.buf = torch.zeros((self.groups, N.STX_AMAX_SLOTS), device=dev,
+                                   dtype=torch.float32)
+        else:
+            self.buf.zero_()
+        self.i = 0
+        self.epoch += 1
+        self.active = True
+
+    def end(self):
+        self.active = False
+
+    def take(self, device):
+        if not self.active or self.i >= self.groups or self.buf.device != device:
+            return None
+        g = self.buf[self.i]
+        self.i += 1
+        return g
+
+    def annotate(self, t, g):
+        if g is not None:
+            t._stx_amax = (g, self.epoch)
+        return t
+
+    def lookup(self, t):
+        a = getattr(t, "_stx_amax", None)
+        if a is None or not self.active or a[1] != self.epoch:
+            return None
+        return a[0]
+
+
+ARENA = AmaxArena()
+
+
 # ----------------------------------------------------------------------- conv
 def conv_weight_dims(cin, cout, ks):
     a, b = C.c_int(), C.c_int()
@@ -409,7 +459,7 @@ def adam_step(p, g, m, v, step_dev, ws, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-
 
 
 # ----------------------------------------------------------------------- instance norm
-def instnorm_fwd(x, gamma, beta, res=None, eps=1e-5, relu=False, out=None):
+def instnorm_fwd(x, gamma, beta, res=None, eps=1e-5, relu=False, out=None, out_amax=None):
     _req(x, "x")
     n, c = x.shape[:2]
     hw = x[0, 0].numel()
@@ -419,12 +469,12 @@ def instnorm_fwd(x, gamma, beta, res=None, eps=1e-5, relu=False, out=None):
     rstd = torch.empty_like(mean)
     check(lib().stx_instnorm_fwd(x.data_ptr(), _p(res), _p(gamma), _p(beta), out.data_ptr(),
                                  mean.data_ptr(), rstd.data_ptr(), n, c, hw, float(eps),
-                                 int(relu), _stream()), "stx_instnorm_fwd")
+                                 int(relu), _p(out_amax), _stream()), "stx_instnorm_fwd")
     return out, mean, rstd
 
 
 def instnorm_bwd(dy, y, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbeta=None,
-                 accumulate=False):
+                 accumulate=False, out_amax=None):
     n, c = x.shape[:2]
     hw = x[0, 0].numel()
     du = torch.empty_like(x)
@@ -432,8 +482,8 @@ def instnorm_bwd(dy, y, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbet
     wp, wn = WS.get(L.stx_instnorm_bwd_ws(n, c), x.device)
     check(L.stx_instnorm_bwd(dy.data_ptr(), _p(y), x.data_ptr(), _p(res), _p(gamma),
                              mean.data_ptr(), rstd.data_ptr(), du.data_ptr(), _p(dgamma),
-                             _p(dbeta), n, c, hw, int(relu), int(accumulate), wp, wn, _stream()),
-          "stx_instnorm_bwd")
+                             _p(dbeta), n, c, hw, int(relu), int(accumulate), _p(out_amax), wp,
+                             wn, _stream()), "stx_instnorm_bwd")
     return du
 
 

@@ -21,6 +21,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from . import ops
 from . import autograd as A
 from . import constants
 from . import vgg as V
@@ -84,9 +85,13 @@ class FastStTrainer:
     def step(self, batch: torch.Tensor) -> torch.Tensor:
         batch = batch.to(self.device, torch.float32).contiguous()
         self.flat_grad.zero_()
-        y = self.itn(batch)
-        total = self._total(batch, y)
-        total.backward()
+        ops.ARENA.begin(self.device)  # InstanceNorm outputs carry their max|.| to the convs
+        try:
+            y = self.itn(batch)
+            total = self._total(batch, y)
+            total.backward()
+        finally:
+            ops.ARENA.end()
         if self.world > 1:
             dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
         self.opt.step()

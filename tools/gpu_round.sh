@@ -25,3 +25,7 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out
   -- python3 tools/bench_conv.py --only "conv1_2" > gpurun_out/pmc_write.log 2>&1 || { tail -20 gpurun_out/pmc_write.log; exit 1; }
 step done
 find gpurun_out -name "*.csv" | head -20
+step rocprof-fast_st
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/proff -o run \
+  -- python3 bench.py --fast-only --steps 30 --warmup 2 > gpurun_out/proff.log 2>&1 || { tail -20 gpurun_out/proff.log; exit 1; }
+step done-fast
