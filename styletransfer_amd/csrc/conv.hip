@@ -655,7 +655,8 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
       set_error("stx_conv2d: split 1x1 mode needs in_amax, no mask, raw input");
       return STX_E_INVALID;
     }
-    if ((p.cin == 64 || p.cin == 128) && p.cout == p.cin && p.cout_pad >= p.cin &&
+    if ((p.cin == 64 || p.cin == 128 || (p.cin == 256 && !p.up_dp)) && p.cout == p.cin &&
+        p.cout_pad >= p.cin &&
         p.ho % 2 == 0 && p.wo % 16 == 0 && !p.bias && !p.accumulate && !p.relu_out &&
         (!p.up_dp || p.up_z == p.x) && (uint64_t)p.cin * p.ho * p.wo * 4 < (1ull << 31)) {
       Gb16 g{p.wt, p.wt_batch_stride, p.cout_pad, p.x, p.in_amax, p.acc_scale, p.up_dp,

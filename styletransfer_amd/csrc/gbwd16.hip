@@ -53,17 +53,21 @@ __device__ __forceinline__ float swap_pair(float v) {  // lane l <- lane l^1
 //         column l32%16 (window partners: lanes l^1, l^16, l^17) -- half the
 //         registers, twice the units (the C = 128 occupancy case)
 // NW waves per block share one staged A (C = 128: 8 waves, one 64 KB copy per CU)
-template <int C, int NB, bool AUX, int NW>
+// CQ: output channels per block (C for 64/128; a quarter of C = 256, whose A slice
+// 64 x 256 is 64 KB of LDS).  With CQ < C the lane's loaded channels are not its
+// accumulator rows, so the fused unpool (which relies on that) needs CQ == C.
+template <int C, int NB, bool AUX, int NW, int CQ = C>
 __global__ void __launch_bounds__(64 * NW, (NW == 8 || (C == 128 && NB == 2)) ? 1 : 2)
 gram_bwd16_kernel(Gb16 p) {
   constexpr int NT = 64 * NW;
   constexpr bool PREFETCH = C * NB <= 128;
   constexpr bool A_IN_REGS = C == 64;  // 64 VGPRs of A fragments stay resident
-  constexpr int NK = C / 16, NCB = C / 32, FRAG = 64 * 16;
+  constexpr int NK = C / 16, NCB = CQ / 32, FRAG = 64 * 16;
+  static_assert(C % CQ == 0 && CQ % 32 == 0, "co split");
   __shared__ __attribute__((aligned(16))) char la[NCB * NK * 2 * FRAG];
   __shared__ float red[NW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
-  const int n = blockIdx.y;
+  const int n = blockIdx.y / (C / CQ), co0 = (blockIdx.y % (C / CQ)) * CQ;
   constexpr int UW = 16 * NB;  // unit width (columns)
   const int W = p.w, plane = p.h * p.w, ucols = W / UW, units = (p.h >> 1) * ucols;
   // lane pixel inside the unit: row offset (NB == 1: l32/16) and column
@@ -106,14 +110,14 @@ gram_bwd16_kernel(Gb16 p) {
   // ---- A' hi/lo fragments -> LDS (fragment (cb, k, P): lane ln's 16 B at ln*16) ----
   int ea;
   {
-    constexpr int NA = C * C / NT;
+    constexpr int NA = C * CQ / NT;
     const float* A = p.coef + (size_t)n * p.coef_bs;
     if (p.dbg & 1) A = p.z_amax;  // profiling: one L2 line, no real staging traffic
     float av[NA];  // all loads in flight at once (A is small and L2 resident)
     float m = 0.f;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int idx = tid + NT * i, c = idx / C, co = idx - c * C;
+      const int idx = tid + NT * i, c = idx / CQ, co = co0 + idx - c * CQ;
       av[i] = A[(p.dbg & 1) ? 0 : (size_t)c * p.pitch + co];
     }
 #pragma unroll
@@ -128,7 +132,7 @@ gram_bwd16_kernel(Gb16 p) {
     const float sa = __builtin_ldexpf(1.f, 15 - amax_exp16(m));
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int idx = tid + NT * i, c = idx / C, co = idx - c * C;
+      const int idx = tid + NT * i, c = idx / CQ, co = idx - c * CQ;  // co: block-local
       const int rem = c & 31, q = rem >> 3;
       const int k = 2 * (c >> 5) + (q >> 1), e = (q & 1) * 4 + (rem & 3);
       const int ln = ((rem >> 2) & 1) * 32 + (co & 31);
@@ -171,7 +175,7 @@ gram_bwd16_kernel(Gb16 p) {
     for (int cb = 0; cb < NCB; ++cb) sel[cb] = 0u;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      if (has_dp) {
+      if (CQ == C && has_dp) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int r = ((k & 1) << 3) | ((e >> 2) << 2) | (e & 3);
@@ -241,8 +245,8 @@ gram_bwd16_kernel(Gb16 p) {
     for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const uint32_t so = (uint32_t)(32 * cb + 8 * (r >> 2) + (r & 3)) * (pl4 >> 2);
-        dpv[cb][r] = has_dp ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        const uint32_t so = (uint32_t)(co0 + 32 * cb + 8 * (r >> 2) + (r & 3)) * (pl4 >> 2);
+        dpv[cb][r] = (CQ == C && has_dp) ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                             rdp, vdp, so, 0))
                             : 0.f;
       }
@@ -253,7 +257,7 @@ gram_bwd16_kernel(Gb16 p) {
       for (int j = 0; j < NB; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const uint32_t so = (uint32_t)(32 * cb + 8 * (r >> 2) + (r & 3)) * pl4;
+          const uint32_t so = (uint32_t)(co0 + 32 * cb + 8 * (r >> 2) + (r & 3)) * pl4;
           dst[j][r] = __builtin_bit_cast(
               float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo + j * W * 4, so, 0));
         }
@@ -266,7 +270,7 @@ gram_bwd16_kernel(Gb16 p) {
       for (int j = 0; j < NB; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const uint32_t so = (uint32_t)(32 * cb + 8 * (r >> 2) + (r & 3)) * pl4;
+          const uint32_t so = (uint32_t)(co0 + 32 * cb + 8 * (r >> 2) + (r & 3)) * pl4;
           const uint32_t vj = vo + j * W * 4;
           float v = acc[cb][j][r] * fout;
           if ((sel[cb] >> (j * 16 + r)) & 1u) v += dpv[cb][r];
@@ -294,21 +298,23 @@ gram_bwd16_kernel(Gb16 p) {
   }
 }
 
-template <int C, int NB>
+template <int C, int NB, int CQ = C>
 static void launch_gb(const Gb16& p, int nimg, hipStream_t st) {
   constexpr int NW = (C == 128 && NB == 1) ? 8 : 4;
   constexpr int slots = NW == 8 ? 256 : 512;  // resident blocks (2048 waves)
+  constexpr int NQ = C / CQ;
   const int units = (p.h / 2) * (p.w / (16 * NB));
-  const int per_img = std::max(1, std::min((units + NW - 1) / NW, std::max(1, slots / nimg)));
+  const int per_img =
+      std::max(1, std::min((units + NW - 1) / NW, std::max(1, slots / (nimg * NQ))));
   if (p.aux)
-    hipLaunchKernelGGL((gram_bwd16_kernel<C, NB, true, NW>), dim3(per_img, nimg), dim3(64 * NW), 0,
-                       st, p);
+    hipLaunchKernelGGL((gram_bwd16_kernel<C, NB, true, NW, CQ>), dim3(per_img, nimg * NQ),
+                       dim3(64 * NW), 0, st, p);
   else
-    hipLaunchKernelGGL((gram_bwd16_kernel<C, NB, false, NW>), dim3(per_img, nimg), dim3(64 * NW), 0,
-                       st, p);
+    hipLaunchKernelGGL((gram_bwd16_kernel<C, NB, false, NW, CQ>), dim3(per_img, nimg * NQ),
+                       dim3(64 * NW), 0, st, p);
 }
 
-// C in {64, 128}, h even, w % 16 == 0, dense channels (pitch >= C); the caller
+// C in {64, 128, 256} (256: no up_dp), h even, w % 16 == 0, dense channels; the caller
 // (stx_conv2d's split 1x1 mode) checks the rest of the contract.
 int gram_bwd16_launch(const Gb16& p, int nimg, int c, hipStream_t st) {
   static const int nb_env = [] {
@@ -325,8 +331,10 @@ int gram_bwd16_launch(const Gb16& p, int nimg, int c, hipStream_t st) {
   const bool two = nb == 2 && p.w % 32 == 0;
   if (c == 64)
     two ? launch_gb<64, 2>(q, nimg, st) : launch_gb<64, 1>(q, nimg, st);
-  else
+  else if (c == 128)
     two ? launch_gb<128, 2>(q, nimg, st) : launch_gb<128, 1>(q, nimg, st);
+  else
+    launch_gb<256, 1, 64>(q, nimg, st);  // C = 256 (conv3_1): no fused unpool
   return check_launch("stx_conv2d(gram backward, split 1x1)");
 }
 

@@ -198,7 +198,7 @@ def test_split_gram(dev, shape):
 
 @pytest.mark.parametrize("shape", [(2, 64, 20, 70), (1, 128, 34, 64), (1, 256, 16, 16),
                                    (1, 64, 9, 13), (1, 64, 128, 256), (3, 128, 32, 96),
-                                   (2, 64, 2, 32)])
+                                   (2, 64, 2, 32), (2, 256, 32, 48)])
 def test_split_gram_bwd(dev, shape):
     """Gram backward dz = s*A.z + unpool(dp)*(z>0) + aux as the split phase alone
     (1x1 mode) vs the fp32 MFMA 1x1 conv."""
@@ -213,6 +213,10 @@ def test_split_gram_bwd(dev, shape):
                              z_amax=ops.amax(z))
     a32 = ops.gram_bwd_fused(coef, z, acc_scale=s, up_dp=dp, aux=aux, aux_scale=-0.25)
     assert rel(a16, a32) < 2e-6
+    # without the unpool term (C = 256 takes the co-split streaming kernel)
+    c16 = ops.gram_bwd_fused(coef, z, acc_scale=s, aux=aux, aux_scale=-0.25, z_amax=ops.amax(z))
+    c32 = ops.gram_bwd_fused(coef, z, acc_scale=s, aux=aux, aux_scale=-0.25)
+    assert rel(c16, c32) < 2e-6
     b16 = ops.gram_bwd_fused(coef, z, z_amax=ops.amax(z))
     f = z.double().cpu().reshape(n, c, h * w)
     A = coef.double().cpu()[:, :c, :c]
