@@ -40,6 +40,11 @@ class ConvParams(C.Structure):
     ]
 
 
+class LossParts(C.Structure):
+    """Mirror of `stx_loss_parts` (include/stx.h)."""
+    _fields_ = [("parts", vp * 8), ("nparts", i32 * 8), ("inv", f32 * 8), ("k", i32)]
+
+
 # name -> (restype, argtypes); every symbol include/stx.h declares
 SIGNATURES = {
     "stx_version": (i32, []),
@@ -75,6 +80,8 @@ SIGNATURES = {
     "stx_mse": (i32, [vp, vp, i64, i32, i32, vp, vp, f32, vp, sz, vp]),
     "stx_diff_scale": (i32, [vp, vp, vp, i64, f32, vp, vp, i32, i32, vp]),
     "stx_loss_combine": (i32, [vp, i32, C.POINTER(f32), vp, vp]),
+    "stx_style_loss_parts": (sz, [i32, i32, i32, C.POINTER(i32)]),
+    "stx_loss_finalize": (i32, [C.POINTER(LossParts), vp, vp, i32, C.POINTER(f32), vp, vp]),
     "stx_maxpool2x2_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "stx_maxpool2x2_bwd": (i32, [vp, vp, vp, i32, i32, i32, vp]),
     "stx_relupool_bwd": (i32, [vp, vp, vp, i32, i32, i32, vp]),

@@ -310,11 +310,14 @@ __device__ __forceinline__ void gram_f16_tile(const float* __restrict__ z, float
   const float* zb = z + (size_t)b * c * hw;
   const int ra0 = I * GT + r, ra1 = I * GT + 32 + r;
   const int rb0 = J * GT + r, rb1 = J * GT + 32 + r;
-  const float* pa0 = zb + (size_t)min(ra0, c - 1) * hw + 8 * h;
-  const float* pa1 = zb + (size_t)min(ra1, c - 1) * hw + 8 * h;
-  const float* pb0 = zb + (size_t)min(rb0, c - 1) * hw + 8 * h;
-  const float* pb1 = zb + (size_t)min(rb1, c - 1) * hw + 8 * h;
-  const bool va0 = ra0 < c, va1 = ra1 < c, vb0 = rb0 < c, vb1 = rb1 < c;
+  // branch-free loads: rows past c and pixels past the split read 0 through the
+  // buffer descriptor's range check (a predicated load compiles to an exec branch and
+  // a vmcnt(0) join, which serialised the double-buffered groups)
+  const auto rz = make_srd(zb, (uint32_t)c * (uint32_t)hw * 4u);
+  const uint32_t oa0 = ra0 < c ? (uint32_t)(ra0 * hw + 8 * h) * 4u : BUF_OOB;
+  const uint32_t oa1 = ra1 < c ? (uint32_t)(ra1 * hw + 8 * h) * 4u : BUF_OOB;
+  const uint32_t ob0 = rb0 < c ? (uint32_t)(rb0 * hw + 8 * h) * 4u : BUF_OOB;
+  const uint32_t ob1 = rb1 < c ? (uint32_t)(rb1 * hw + 8 * h) * 4u : BUF_OOB;
   const int e = gram_amax_exp(read_amax(z_amax));
   const float sx = __builtin_ldexpf(1.f, 15 - e);
   const float inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
@@ -331,15 +334,16 @@ __device__ __forceinline__ void gram_f16_tile(const float* __restrict__ z, float
   auto load = [&](int p0, Grp& g) {
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      const int pp = p0 + 16 * st;       // + 8h folded into the row pointers
+      const int pp = p0 + 16 * st;       // + 8h folded into the row offsets
       const bool ok = pp + 8 * h < p_end;  // hw % 8 == 0: a lane's 8 pixels all in or out
+      const uint32_t po = ok ? (uint32_t)pp * 4u : BUF_OOB;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        g.x[0][st][q] = (ok && va0) ? *reinterpret_cast<const f32x4*>(pa0 + pp + 4 * q) : zero;
-        g.x[1][st][q] = (ok && va1) ? *reinterpret_cast<const f32x4*>(pa1 + pp + 4 * q) : zero;
+        g.x[0][st][q] = buf_ld4(rz, (oa0 | (po & BUF_OOB)) + (po & ~BUF_OOB) + 16u * q);
+        g.x[1][st][q] = buf_ld4(rz, (oa1 | (po & BUF_OOB)) + (po & ~BUF_OOB) + 16u * q);
         if (!DIAG) {
-          g.x[2][st][q] = (ok && vb0) ? *reinterpret_cast<const f32x4*>(pb0 + pp + 4 * q) : zero;
-          g.x[3][st][q] = (ok && vb1) ? *reinterpret_cast<const f32x4*>(pb1 + pp + 4 * q) : zero;
+          g.x[2][st][q] = buf_ld4(rz, (ob0 | (po & BUF_OOB)) + (po & ~BUF_OOB) + 16u * q);
+          g.x[3][st][q] = buf_ld4(rz, (ob1 | (po & BUF_OOB)) + (po & ~BUF_OOB) + 16u * q);
         }
       }
     }
@@ -496,6 +500,10 @@ __global__ void zero_kernel(float* p, long long n) {
     p[i] = 0.f;
 }
 
+struct LossWF {
+  float w[16];
+};
+
 static void gram_geometry(int c, int hw, int b, int& nsplit, int& split_len, int& ntu) {
   const int nt = cdiv(c, GT);
   ntu = nt * (nt + 1) / 2;
@@ -531,13 +539,22 @@ static void gram_geometry16(int c, int hw, int b, int& nsplit, int& split_len, i
   nsplit = rup(cdiv(hw, split_len), 8);
 }
 
-static size_t gram_ws_bytes(int b, int c, int hw) {
+// workspace layout: [partial slabs (largest geometry)][loss partials b*ntu*FSUB]; the
+// loss partials sit at a geometry-independent offset so a caller can keep them for a
+// deferred, fused loss reduction (stx_style_loss_parts / stx_loss_finalize)
+static size_t gram_parts_offset(int b, int c, int hw, int* nparts) {
   int nsplit, split_len, ntu, ns16, sl16;
   gram_geometry(c, hw, b, nsplit, split_len, ntu);
   gram_geometry16(c, hw, b, ns16, sl16, ntu);
   nsplit = std::max(nsplit, ns16);
-  // partial slabs + loss parts
-  return ((size_t)b * ntu * nsplit * GT * GT + (size_t)b * ntu * FSUB + 64) * sizeof(float);
+  if (nparts) *nparts = b * ntu * FSUB;
+  return (size_t)b * ntu * nsplit * GT * GT * sizeof(float);
+}
+
+static size_t gram_ws_bytes(int b, int c, int hw) {
+  int nparts;
+  const size_t off = gram_parts_offset(b, c, hw, &nparts);
+  return off + ((size_t)nparts + 64) * sizeof(float);
 }
 
 static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_out,
@@ -560,7 +577,7 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
     return STX_E_WORKSPACE;
   }
   float* slabs = (float*)ws;
-  float* parts = slabs + (size_t)b * ntu * nsplit * GT * GT;
+  float* parts = (float*)((char*)ws + gram_parts_offset(b, c, hw, nullptr));
   if (f16) {
     hipLaunchKernelGGL(gram_partial_f16_kernel, dim3(nsplit * ntu, 1, b), dim3(256), 0, st, z,
                        slabs, c, hw, nsplit, split_len, z_amax);
@@ -589,6 +606,53 @@ using namespace stx;
 
 extern "C" size_t stx_gram_ws(int b, int c, int hw) { return gram_ws_bytes(b, c, hw); }
 
+extern "C" size_t stx_style_loss_parts(int b, int c, int hw, int* nparts) {
+  return gram_parts_offset(b, c, hw, nparts);
+}
+
+namespace stx {
+// one block: losses[i] = inv_i * sum(parts_i) (the per-thread strided order of
+// sum_parts_kernel, so the values are identical), then the weighted total
+__global__ void loss_finalize_kernel(stx_loss_parts lp, float* __restrict__ losses,
+                                     const float* __restrict__ extra, int m, LossWF w,
+                                     float* __restrict__ total) {
+  __shared__ float red[4];
+  float lv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    lv[i] = 0.f;
+    if (i < lp.k) {
+      float s = 0.f;
+      for (int j = threadIdx.x; j < lp.nparts[i]; j += 256) s += lp.parts[i][j];
+      lv[i] = block_sum<256>(s, red) * lp.inv[i];
+    }
+  }
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < lp.k; ++i) {
+      losses[i] = lv[i];
+      t += w.w[i] * lv[i];
+    }
+    for (int j = 0; j < m; ++j) t += w.w[lp.k + j] * extra[j];
+    if (total) *total = t;
+  }
+}
+}  // namespace stx
+
+extern "C" int stx_loss_finalize(const stx_loss_parts* lp, float* losses, const float* extra,
+                                 int m, const float* w_host, float* total, void* stream) {
+  if (!lp || lp->k < 0 || lp->k > 8 || m < 0 || lp->k + m > 16 || !losses ||
+      (m && !extra) || (total && !w_host)) {
+    set_error("stx_loss_finalize: invalid arguments");
+    return STX_E_INVALID;
+  }
+  LossWF w{};
+  for (int i = 0; i < lp->k + m && w_host; ++i) w.w[i] = w_host[i];
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *lp,
+                     losses, extra, m, w, total);
+  return check_launch("stx_loss_finalize");
+}
+
 extern "C" int stx_gram_coef_pitch(int c) { return c <= 64 ? rup(c, 64) : rup(c, 128); }
 
 extern "C" int stx_gram(const float* z, float* g, int b, int c, int hw, float scale,
@@ -601,8 +665,8 @@ extern "C" int stx_gram(const float* z, float* g, int b, int c, int hw, float sc
 extern "C" int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
                               float* loss, int b, int c, int hw, int target_batched, float weight, float diag_alpha,
                               const float* z_amax, void* ws, size_t ws_bytes, void* stream) {
-  if (!target || !loss) {
-    set_error("stx_style_loss: target and loss are required");
+  if (!target) {  // loss == NULL: partials stay in ws (stx_style_loss_parts)
+    set_error("stx_style_loss: target is required");
     return STX_E_INVALID;
   }
   hipStream_t st = (hipStream_t)stream;

@@ -329,8 +329,10 @@ def coef_pitch(c):
 
 
 def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None, loss=None,
-               coef=None, z_amax=None):
-    """mean((gram(z) - target)^2) -> 0-d loss; coef = d(weight*loss)/dz operator."""
+               coef=None, z_amax=None, defer_ws=None):
+    """mean((gram(z) - target)^2) -> 0-d loss; coef = d(weight*loss)/dz operator.
+    defer_ws (uint8 device buffer >= stx_gram_ws): the loss is not reduced here; its
+    partials stay in defer_ws for loss_finalize (returns (LossPart, coef))."""
     _req(z, "z")
     _req(target, "target")
     b, c = z.shape[:2]
@@ -339,17 +341,43 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
     tb = target.numel() == b * c * c and b > 1
     if not tb and target.numel() != c * c:
         raise ValueError(f"style target {tuple(target.shape)} cannot expand to ({b},{c},{c})")
-    if loss is None:
+    if loss is None and defer_ws is None:
         loss = torch.empty((), device=z.device, dtype=torch.float32)
     if want_coef and coef is None:
         cp = coef_pitch(c)
         coef = torch.empty((b, cp, cp), device=z.device, dtype=torch.float32)
     L = lib()
-    wp, wn = WS.get(L.stx_gram_ws(b, c, hw), z.device)
+    need = L.stx_gram_ws(b, c, hw)
+    if defer_ws is not None:
+        assert defer_ws.numel() >= need, (defer_ws.numel(), need)
+        wp, wn = defer_ws.data_ptr(), defer_ws.numel()
+    else:
+        wp, wn = WS.get(need, z.device)
     check(L.stx_style_loss(z.data_ptr(), target.data_ptr(), _p(g_out), _p(coef) if want_coef
-                           else None, loss.data_ptr(), b, c, hw, int(tb), float(weight),
+                           else None, _p(loss), b, c, hw, int(tb), float(weight),
                            float(diag_alpha), _p(z_amax), wp, wn, _stream()), "stx_style_loss")
+    if defer_ws is not None:
+        npart = C.c_int()
+        off = L.stx_style_loss_parts(b, c, hw, C.byref(npart))
+        return (wp + off, npart.value, 1.0 / (b * c * c)), (coef if want_coef else None)
     return loss, (coef if want_coef else None)
+
+
+def loss_finalize(parts, losses, extra=None, weights=None, total=None):
+    """One launch: losses[i] = reduced deferred style-loss partials (parts from
+    style_loss(defer_ws=...)), and optionally total = sum w_i losses_i + sum w extra."""
+    lp = N.LossParts()
+    assert len(parts) <= 8
+    for i, (ptr, n, inv) in enumerate(parts):
+        lp.parts[i], lp.nparts[i], lp.inv[i] = ptr, n, inv
+    lp.k = len(parts)
+    m = 0 if extra is None else extra.numel()
+    w = None
+    if weights is not None:
+        w = (C.c_float * len(weights))(*[float(x) for x in weights])
+    check(lib().stx_loss_finalize(C.byref(lp), losses.data_ptr(), _p(extra), m, w, _p(total),
+                                  _stream()), "stx_loss_finalize")
+    return losses
 
 
 def gram_bwd_fused(coef, z, out=None, acc_scale=None, up_dp=None, aux=None, aux_scale=0.0,

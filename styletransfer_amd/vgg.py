@@ -160,10 +160,12 @@ class LossState:
     alpha: float = 0.0
     amax: torch.Tensor = None                   # [16] max|.| slots of split-conv inputs
     pools: list = field(default_factory=lambda: [None] * 5)  # fused relu+pool outputs
+    lws: list = field(default_factory=lambda: [None] * 5)    # per-layer style-loss scratch
+    parts: list = field(default_factory=lambda: [None] * 5)  # deferred loss partials
 
 
 def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
-                 folded_weights=None):
+                 folded_weights=None, total=None):
     """Forward of all 7 losses for input batch x [B,3,H,W] given style targets and
     the content target c4 (= Z4 of the content image, pre-ReLU).
 
@@ -171,7 +173,11 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     into the backward operators (A_l scaled by style_weight; the content term's
     alpha*Z4 on A_4's diagonal) so the backward needs no device scalars — the
     Gatys engine's case.  None: operators for weight 1; the backward scales by the
-    upstream gradient vector (autograd case)."""
+    upstream gradient vector (autograd case).
+
+    The five style-loss reductions are deferred (partials kept in per-layer
+    workspaces) and done in one launch after the forward, together with the
+    weighted total (into `total`, if given, with the folded weights)."""
     if st is None:
         st = LossState()
     dev = x.device
@@ -226,10 +232,14 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                 z.record_stream(side)
         with torch.cuda.stream(side):
             i = STYLE_CONVS.index(l)
-            _, st.coef[i] = ops.style_loss(z, targets[i], weight=sw,
-                                           diag_alpha=alpha if l == CONTENT_CONV else 0.0,
-                                           loss=st.losses[i], coef=st.coef[i],
-                                           z_amax=slot(st.amax, l + 1) if split else None)
+            b_, c_ = z.shape[:2]
+            need = N.lib().stx_gram_ws(b_, c_, z[0, 0].numel())
+            if st.lws[i] is None or st.lws[i].numel() < need:
+                st.lws[i] = torch.empty(need, device=dev, dtype=torch.uint8)
+            st.parts[i], st.coef[i] = ops.style_loss(
+                z, targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
+                coef=st.coef[i], z_amax=slot(st.amax, l + 1) if split else None,
+                defer_ws=st.lws[i])
             if l == CONTENT_CONV:  # content, feature, feature-mse: one pass
                 ops.mse(z, c4, mode=2, out=st.losses[5:8])
 
@@ -240,6 +250,13 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         if not capturing:
             for c in st.coef:
                 c.record_stream(main)
+    # the 5 style losses (+ the weighted total) in one launch
+    w = None
+    if total is not None:
+        fw = folded_weights if folded_weights is not None else (1.0, 1.0)
+        w = [float(fw[0])] * 5 + [float(fw[1])]
+    ops.loss_finalize(st.parts, st.losses[0:5], extra=st.losses[5:6] if w else None, weights=w,
+                      total=total)
     return st
 
 
@@ -369,8 +386,7 @@ class GatysEngine:
 
     def _iteration(self):
         loss_forward(self.feat, self.targets, self.x, self.c4, self.st,
-                     folded_weights=(self.sw, self.cw))
-        ops.loss_combine(self.st.losses, [self.sw] * 5 + [self.cw], self.total)
+                     folded_weights=(self.sw, self.cw), total=self.total)
         loss_backward(self.feat, self.st, dx=self.grad, feature_grad=False,
                       scratch=self.scratch)
         ops.adam_step(self.x, self.grad, self.m, self.v, self.step_dev, self.adam_ws, self.lr,
