@@ -68,6 +68,8 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
       for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
 
   const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const auto rdy = make_srd(dy, (uint32_t)((size_t)g.n * g.cout * H * W * 4u));
+  const auto rx = make_srd(x, (uint32_t)((size_t)g.n * g.cin * g.h * g.w * 4u));
   struct Step {
     f32x4 a0, a1;   // dY[co][y][x0+8h .. +7]
     f32x4 c0, c1;   // dY[co+32][y][x0+8h .. +7]
@@ -86,36 +88,30 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
         ++ln;
       }
     }
-    const float* pa = dy + (((size_t)n * g.cout + co) * H + y) * W + x0;
-    if (co_ok) {
-      t.a0 = *reinterpret_cast<const f32x4*>(pa);
-      t.a1 = *reinterpret_cast<const f32x4*>(pa + 4);
-    } else {
-      t.a0 = t.a1 = zero4;
-    }
-    if (co2_ok) {
-      const float* pc = pa + (size_t)32 * H * W;
-      t.c0 = *reinterpret_cast<const f32x4*>(pc);
-      t.c1 = *reinterpret_cast<const f32x4*>(pc + 4);
-    } else {
-      t.c0 = t.c1 = zero4;
-    }
+    // branch-free: invalid rows / taps / neighbours read 0 through the descriptors'
+    // range check (predicated loads compiled to exec branches with vmcnt(0) joins,
+    // which serialised the prefetch ring)
+    const uint32_t oa = (uint32_t)((((size_t)n * g.cout + co) * H + y) * W + x0) * 4u;
+    t.a0 = buf_ld4(rdy, co_ok ? oa : BUF_OOB);
+    t.a1 = buf_ld4(rdy, co_ok ? oa + 16u : BUF_OOB);
+    const uint32_t oc = oa + (uint32_t)32 * H * W * 4u;
+    t.c0 = buf_ld4(rdy, co2_ok ? oc : BUF_OOB);
+    t.c1 = buf_ld4(rdy, co2_ok ? oc + 16u : BUF_OOB);
     const int vy = y + kh - 1;
-    t.b0 = t.b1 = zero4;
-    t.bl = t.br = 0.f;
-    if (ci_ok && vy >= 0 && vy < H) {
-      if (!up) {
-        const float* pb = x + (((size_t)n * g.cin + ci) * g.h + vy) * g.w + x0;
-        t.b0 = *reinterpret_cast<const f32x4*>(pb);
-        t.b1 = *reinterpret_cast<const f32x4*>(pb + 4);
-        if (x0 > 0) t.bl = pb[-1];
-        if (x0 + 8 < W) t.br = pb[8];
-      } else {  // V[vy][vx] = x[vy/2][vx/2]; x0 is even
-        const float* pb = x + (((size_t)n * g.cin + ci) * g.h + (vy >> 1)) * g.w + (x0 >> 1);
-        t.b0 = *reinterpret_cast<const f32x4*>(pb);
-        if (x0 > 0) t.bl = pb[-1];
-        if (x0 + 8 < W) t.br = pb[4];
-      }
+    const bool bok = ci_ok && vy >= 0 && vy < H;
+    if (!up) {
+      const uint32_t ob = (uint32_t)((((size_t)n * g.cin + ci) * g.h + vy) * g.w + x0) * 4u;
+      t.b0 = buf_ld4(rx, bok ? ob : BUF_OOB);
+      t.b1 = buf_ld4(rx, bok ? ob + 16u : BUF_OOB);
+      t.bl = buf_ld(rx, (bok && x0 > 0) ? ob - 4u : BUF_OOB);
+      t.br = buf_ld(rx, (bok && x0 + 8 < W) ? ob + 32u : BUF_OOB);
+    } else {  // V[vy][vx] = x[vy/2][vx/2]; x0 is even
+      const uint32_t ob =
+          (uint32_t)((((size_t)n * g.cin + ci) * g.h + (vy >> 1)) * g.w + (x0 >> 1)) * 4u;
+      t.b0 = buf_ld4(rx, bok ? ob : BUF_OOB);
+      t.b1 = zero4;
+      t.bl = buf_ld(rx, (bok && x0 > 0) ? ob - 4u : BUF_OOB);
+      t.br = buf_ld(rx, (bok && x0 + 8 < W) ? ob + 16u : BUF_OOB);
     }
   };
   auto compute = [&](const Step& t) {
@@ -235,6 +231,8 @@ __global__ void wgrad16_reduce_kernel(const float* __restrict__ ws, float* __res
 
 static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg16& g) {
   if (wv % 16 != 0 || cin < 16 || cout < 16 || n <= 0 || hv <= 0) return false;
+  // 32-bit buffer offsets over the whole dy / x tensors
+  if ((size_t)n * std::max(cin, cout) * hv * wv * 4 >= (1ull << 31)) return false;
   if (in_mode != STX_IN_RAW && in_mode != STX_IN_RELU && in_mode != STX_IN_UPSAMPLE2) return false;
   g.n = n;
   g.cin = cin;
