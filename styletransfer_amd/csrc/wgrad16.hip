@@ -36,6 +36,7 @@ struct Wg16 {
   int cout32, cin32;
 };
 
+template <int PF>
 __global__ void __launch_bounds__(256)
 wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ ws,
                const float* __restrict__ x_amax, const float* __restrict__ dy_amax, Wg16 g) {
@@ -169,7 +170,6 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
   // four steps of loads in flight (HBM latency >> one step of 9 MFMAs)
   const int s0 = split * g.steps_per_split;
   const int s1 = min(g.steps, s0 + g.steps_per_split);
-  constexpr int PF = 4;
   {
     const int r0 = s0 / wsteps;
     lxs = s0 - r0 * wsteps;
@@ -246,7 +246,13 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   g.cin32 = g.ncit * 32;
   g.steps = n * hv * (wv / 16);
   const int units = 3 * g.ncot * g.ncit;
-  int ns = cdiv(1024, units);                     // ~1024 waves
+  static const int target = [] {
+    const char* e = getenv("STX_WG16_WAVES");
+    return e ? atoi(e) : 2048;
+  }();
+  // ~2048 waves (one per SIMD pair at this kernel's 1 wave/SIMD; measured 8 % faster
+  // than 1024 on the ITN residual convs despite the larger split-K slab)
+  int ns = cdiv(target, units);
   ns = std::max(1, std::min(ns, cdiv(g.steps, 8)));  // >= 8 steps per wave
   g.steps_per_split = cdiv(g.steps, ns);
   g.nsplit = cdiv(g.steps, g.steps_per_split);
@@ -290,8 +296,19 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
   }
   hipStream_t st = (hipStream_t)stream;
   const int units = g.nsplit * 3 * g.ncot * g.ncit;
-  hipLaunchKernelGGL(wgrad16_kernel, dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy, (float*)ws,
-                     x_amax, dy_amax, g);
+  static const int pf = [] {
+    const char* e = getenv("STX_WG16_PF");
+    return e ? atoi(e) : 4;
+  }();
+  if (pf >= 12)
+    hipLaunchKernelGGL(wgrad16_kernel<12>, dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
+                       (float*)ws, x_amax, dy_amax, g);
+  else if (pf >= 8)
+    hipLaunchKernelGGL(wgrad16_kernel<8>, dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
+                       (float*)ws, x_amax, dy_amax, g);
+  else
+    hipLaunchKernelGGL(wgrad16_kernel<4>, dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
+                       (float*)ws, x_amax, dy_amax, g);
   const long long total = (long long)cout * cin * 9;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(wgrad16_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, dw,
