@@ -92,14 +92,31 @@ instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
 // Backward.  g = dy * (y > 0 if relu);  xh = (u-mean)*rstd
 //   dgamma_nc = sum g*xh ; dbeta_nc = sum g
 //   du = gamma*rstd/HW * (HW*g - dbeta_nc - xh*dgamma_nc)
-__global__ void __launch_bounds__(NB)
+// max |.| over an NT-thread block, then one atomic into slot (block id & 31)
+template <int NT>
+__device__ __forceinline__ void block_max_to_nt(float* group, uint32_t mu, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mu = max(mu, (uint32_t)__shfl_xor((int)mu, o, 64));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = __uint_as_float(mu);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t r = 0u;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) r = max(r, __float_as_uint(red[i]));
+    atomic_max_abs(group + (blockIdx.x & (STX_AMAX_SLOTS - 1)), __uint_as_float(r));
+  }
+}
+
+template <int NBT>
+__global__ void __launch_bounds__(NBT)
 instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                     const float* __restrict__ x, const float* __restrict__ res,
                     const float* __restrict__ gamma, const float* __restrict__ mean,
                     const float* __restrict__ rstd, float* __restrict__ du,
                     float* __restrict__ parts, int c, int hw, int relu,
                     float* __restrict__ out_amax) {
-  __shared__ float red[NB / 64];
+  __shared__ float red[NBT / 64];
   const size_t base = (size_t)blockIdx.x * hw;
   const int ch = blockIdx.x % c;
   const float mu = mean[blockIdx.x], rs = rstd[blockIdx.x];
@@ -116,7 +133,7 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
   // each thread keeps 8 loads in flight
   auto ld4 = [](const float* p, int i) { return *reinterpret_cast<const f32x4*>(p + i); };
   if (vec) {
-    for (int i = threadIdx.x * 4; i < hw; i += NB * 4) {
+    for (int i = threadIdx.x * 4; i < hw; i += NBT * 4) {
       const f32x4 d4 = ld4(dyp, i);
       const f32x4 x4 = ld4(xp, i);
       const f32x4 r4 = rp ? ld4(rp, i) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -130,7 +147,7 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
       }
     }
   } else {
-    for (int i = threadIdx.x; i < hw; i += NB) {
+    for (int i = threadIdx.x; i < hw; i += NBT) {
       float g = dyp[i];
       if (relu && !(yp[i] > 0.f)) g = 0.f;
       const float xh = (xp[i] + (rp ? rp[i] : 0.f) - mu) * rs;
@@ -138,14 +155,14 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
       sgx += g * xh;
     }
   }
-  sg = block_sum<NB>(sg, red);
-  sgx = block_sum<NB>(sgx, red);
+  sg = block_sum<NBT>(sg, red);
+  sgx = block_sum<NBT>(sgx, red);
   const float gm = gamma ? gamma[ch] : 1.f;
   const float k = gm * rs / (float)hw;
   float* dup = du + base;
   uint32_t om = 0u;  // max |du| as IEEE bits
   if (vec) {
-    for (int i = threadIdx.x * 4; i < hw; i += NB * 4) {
+    for (int i = threadIdx.x * 4; i < hw; i += NBT * 4) {
       const f32x4 d4 = ld4(dyp, i);
       const f32x4 x4 = ld4(xp, i);
       const f32x4 r4 = rp ? ld4(rp, i) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -161,7 +178,7 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
       *reinterpret_cast<f32x4*>(dup + i) = o;
     }
   } else {
-    for (int i = threadIdx.x; i < hw; i += NB) {
+    for (int i = threadIdx.x; i < hw; i += NBT) {
       float g = dyp[i];
       if (relu && !(yp[i] > 0.f)) g = 0.f;
       const float xh = (xp[i] + (rp ? rp[i] : 0.f) - mu) * rs;
@@ -174,7 +191,177 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
     parts[2 * blockIdx.x] = sgx;
     parts[2 * blockIdx.x + 1] = sg;
   }
-  if (out_amax) block_max_to(out_amax, __uint_as_float(om));
+  if (out_amax) block_max_to_nt<NBT>(out_amax, om, red);
+}
+
+// Register-resident variants for planes of up to 4*NT*R4 floats (the ImageTransformNet
+// planes: 64^2, 128^2, 256^2): each thread loads its R4 float4s of u = x (+res) once,
+// and the statistics and the output come from registers -- one HBM read and one write
+// per element instead of three passes (the loop kernels above re-read the plane).
+// Same arithmetic; block reductions in a fixed order (bit-reproducible).
+template <int NT>
+__device__ __forceinline__ float block_sum_nt(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s += red[i];
+  return s;
+}
+
+template <int NT, int R4>
+__global__ void __launch_bounds__(NT)
+instnorm_fwd_reg_kernel(const float* __restrict__ x, const float* __restrict__ res,
+                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                        float* __restrict__ y, float* __restrict__ mean_out,
+                        float* __restrict__ rstd_out, int c, int hw, float eps, int relu,
+                        float* __restrict__ out_amax) {
+  __shared__ float red[NT / 64];
+  const size_t base = (size_t)blockIdx.x * hw;
+  const int ch = blockIdx.x % c;
+  const int n4 = hw >> 2;
+  const f32x4* xp = reinterpret_cast<const f32x4*>(x + base);
+  const f32x4* rp = res ? reinterpret_cast<const f32x4*>(res + base) : nullptr;
+  f32x4 u[R4];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < R4; ++k) {
+    const int i = threadIdx.x + k * NT;
+    u[k] = i < n4 ? xp[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (rp && i < n4) u[k] += rp[i];
+  }
+#pragma unroll
+  for (int k = 0; k < R4; ++k) s += (u[k][0] + u[k][1]) + (u[k][2] + u[k][3]);
+  const float mean = block_sum_nt<NT>(s, red) / (float)hw;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < R4; ++k) {
+    if (threadIdx.x + k * NT < n4) {
+      const f32x4 d = u[k] - mean;
+      q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+    }
+  }
+  const float var = block_sum_nt<NT>(q, red) / (float)hw;
+  const float rstd = 1.f / sqrtf(var + eps);
+  const float gsc = gamma ? gamma[ch] * rstd : rstd;
+  const float sh = (beta ? beta[ch] : 0.f) - mean * gsc;
+  f32x4* yp = reinterpret_cast<f32x4*>(y + base);
+  uint32_t om = 0u;
+#pragma unroll
+  for (int k = 0; k < R4; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < n4) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = u[k][e] * gsc + sh;
+        if (relu) o[e] = fmaxf(o[e], 0.f);
+        om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
+      }
+      yp[i] = o;
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (mean_out) mean_out[blockIdx.x] = mean;
+    if (rstd_out) rstd_out[blockIdx.x] = rstd;
+  }
+  if (out_amax) {
+    uint32_t m = om;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = __uint_as_float(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t r = 0u;
+#pragma unroll
+      for (int i = 0; i < NT / 64; ++i) r = max(r, __float_as_uint(red[i]));
+      atomic_max_abs(out_amax + (blockIdx.x & (STX_AMAX_SLOTS - 1)), __uint_as_float(r));
+    }
+  }
+}
+
+template <int NT, int R4>
+__global__ void __launch_bounds__(NT)
+instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                        const float* __restrict__ x, const float* __restrict__ res,
+                        const float* __restrict__ gamma, const float* __restrict__ mean,
+                        const float* __restrict__ rstd, float* __restrict__ du,
+                        float* __restrict__ parts, int c, int hw, int relu,
+                        float* __restrict__ out_amax) {
+  __shared__ float red[NT / 64];
+  const size_t base = (size_t)blockIdx.x * hw;
+  const int ch = blockIdx.x % c;
+  const float mu = mean[blockIdx.x], rs = rstd[blockIdx.x];
+  const int n4 = hw >> 2;
+  const f32x4* dyp = reinterpret_cast<const f32x4*>(dy + base);
+  const f32x4* yp = relu ? reinterpret_cast<const f32x4*>(y + base) : nullptr;
+  const f32x4* xp = reinterpret_cast<const f32x4*>(x + base);
+  const f32x4* rp = res ? reinterpret_cast<const f32x4*>(res + base) : nullptr;
+  f32x4 g[R4], xh[R4];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int k = 0; k < R4; ++k) {
+    const int i = threadIdx.x + k * NT;
+    const bool in = i < n4;
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 d4 = in ? dyp[i] : z4;
+    f32x4 u4 = in ? xp[i] : z4;
+    if (rp && in) u4 += rp[i];
+    const f32x4 y4 = (relu && in) ? yp[i] : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      g[k][e] = (relu && !(y4[e] > 0.f)) ? 0.f : d4[e];
+      xh[k][e] = in ? (u4[e] - mu) * rs : 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < R4; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sg += g[k][e];
+      sgx += g[k][e] * xh[k][e];
+    }
+  sg = block_sum_nt<NT>(sg, red);
+  sgx = block_sum_nt<NT>(sgx, red);
+  const float gm = gamma ? gamma[ch] : 1.f;
+  const float kk = gm * rs / (float)hw;
+  f32x4* dup = reinterpret_cast<f32x4*>(du + base);
+  uint32_t om = 0u;
+#pragma unroll
+  for (int k = 0; k < R4; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < n4) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = kk * ((float)hw * g[k][e] - sg - xh[k][e] * sgx);
+        om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
+      }
+      dup[i] = o;
+    }
+  }
+  if (threadIdx.x == 0) {
+    parts[2 * blockIdx.x] = sgx;
+    parts[2 * blockIdx.x + 1] = sg;
+  }
+  if (out_amax) {
+    uint32_t m = om;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = __uint_as_float(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t r = 0u;
+#pragma unroll
+      for (int i = 0; i < NT / 64; ++i) r = max(r, __float_as_uint(red[i]));
+      atomic_max_abs(out_amax + (blockIdx.x & (STX_AMAX_SLOTS - 1)), __uint_as_float(r));
+    }
+  }
 }
 
 __global__ void instnorm_param_grad_kernel(const float* __restrict__ parts, int n, int c,
@@ -207,8 +394,19 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
     set_error("stx_instnorm_fwd: 16-byte alignment required");
     return STX_E_INVALID;
   }
-  hipLaunchKernelGGL(instnorm_fwd_kernel, dim3(n * c), dim3(NB), 0, (hipStream_t)stream, x, res,
-                     gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
+  hipStream_t st = (hipStream_t)stream;
+  if (hw % 4 == 0 && hw <= 4 * 256 * 4)
+    hipLaunchKernelGGL((instnorm_fwd_reg_kernel<256, 4>), dim3(n * c), dim3(256), 0, st, x, res,
+                       gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
+  else if (hw % 4 == 0 && hw <= 4 * 256 * 16)
+    hipLaunchKernelGGL((instnorm_fwd_reg_kernel<256, 16>), dim3(n * c), dim3(256), 0, st, x, res,
+                       gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
+  else if (hw % 4 == 0 && hw <= 4 * 1024 * 16)
+    hipLaunchKernelGGL((instnorm_fwd_reg_kernel<1024, 16>), dim3(n * c), dim3(1024), 0, st, x,
+                       res, gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
+  else
+    hipLaunchKernelGGL(instnorm_fwd_kernel, dim3(n * c), dim3(NB), 0, st, x, res, gamma, beta, y,
+                       mean, rstd, c, hw, eps, relu, out_amax);
   return check_launch("stx_instnorm_fwd");
 }
 
@@ -230,8 +428,21 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
     return STX_E_WORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(instnorm_bwd_kernel, dim3(n * c), dim3(NB), 0, st, dy, y, x, res, gamma, mean,
-                     rstd, du, (float*)ws, c, hw, relu, out_amax);
+  const bool al = ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(y) |
+                    reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) |
+                    reinterpret_cast<uintptr_t>(du)) & 15) == 0 && hw % 4 == 0;
+  if (al && hw <= 4 * 256 * 4)
+    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 4>), dim3(n * c), dim3(256), 0, st, dy, y, x,
+                       res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
+  else if (al && hw <= 4 * 256 * 16)
+    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 16>), dim3(n * c), dim3(256), 0, st, dy, y,
+                       x, res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
+  else if (hw >= 4 * 1024 * 4)  // big planes (256^2): 16 waves per plane
+    hipLaunchKernelGGL(instnorm_bwd_kernel<1024>, dim3(n * c), dim3(1024), 0, st, dy, y, x, res,
+                       gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
+  else
+    hipLaunchKernelGGL(instnorm_bwd_kernel<NB>, dim3(n * c), dim3(NB), 0, st, dy, y, x, res, gamma,
+                       mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   if (dgamma || dbeta)
     hipLaunchKernelGGL(instnorm_param_grad_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st,
                        (const float*)ws, n, c, dgamma, dbeta, accumulate_params);

@@ -205,28 +205,39 @@ def test_adam(dev):
     assert rel(p, pr.detach().to(dev)) < 1e-6
 
 
-@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (False, True)])
-def test_instnorm(dev, relu, res):
-    x = rnd(2, 32, 12, 20, dev=dev, seed=71, scale=3, shift=-1).requires_grad_()
-    r = rnd(2, 32, 12, 20, dev=dev, seed=72).requires_grad_() if res else None
-    gamma = rnd(32, dev=dev, seed=73, shift=0.5).requires_grad_()
-    beta = rnd(32, dev=dev, seed=74).requires_grad_()
+@pytest.mark.parametrize("relu,res,hw", [(False, False, (12, 20)), (True, False, (12, 20)),
+                                         (False, True, (12, 20)), (True, True, (64, 64)),
+                                         (True, False, (128, 128)), (False, True, (256, 256)),
+                                         (True, False, (7, 9))])
+def test_instnorm(dev, relu, res, hw):
+    """InstanceNorm (+res, +ReLU) forward/backward on every kernel variant (register-
+    resident planes up to 64^2 / 128^2 / 256^2, the loop kernels otherwise) and the
+    max|.| annotations of y and du."""
+    c = 32 if hw == (12, 20) else 4
+    x = rnd(2, c, *hw, dev=dev, seed=71, scale=3, shift=-1).requires_grad_()
+    r = rnd(2, c, *hw, dev=dev, seed=72).requires_grad_() if res else None
+    gamma = rnd(c, dev=dev, seed=73, shift=0.5).requires_grad_()
+    beta = rnd(c, dev=dev, seed=74).requires_grad_()
     u = x + r if res else x
     ref = F.instance_norm(u, weight=gamma, bias=beta, eps=1e-5)
     if relu:
         ref = F.relu(ref)
+    ya = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
     y, mean, rstd = ops.instnorm_fwd(x.detach(), gamma.detach(), beta.detach(),
-                                     res=r.detach() if res else None, relu=relu)
+                                     res=r.detach() if res else None, relu=relu, out_amax=ya)
     assert rel(y, ref) < 1e-5
+    assert float(ya.max()) == float(y.abs().max())
     dy = rnd(*y.shape, dev=dev, seed=75, scale=2, shift=-1)
     grads = torch.autograd.grad(ref, [x, gamma, beta], dy)
-    dg = torch.empty(32, device=dev)
-    db = torch.empty(32, device=dev)
+    dg = torch.empty(c, device=dev)
+    db = torch.empty(c, device=dev)
+    da = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
     du = ops.instnorm_bwd(dy, y, x.detach(), r.detach() if res else None, gamma.detach(), mean,
-                          rstd, relu=relu, dgamma=dg, dbeta=db)
+                          rstd, relu=relu, dgamma=dg, dbeta=db, out_amax=da)
     assert rel(du, grads[0]) < 1e-4
     assert rel(dg, grads[1]) < 1e-5
     assert rel(db, grads[2]) < 1e-5
+    assert float(da.max()) == float(du.abs().max())
 
 
 def test_upsample_tv(dev):
