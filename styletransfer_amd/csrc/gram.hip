@@ -532,7 +532,11 @@ static void gram_geometry(int c, int hw, int b, int& nsplit, int& split_len, int
 static void gram_geometry16(int c, int hw, int b, int& nsplit, int& split_len, int& ntu) {
   const int nt = cdiv(c, GT);
   ntu = nt * (nt + 1) / 2;
-  int want = rup(cdiv(640, ntu * b), 8);
+  static const int target = [] {
+    const char* e = getenv("STX_GRAM_BLOCKS");
+    return e ? std::max(8, atoi(e)) : 640;
+  }();
+  int want = rup(cdiv(target, ntu * b), 8);
   const int max_splits = std::max(1, cdiv(hw, 256));
   want = std::max(8, std::min(want, rup(max_splits, 8)));
   split_len = rup(cdiv(hw, want), 256);
