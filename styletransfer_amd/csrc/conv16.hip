@@ -624,6 +624,44 @@ __global__ void amax_kernel(const float* __restrict__ x, long long n, float* __r
   block_max_to(out, m);
 }
 
+// One launch, no clearing: exactly STX_AMAX_SLOTS blocks, block b reduces slice b of x
+// and stores its max into slot b (plain store), so the group's max is max|x|.
+__global__ void __launch_bounds__(1024) amax_slots_kernel(const float* __restrict__ x,
+                                                          long long n, float* __restrict__ out) {
+  __shared__ float red[16];
+  const long long n4 = n >> 2;
+  const long long per = (n4 + STX_AMAX_SLOTS - 1) / STX_AMAX_SLOTS;
+  const long long b0 = blockIdx.x * per, b1 = min(n4, b0 + per);
+  float m = 0.f;
+  auto upd = [&](float v) {
+    const float a = fabsf(v);
+    m = (a != a) ? a : fmaxf(m, a);
+  };
+#pragma unroll 4
+  for (long long i = b0 + threadIdx.x; i < b1; i += 1024) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    upd(v[0]);
+    upd(v[1]);
+    upd(v[2]);
+    upd(v[3]);
+  }
+  if (blockIdx.x == 0)
+    for (long long i = 4 * n4 + threadIdx.x; i < n; i += 1024) upd(x[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float other = __shfl_xor(m, o, 64);
+    m = (other != other) ? other : fmaxf(m, other);
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = red[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
+    out[blockIdx.x] = r;
+  }
+}
+
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st) {
   switch (p.in_mode) {
     case STX_IN_RAW: return dispatch16_tw<STX_IN_RAW>(p, st);
@@ -653,6 +691,10 @@ extern "C" int stx_amax(const float* x, long long n, float* out, void* stream) {
   if (reinterpret_cast<uintptr_t>(x) & 15) {
     set_error("stx_amax: x must be 16-byte aligned");
     return STX_E_INVALID;
+  }
+  if (n <= (8ll << 20)) {  // up to 32 MB: one launch, every slot written (no clearing)
+    hipLaunchKernelGGL(amax_slots_kernel, dim3(STX_AMAX_SLOTS), dim3(1024), 0, st, x, n, out);
+    return check_launch("stx_amax");
   }
   // the slots are cleared by a kernel, not hipMemsetAsync: a memset node captured into a
   // hipGraph was observed to run out of order with the amax kernel on replay
