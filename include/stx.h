@@ -127,6 +127,10 @@ size_t stx_conv_weight16_bytes(int cin, int cout, int ks, int transpose);
  * stx_conv_weight_prep). */
 int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax, int cout, int cin, int ks,
                            int transpose, void* stream);
+/* Both split slabs of one weight (forward and data gradient) and their shared w_amax in
+ * two launches (one max pass, one conversion) -- a trained layer re-preps every step. */
+int stx_conv_weight_prep16_pair(const float* w, void* wt16, void* wtT16, float* w_amax,
+                                int cout, int cin, int ks, void* stream);
 /* *out = max |x[i]| over n floats (device scalar; NaN propagates). */
 int stx_amax(const float* x, long long n, float* out, void* stream);
 
@@ -181,6 +185,22 @@ int stx_gram(const float* z, float* g, int b, int c, int hw, float scale,
  * so that dz = A·z (+ aux) is d(weight*loss)/dz; g_out (optional) receives G.
  * cpad = stx_gram_coef_pitch(c).  ws: stx_gram_ws(b, c, hw). */
 int stx_gram_coef_pitch(int c);
+/* With loss == NULL stx_style_loss leaves its loss partials in ws: *nparts floats at
+ * byte offset stx_style_loss_parts(b, c, hw, &nparts), loss = sum * 1/(b*c*c). */
+size_t stx_style_loss_parts(int b, int c, int hw, int* nparts);
+/* Deferred loss reductions in one launch (the 5 StyleLoss values of a forward, then
+ * the weighted total of get_total_current_{style,content}_loss):
+ *   losses[i] = inv[i] * sum(parts[i][0 .. nparts[i]))          i < k (fixed order)
+ *   *total    = sum_i w[i] losses[i] + sum_j w[k+j] extra[j]    (if total != NULL)
+ * extra: m device scalars (e.g. the content loss); w_host: k + m host floats. */
+typedef struct stx_loss_parts {
+  const float* parts[8];
+  int nparts[8];
+  float inv[8];
+  int k;
+} stx_loss_parts;
+int stx_loss_finalize(const stx_loss_parts* lp, float* losses, const float* extra, int m,
+                      const float* w_host, float* total, void* stream);
 int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
                    float* loss, int b, int c, int hw, int target_batched, float weight,
                    float diag_alpha, const float* z_amax, void* ws, size_t ws_bytes,

@@ -45,9 +45,14 @@ class Conv2dFn(torch.autograd.Function):
         # (no fp32 slab needed); max|x| is computed once and kept for the wgrad
         split = _split_on() and pad == 1 and ops.split_eligible(cin, cout, ks, stride)
         x_amax = None
+        ctx.wtT16 = None
         if split:
             if wt16 is None:
-                wt16 = ops.conv_weight_prep16(w.detach().contiguous())
+                if w.requires_grad and stride == 1 and ops.split_eligible(cout, cin, ks, 1):
+                    # trained layer: both slabs (forward + data gradient) in one go
+                    wt16, ctx.wtT16 = ops.conv_weight_prep16_pair(w.detach().contiguous())
+                else:
+                    wt16 = ops.conv_weight_prep16(w.detach().contiguous())
             x_amax = ops.ARENA.lookup(x)  # annotated by the producer (InstanceNorm)
             if x_amax is None:
                 x_amax = ops.amax(x)
@@ -83,7 +88,8 @@ class Conv2dFn(torch.autograd.Function):
             if stride == 1:
                 wtT = wtT16 = None
                 if split_d:
-                    wtT16 = ops.conv_weight_prep16(w.detach().contiguous(), transpose=True)
+                    wtT16 = ctx.wtT16 if ctx.wtT16 is not None else ops.conv_weight_prep16(
+                        w.detach().contiguous(), transpose=True)
                 else:
                     wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
                 dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16,

@@ -569,9 +569,10 @@ static int dispatch16_tw(const stx_conv_params& p, hipStream_t st) {
 
 // ------------------------------------------------------------ weight split prep
 // slab [cin16/16][tap][P][cg][cout64][8] fp16 of the GEMM weights W'[co][ci][tap]
-__global__ void weight_prep16_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
-                                     const float* __restrict__ w_amax, int cout, int cin,
-                                     int transpose, int gin16, int gout64) {
+__device__ __forceinline__ void weight_prep16_body(const float* __restrict__ w,
+                                                   _Float16* __restrict__ out,
+                                                   const float* __restrict__ w_amax, int cout,
+                                                   int cin, int transpose, int gin16, int gout64) {
   const long long total = (long long)gin16 * 9 * 2 * gout64;
   const float sw = __builtin_ldexpf(1.f, 15 - amax_exp(read_amax(w_amax)));
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -599,6 +600,22 @@ __global__ void weight_prep16_kernel(const float* __restrict__ w, _Float16* __re
     const _Float16 vh = (_Float16)v;
     out[i] = P == 0 ? vh : (_Float16)(v - (float)vh);
   }
+}
+
+__global__ void weight_prep16_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
+                                     const float* __restrict__ w_amax, int cout, int cin,
+                                     int transpose, int gin16, int gout64) {
+  weight_prep16_body(w, out, w_amax, cout, cin, transpose, gin16, gout64);
+}
+
+// both slabs of one weight in one launch: blockIdx.y 0 = forward, 1 = data gradient
+__global__ void weight_prep16_pair_kernel(const float* __restrict__ w, _Float16* __restrict__ fwd,
+                                          _Float16* __restrict__ dgr,
+                                          const float* __restrict__ w_amax, int cout, int cin) {
+  if (blockIdx.y == 0)
+    weight_prep16_body(w, fwd, w_amax, cout, cin, 0, rup(cin, 16), rup(cout, 64));
+  else
+    weight_prep16_body(w, dgr, w_amax, cout, cin, 1, rup(cout, 16), rup(cin, 64));
 }
 
 // -------------------------------------------------------------------- amax
@@ -703,6 +720,23 @@ extern "C" int stx_amax(const float* x, long long n, float* out, void* stream) {
   const int blocks = (int)std::min<long long>(std::max<long long>(1, (n / 4 + 255) / 256), 512);
   hipLaunchKernelGGL(amax_kernel, dim3(blocks), dim3(256), 0, st, x, n, out);
   return check_launch("stx_amax");
+}
+
+extern "C" int stx_conv_weight_prep16_pair(const float* w, void* wt16, void* wtT16, float* w_amax,
+                                           int cout, int cin, int ks, void* stream) {
+  if (ks != 3 || !w || !wt16 || !wtT16 || !w_amax || cout <= 0 || cin <= 0) {
+    set_error("stx_conv_weight_prep16_pair: ks must be 3 and pointers non-NULL");
+    return STX_E_INVALID;
+  }
+  int rc = stx_amax(w, (long long)cout * cin * 9, w_amax, stream);
+  if (rc) return rc;
+  const long long total = std::max((long long)rup(cin, 16) * rup(cout, 64),
+                                   (long long)rup(cout, 16) * rup(cin, 64)) * 9 * 2;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(weight_prep16_pair_kernel, dim3(blocks, 2), dim3(256), 0,
+                     (hipStream_t)stream, w, reinterpret_cast<_Float16*>(wt16),
+                     reinterpret_cast<_Float16*>(wtT16), w_amax, cout, cin);
+  return check_launch("stx_conv_weight_prep16_pair");
 }
 
 extern "C" int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax, int cout, int cin,

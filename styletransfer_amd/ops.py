@@ -147,6 +147,22 @@ def conv_weight_prep16(w: torch.Tensor, transpose: bool = False):
     return wt16, w_amax
 
 
+def conv_weight_prep16_pair(w: torch.Tensor):
+    """(forward slab, data-gradient slab), sharing one device max|w| (two launches)."""
+    _req(w, "weight")
+    cout, cin, ks, _ = w.shape
+    L = lib()
+    wt16 = torch.empty(L.stx_conv_weight16_bytes(cin, cout, ks, 0), device=w.device,
+                       dtype=torch.uint8)
+    wtT16 = torch.empty(L.stx_conv_weight16_bytes(cin, cout, ks, 1), device=w.device,
+                        dtype=torch.uint8)
+    w_amax = torch.empty(N.STX_AMAX_SLOTS, device=w.device, dtype=torch.float32)
+    check(L.stx_conv_weight_prep16_pair(w.data_ptr(), wt16.data_ptr(), wtT16.data_ptr(),
+                                        w_amax.data_ptr(), cout, cin, ks, _stream()),
+          "conv_weight_prep16_pair")
+    return (wt16, w_amax), (wtT16, w_amax)
+
+
 def split_eligible(cin, cout, ks, stride=1):
     """Shapes stx_conv2d runs on the fp16 hi/lo split MFMA kernel (conv16.hip)."""
     return ks == 3 and stride == 1 and cin >= 16 and cout > 4

@@ -285,3 +285,15 @@ def test_split_wgrad_9x9_few(dev, case):
     acc = dw16.clone()
     ops.conv2d_wgrad(x, dy, cin, cout, 9, dw=acc, accumulate=True)
     assert rel(acc, 2 * ref) < TOL64
+
+
+@pytest.mark.parametrize("shape", [(64, 64), (128, 32), (20, 70)])
+def test_weight_prep16_pair(dev, shape):
+    """Both split slabs in one call == the two single preps, bit for bit."""
+    cout, cin = shape
+    w = rnd(cout, cin, 3, 3, dev=dev, seed=91, scale=0.2, shift=-0.1)
+    (a, am), (b, bm) = ops.conv_weight_prep16_pair(w)
+    a1, am1 = ops.conv_weight_prep16(w)
+    b1, bm1 = ops.conv_weight_prep16(w, transpose=True)
+    assert torch.equal(a, a1) and torch.equal(b, b1)
+    assert float(am.max()) == float(am1.max()) == float(w.abs().max())
