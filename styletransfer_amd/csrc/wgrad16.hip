@@ -115,8 +115,37 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
       t.br = buf_ld(rx, (bok && x0 + 8 < W) ? ob + 16u : BUF_OOB);
     }
   };
+  // Packed split: pairs of scaled values -> (hi, lo) fp16 pairs with 2-wide VALU
+  // (v_pk_mul/v_pk_add_f32, v_cvt_pkrtz_f16_f32: hi rounded toward zero, lo = v - hi
+  // exactly as before, so hi + lo keeps ~22 significant bits); the three kw-shifted B
+  // fragments reuse the packed pairs (kw = 0, 2) or one v_alignbit per dword (kw = 1).
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  auto split2 = [](f2 v, uint32_t& hi, uint32_t& lo) {
+    const auto h = __builtin_amdgcn_cvt_pkrtz(v.x, v.y);
+    hi = __builtin_bit_cast(uint32_t, h);
+    const f2 hf = {(float)h[0], (float)h[1]};
+    const f2 r = v - hf;
+    lo = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(r.x, r.y));
+  };
   auto compute = [&](const Step& t) {
-    float av[8] = {t.a0[0], t.a0[1], t.a0[2], t.a0[3], t.a1[0], t.a1[1], t.a1[2], t.a1[3]};
+    // A: dY rows co and co+32 (8 pixels each)
+    uint32_t ahs[2][4], als[2][4];
+    const f2 sd2 = {sd, sd};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f2 va = {q < 2 ? t.a0[2 * q] : t.a1[2 * q - 4], q < 2 ? t.a0[2 * q + 1] : t.a1[2 * q - 3]};
+      const f2 vc = {q < 2 ? t.c0[2 * q] : t.c1[2 * q - 4], q < 2 ? t.c0[2 * q + 1] : t.c1[2 * q - 3]};
+      split2(va * sd2, ahs[0][q], als[0][q]);
+      split2(vc * sd2, ahs[1][q], als[1][q]);
+    }
+    u4v ahu[2], alu[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ahu[i] = u4v{ahs[i][0], ahs[i][1], ahs[i][2], ahs[i][3]};
+      alu[i] = u4v{als[i][0], als[i][1], als[i][2], als[i][3]};
+    }
+    // B: V[ci] at x0-1 .. x0+8 (10 values) -> 5 packed pairs
     float bv[10];
     bv[0] = t.bl;
     bv[9] = t.br;
@@ -130,39 +159,41 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[1 + 2 * e] = bv[2 + 2 * e] = t.b0[e];
     }
-    float cv[8] = {t.c0[0], t.c0[1], t.c0[2], t.c0[3], t.c1[0], t.c1[1], t.c1[2], t.c1[3]};
-    h8 ah[2], al[2];
+    uint32_t ph[5], pl[5];
+    const f2 sv2 = {sv, sv};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float v = av[e] * sd, w2 = cv[e] * sd;
-      const _Float16 vh = (_Float16)v, wh = (_Float16)w2;
-      ah[0][e] = vh;
-      al[0][e] = (_Float16)(v - (float)vh);
-      ah[1][e] = wh;
-      al[1][e] = (_Float16)(w2 - (float)wh);
-    }
-    _Float16 bh[10], bl[10];
-#pragma unroll
-    for (int e = 0; e < 10; ++e) {
-      float v = bv[e];
-      if (relu) v = fmaxf(v, 0.f);
-      v *= sv;
-      bh[e] = (_Float16)v;
-      bl[e] = (_Float16)(v - (float)bh[e]);
+    for (int q = 0; q < 5; ++q) {
+      f2 v = {bv[2 * q], bv[2 * q + 1]};
+      if (relu) {
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+      }
+      split2(v * sv2, ph[q], pl[q]);
     }
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
-      h8 fh, fl;
+      uint32_t fh4[4], fl4[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        fh[e] = bh[e + kw];
-        fl[e] = bl[e + kw];
+      for (int q = 0; q < 4; ++q) {
+        if (kw == 0) {
+          fh4[q] = ph[q];
+          fl4[q] = pl[q];
+        } else if (kw == 2) {
+          fh4[q] = ph[q + 1];
+          fl4[q] = pl[q + 1];
+        } else {  // halves (2q+1, 2q+2)
+          fh4[q] = __builtin_amdgcn_alignbit(ph[q + 1], ph[q], 16);
+          fl4[q] = __builtin_amdgcn_alignbit(pl[q + 1], pl[q], 16);
+        }
       }
+      const u4v fhu = {fh4[0], fh4[1], fh4[2], fh4[3]}, flu = {fl4[0], fl4[1], fl4[2], fl4[3]};
+      const h8 fh = __builtin_bit_cast(h8, fhu), fl = __builtin_bit_cast(h8, flu);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], fh, acc[i][kw], 0, 0, 0);
-        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], fl, acc[i][kw], 0, 0, 0);
-        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], fh, acc[i][kw], 0, 0, 0);
+        const h8 ah = __builtin_bit_cast(h8, ahu[i]), al = __builtin_bit_cast(h8, alu[i]);
+        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, fh, acc[i][kw], 0, 0, 0);
+        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, fl, acc[i][kw], 0, 0, 0);
+        acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, fh, acc[i][kw], 0, 0, 0);
       }
     }
   };
