@@ -155,6 +155,15 @@ int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, int accumulat
                        int cin, int h, int w, int cout, int in_mode, int hv, int wv,
                        const float* x_amax, const float* dy_amax, void* ws, size_t ws_bytes,
                        void* stream);
+/* Weight gradient of the 3x3 stride-2 pad-1 downsampling convs of ImageTransformNet
+ * (stransfer/network.py:528-533; replaces the autograd conv2d weight gradient of
+ * static_train :690-765) on the fp16 hi/lo split MFMA: raw input x [n][cin][h][w]
+ * with h = 2 ho, w = 2 wo, dy [n][cout][ho][wo], wo % 16 == 0, cin / cout >= 16.
+ * Workspace: stx_conv2d_wgrad16_s2_ws (0 = unsupported shape). */
+size_t stx_conv2d_wgrad16_s2_ws(int n, int cin, int cout, int ho, int wo);
+int stx_conv2d_wgrad16_s2(const float* x, const float* dy, float* dw, int accumulate, int n,
+                          int cin, int h, int w, int cout, int ho, int wo, const float* x_amax,
+                          const float* dy_amax, void* ws, size_t ws_bytes, void* stream);
 
 /* dW of the ImageTransformNet 9x9 stride-1 pad-4 layers whose one side has 1..3
  * channels and the other 32 (conv0 3->32, conv22 32->3; stransfer/network.py:525-527,

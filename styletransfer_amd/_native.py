@@ -62,6 +62,9 @@ SIGNATURES = {
     "stx_conv2d_wgrad16_ws": (sz, [i32, i32, i32, i32, i32, i32]),
     "stx_conv2d_wgrad16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                  vp, sz, vp]),
+    "stx_conv2d_wgrad16_s2_ws": (sz, [i32, i32, i32, i32, i32]),
+    "stx_conv2d_wgrad16_s2": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                                    vp, sz, vp]),
     "stx_conv2d_wgrad_few16_ws": (sz, [i32, i32, i32, i32, i32, i32]),
     "stx_conv2d_wgrad_few16": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                      vp, sz, vp]),

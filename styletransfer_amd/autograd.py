@@ -58,6 +58,8 @@ class Conv2dFn(torch.autograd.Function):
                 x_amax = ops.amax(x)
         elif wt is None:
             wt = ops.conv_weight_prep(w.detach().contiguous())
+            if stride == 2 and _split_on() and w.requires_grad:
+                x_amax = ops.ARENA.lookup(x)  # for the split stride-2 wgrad (None: computed there)
         y = ops.conv2d(x, wt, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
                        bias=None if b is None else b.detach(), wt16=wt16 if split else None,
                        in_amax=x_amax)
@@ -78,7 +80,7 @@ class Conv2dFn(torch.autograd.Function):
         dy_amax = None
         split_d = stride == 1 and _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1)
         if (split_d and ctx.needs_input_grad[0]) or (ctx.needs_input_grad[1] and _split_on() and (
-                (ks == 3 and stride == 1 and pad == 1) or ks == 9)):
+                (ks == 3 and stride in (1, 2) and pad == 1) or ks == 9)):
             dy_amax = ops.ARENA.lookup(dy)
             if dy_amax is None:
                 dy_amax = ops.amax(dy)

@@ -17,6 +17,11 @@
 //
 // Reference: autograd of the ImageTransformNet 3x3 convs trained by static_train
 // (stransfer/network.py:468-481, 525-609, :690-765).
+//
+// S2 (the stride-2 downsampling convs, stransfer/network.py:528-533): the same
+// (32 couts, 32 cins, kh) units over output pixels; the lane loads 16 consecutive
+// input pixels 2*x0 .. 2*x0+15 (four float4) plus 2*x0-1 and takes the even ones
+// (kw = 1) and the odd ones shifted by zero / one (kw = 0 / 2) as packed pairs.
 #include "common.h"
 #include "../../include/stx.h"
 
@@ -36,7 +41,9 @@ struct Wg16 {
   int cout32, cin32;
 };
 
-template <int PF>
+constexpr int WG16_S2 = 16;  // private mode: stride 2, pad 1, raw input (h = 2 hv, w = 2 wv)
+
+template <int PF, bool S2>
 __global__ void __launch_bounds__(256)
 wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ ws,
                const float* __restrict__ x_amax, const float* __restrict__ dy_amax, Wg16 g) {
@@ -76,6 +83,7 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
     f32x4 c0, c1;   // dY[co+32][y][x0+8h .. +7]
     f32x4 b0, b1;   // V[ci][vy][x0+8h .. +7] (b1 unused for the upsample loader)
     float bl, br;   // V at x0+8h-1 and x0+8h+8
+    f32x4 b2, b3;   // S2: x[ci][2y+kh-1][2x0+8 .. +15] (b0/b1: 2x0 .. 2x0+7; bl: 2x0-1)
   };
   // running (image, row, 16-pixel column step) of the next load: loads are issued in
   // step order, so no integer division per step
@@ -98,6 +106,17 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
     const uint32_t oc = oa + (uint32_t)32 * H * W * 4u;
     t.c0 = buf_ld4(rdy, co2_ok ? oc : BUF_OOB);
     t.c1 = buf_ld4(rdy, co2_ok ? oc + 16u : BUF_OOB);
+    if constexpr (S2) {
+      const int vy = 2 * y + kh - 1;
+      const bool bok = ci_ok && vy >= 0 && vy < g.h;
+      const uint32_t ob = (uint32_t)((((size_t)n * g.cin + ci) * g.h + vy) * g.w + 2 * x0) * 4u;
+      t.b0 = buf_ld4(rx, bok ? ob : BUF_OOB);
+      t.b1 = buf_ld4(rx, bok ? ob + 16u : BUF_OOB);
+      t.b2 = buf_ld4(rx, bok ? ob + 32u : BUF_OOB);
+      t.b3 = buf_ld4(rx, bok ? ob + 48u : BUF_OOB);
+      t.bl = buf_ld(rx, (bok && x0 > 0) ? ob - 4u : BUF_OOB);
+      return;
+    }
     const int vy = y + kh - 1;
     const bool bok = ci_ok && vy >= 0 && vy < H;
     if (!up) {
@@ -144,6 +163,52 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
     for (int i = 0; i < 2; ++i) {
       ahu[i] = u4v{ahs[i][0], ahs[i][1], ahs[i][2], ahs[i][3]};
       alu[i] = u4v{als[i][0], als[i][1], als[i][2], als[i][3]};
+    }
+    if constexpr (S2) {
+      // even inputs 2(x0+e) -> kw = 1; odd sequence o = [2x0-1, 2x0+1, .., 2x0+15]:
+      // o[0..7] -> kw = 0, o[1..8] -> kw = 2 (one v_alignbit per dword)
+      const float xs[16] = {t.b0[0], t.b0[1], t.b0[2], t.b0[3], t.b1[0], t.b1[1], t.b1[2], t.b1[3],
+                            t.b2[0], t.b2[1], t.b2[2], t.b2[3], t.b3[0], t.b3[1], t.b3[2], t.b3[3]};
+      const float od[10] = {t.bl, xs[1], xs[3], xs[5], xs[7], xs[9], xs[11], xs[13], xs[15], 0.f};
+      uint32_t eh[4], el[4], oh[5], ol[5];
+      const f2 sv2 = {sv, sv};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f2 v = {xs[4 * q], xs[4 * q + 2]};
+        split2(v * sv2, eh[q], el[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const f2 v = {od[2 * q], od[2 * q + 1]};
+        split2(v * sv2, oh[q], ol[q]);
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        uint32_t fh4[4], fl4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (kw == 0) {
+            fh4[q] = oh[q];
+            fl4[q] = ol[q];
+          } else if (kw == 1) {
+            fh4[q] = eh[q];
+            fl4[q] = el[q];
+          } else {
+            fh4[q] = __builtin_amdgcn_alignbit(oh[q + 1], oh[q], 16);
+            fl4[q] = __builtin_amdgcn_alignbit(ol[q + 1], ol[q], 16);
+          }
+        }
+        const u4v fhu = {fh4[0], fh4[1], fh4[2], fh4[3]}, flu = {fl4[0], fl4[1], fl4[2], fl4[3]};
+        const h8 fh = __builtin_bit_cast(h8, fhu), fl = __builtin_bit_cast(h8, flu);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const h8 ah = __builtin_bit_cast(h8, ahu[i]), al = __builtin_bit_cast(h8, alu[i]);
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, fh, acc[i][kw], 0, 0, 0);
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, fl, acc[i][kw], 0, 0, 0);
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, fh, acc[i][kw], 0, 0, 0);
+        }
+      }
+      return;
     }
     // B: V[ci] at x0-1 .. x0+8 (10 values) -> 5 packed pairs
     float bv[10];
@@ -264,7 +329,9 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   if (wv % 16 != 0 || cin < 16 || cout < 16 || n <= 0 || hv <= 0) return false;
   // 32-bit buffer offsets over the whole dy / x tensors
   if ((size_t)n * std::max(cin, cout) * hv * wv * 4 >= (1ull << 31)) return false;
-  if (in_mode != STX_IN_RAW && in_mode != STX_IN_RELU && in_mode != STX_IN_UPSAMPLE2) return false;
+  if (in_mode != STX_IN_RAW && in_mode != STX_IN_RELU && in_mode != STX_IN_UPSAMPLE2 &&
+      in_mode != WG16_S2)
+    return false;
   g.n = n;
   g.cin = cin;
   g.cout = cout;
@@ -312,7 +379,8 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
   g.h = h;
   g.w = w;
   if ((in_mode == STX_IN_UPSAMPLE2 && (hv != 2 * h || wv != 2 * w)) ||
-      (in_mode != STX_IN_UPSAMPLE2 && (hv != h || wv != w))) {
+      (in_mode == WG16_S2 && (h != 2 * hv || w != 2 * wv)) ||
+      (in_mode != STX_IN_UPSAMPLE2 && in_mode != WG16_S2 && (hv != h || wv != w))) {
     set_error("stx_conv2d_wgrad16: virtual dims do not match the input mode");
     return STX_E_INVALID;
   }
@@ -331,18 +399,33 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
     const char* e = getenv("STX_WG16_PF");
     return e ? atoi(e) : 4;
   }();
-  if (pf >= 12)
-    hipLaunchKernelGGL(wgrad16_kernel<12>, dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
+  if (g.mode == WG16_S2)
+    hipLaunchKernelGGL((wgrad16_kernel<4, true>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
+                       (float*)ws, x_amax, dy_amax, g);
+  else if (pf >= 12)
+    hipLaunchKernelGGL((wgrad16_kernel<12, false>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
                        (float*)ws, x_amax, dy_amax, g);
   else if (pf >= 8)
-    hipLaunchKernelGGL(wgrad16_kernel<8>, dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
+    hipLaunchKernelGGL((wgrad16_kernel<8, false>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
                        (float*)ws, x_amax, dy_amax, g);
   else
-    hipLaunchKernelGGL(wgrad16_kernel<4>, dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
+    hipLaunchKernelGGL((wgrad16_kernel<4, false>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
                        (float*)ws, x_amax, dy_amax, g);
   const long long total = (long long)cout * cin * 9;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(wgrad16_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, dw,
                      g, accumulate);
   return check_launch("stx_conv2d_wgrad16");
+}
+
+extern "C" size_t stx_conv2d_wgrad16_s2_ws(int n, int cin, int cout, int ho, int wo) {
+  return stx_conv2d_wgrad16_ws(n, cin, cout, WG16_S2, ho, wo);
+}
+
+extern "C" int stx_conv2d_wgrad16_s2(const float* x, const float* dy, float* dw, int accumulate,
+                                     int n, int cin, int h, int w, int cout, int ho, int wo,
+                                     const float* x_amax, const float* dy_amax, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  return stx_conv2d_wgrad16(x, dy, dw, accumulate, n, cin, h, w, cout, WG16_S2, ho, wo, x_amax,
+                            dy_amax, ws, ws_bytes, stream);
 }

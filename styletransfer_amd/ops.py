@@ -263,8 +263,8 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
 
 def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, dw=None,
                  accumulate=False, split=True, x_amax=None, dy_amax=None):
-    """dW (+)= sum dy * V(x); 3x3 stride-1 shapes run on the fp16 hi/lo split MFMA
-    (stx_conv2d_wgrad16) unless split=False or STX_CONV_SPLIT=0."""
+    """dW (+)= sum dy * V(x); 3x3 stride-1 / stride-2 shapes run on the fp16 hi/lo split
+    MFMA (stx_conv2d_wgrad16[_s2]) unless split=False or STX_CONV_SPLIT=0."""
     _req(x, "x")
     _req(dy, "dy")
     n, _, h, w = x.shape
@@ -300,6 +300,19 @@ def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW,
                                        int(accumulate), n, cin, h, w, cout, in_mode, ho, wo,
                                        xa.data_ptr(), da.data_ptr(), wp, wn, _stream()),
                   "stx_conv2d_wgrad16")
+            return dw
+    if split and ks == 3 and stride == 2 and pad == 1 and in_mode == N.STX_IN_RAW \
+            and os.environ.get("STX_WG16_S2", "1") != "0" \
+            and h == 2 * ho and w == 2 * wo:
+        need16 = L.stx_conv2d_wgrad16_s2_ws(n, cin, cout, ho, wo)
+        if need16:
+            xa = x_amax if x_amax is not None else amax(x)
+            da = dy_amax if dy_amax is not None else amax(dy)
+            wp, wn = WS.get(need16, x.device)
+            check(L.stx_conv2d_wgrad16_s2(x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
+                                          int(accumulate), n, cin, h, w, cout, ho, wo,
+                                          xa.data_ptr(), da.data_ptr(), wp, wn, _stream()),
+                  "stx_conv2d_wgrad16_s2")
             return dw
     need = L.stx_conv2d_wgrad_ws(n, cin, cout, ks, stride, ho, wo)
     wp, wn = WS.get(need, x.device)

@@ -268,6 +268,23 @@ def test_split_wgrad(dev, case):
     assert rel(acc, 2 * ref) < TOL64
 
 
+@pytest.mark.parametrize("case", [(2, 32, 64, 32, 64), (3, 24, 40, 18, 32), (1, 64, 128, 8, 128)])
+def test_split_wgrad_stride2(dev, case):
+    """3x3 stride-2 weight gradient (ITN downsampling convs, wgrad16 S2) vs fp64."""
+    n, cin, cout, h, w = case
+    x = rnd(n, cin, h, w, dev=dev, seed=64, scale=2, shift=-1)
+    wgt = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x.double().cpu(), wgt, stride=2, padding=1)
+    assert N.lib().stx_conv2d_wgrad16_s2_ws(n, cin, cout, y.shape[2], y.shape[3]) > 0
+    dy = rnd(*y.shape, dev=dev, seed=65, scale=2e-3, shift=-1e-3)
+    (ref,) = torch.autograd.grad(y, wgt, dy.double().cpu())
+    dw16 = ops.conv2d_wgrad(x, dy, cin, cout, 3, stride=2)
+    assert rel(dw16, ref) < TOL64, rel(dw16, ref)
+    acc = dw16.clone()
+    ops.conv2d_wgrad(x, dy, cin, cout, 3, stride=2, dw=acc, accumulate=True)
+    assert rel(acc, 2 * ref) < TOL64
+
+
 @pytest.mark.parametrize("case", [(2, 3, 32, 64, 64), (2, 32, 3, 48, 80), (1, 1, 32, 20, 272),
                                   (3, 32, 2, 9, 16)])
 def test_split_wgrad_9x9_few(dev, case):
