@@ -97,6 +97,14 @@ class AmaxArena:
         self.i += 1
         return g
 
+    def take_span(self, k, device):
+        """k consecutive zeroed groups as one flat slot vector (vgg.slot layout)."""
+        if not self.active or self.i + k > self.groups or self.buf.device != device:
+            return None
+        g = self.buf[self.i:self.i + k].view(-1)
+        self.i += k
+        return g
+
     def annotate(self, t, g):
         if g is not None:
             t._stx_amax = (g, self.epoch)

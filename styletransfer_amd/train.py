@@ -76,7 +76,7 @@ class FastStTrainer:
 
     def _total(self, batch, y):
         with torch.no_grad():
-            c4 = V.content_target(self.feat, batch)
+            c4 = V.content_target(self.feat, batch, amax=ops.ARENA.take_span(5, batch.device))
         losses = A.VGGLossFn.apply(y, c4, self.feat, self.targets, False)  # feature loss unused
         tv = A.TVLossFn.apply(y, self.tv)
         w = self.world

@@ -343,10 +343,12 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
     return feat.dgrad(0, dz1, dx)
 
 
-def content_target(feat: VGGFeatures, content, out=None):
-    """C4 = conv2_2 output of the content image (ContentLoss target, pre-ReLU)."""
-    return feat.forward(content.contiguous(), 4)[3] if out is None else \
-        feat.forward(content.contiguous(), 4, [None, None, None, out])[3]
+def content_target(feat: VGGFeatures, content, out=None, amax=None):
+    """C4 = conv2_2 output of the content image (ContentLoss target, pre-ReLU).
+    amax: optional zeroed slot vector (>= 5 groups): each conv then emits its output's
+    max|.| for the next split conv instead of that conv re-reading its input."""
+    return feat.forward(content.contiguous(), 4, amax=amax)[3] if out is None else \
+        feat.forward(content.contiguous(), 4, [None, None, None, out], amax=amax)[3]
 
 
 class GatysEngine:

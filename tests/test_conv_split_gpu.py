@@ -46,6 +46,10 @@ CASES = [
     (2, 128, 128, 16, 16, N.STX_IN_RAW),
     (1, 20, 70, 33, 17, N.STX_IN_RAW),       # cin, cout not tile multiples
     (1, 16, 5, 9, 67, N.STX_IN_RELU),        # smallest eligible cout, ragged width
+    # small grids with cout % 128 == 0: 128 x 128 blocks (WM = 2), ragged and exact
+    (2, 128, 128, 18, 70, N.STX_IN_RAW),
+    (2, 64, 256, 32, 64, N.STX_IN_RAW),
+    (2, 128, 128, 64, 64, N.STX_IN_RAW),     # ITN residual conv shape
 ]
 
 

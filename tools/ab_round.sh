@@ -1,5 +1,6 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 120 python tools/bench_conv.py --only "wgrad" || exit 1
-for v in 1 0 1 0; do echo "fast S2=$v $(STX_WG16_S2=$v timeout -k 10 200 python bench.py --fast-only --steps 20 --warmup 3 2>/dev/null)"; done
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -30 gpurun_out/t.log; exit 1; }
+tail -2 gpurun_out/t.log
+for v in 1 2 3; do echo "fast $(timeout -k 10 200 python bench.py --fast-only --steps 20 --warmup 3 2>/dev/null)"; done
