@@ -640,8 +640,8 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   }
   // fp16 hi/lo split MFMA path (conv16.hip) for the 3x3 stride-1 layers it covers;
   // other shapes keep the fp32 MFMA kernels (wt is always required)
-  if (p.wt16 && p.ks == 3 && p.stride == 1 && p.pad == 1 && p.cout > 4 && p.cin >= 16 &&
-      p.wt_batch_stride == 0) {
+  if (p.wt16 && p.ks == 3 && p.pad == 1 && p.cout > 4 && p.cin >= 16 &&
+      (p.stride == 1 || (p.stride == 2 && p.in_mode == STX_IN_RAW)) && p.wt_batch_stride == 0) {
     if (!p.w_amax || !p.in_amax || (p.p2_z && !p.p2_amax)) {
       set_error("stx_conv2d: the wt16 path needs w_amax, in_amax (and p2_amax with p2_z)");
       return STX_E_INVALID;

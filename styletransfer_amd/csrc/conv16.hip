@@ -231,10 +231,15 @@ __device__ __forceinline__ void phase2_f16(f32x16 (&acc)[2][2], const stx_conv_p
       for (int r = 0; r < 16; ++r) acc[i][j][r] *= down;
 }
 
-template <int TW, int NI>
+// S = 2: the stride-2 downsampling convs (raw input, loader mode LM_S2): the tile's
+// input window is (2 TH + 1) x (2 TW + 1) and output pixel (ty, tx) reads its taps at
+// window position (2 ty + kh, 2 tx + kw)
+constexpr int LM_S2 = 16;
+
+template <int TW, int NI, int S = 1>
 struct C16 {
   static constexpr int BM = 64, NPIX = 128 * NI, TH = NPIX / TW;
-  static constexpr int RH = TH + 2, RW = TW + 2, NPOS = RH * RW;
+  static constexpr int RH = S * (TH - 1) + 3, RW = S * (TW - 1) + 3, NPOS = RH * RW;
   static constexpr int NITEM = 2 * NPOS;                   // (channel group, position)
   static constexpr int NIT = (NITEM + 255) / 256;          // items per thread
   static constexpr int NITP = NIT * 256;                   // padded: stores unconditional
@@ -252,8 +257,9 @@ struct C16 {
 template <int TW, int LM, int DBG = 0, int P2 = 0, int NI = 2>
 __global__ void __launch_bounds__(256, 2)
 conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
-  using C = C16<TW, NI>;
-  constexpr bool RP = TW == 64 && NI == 2;  // row-pair tiles (fused pool / unpool)
+  constexpr int S = LM == LM_S2 ? 2 : 1;
+  using C = C16<TW, NI, S>;
+  constexpr bool RP = TW == 64 && NI == 2 && S == 1;  // row-pair tiles (fused pool / unpool)
   static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
   constexpr int BM = C::BM;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
@@ -277,7 +283,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
 
   const int plane_in = p.h * p.w;
   const float* __restrict__ xn = p.x + (size_t)n * p.cin * plane_in;
-  const int vy0 = ty0 - 1, vx0 = tx0 - 1;
+  const int vy0 = S * ty0 - 1, vx0 = S * tx0 - 1;
 
   // chunk-invariant byte offsets of channel 0 of each halo item (BUF_OOB = zero pad)
   uint32_t hoff[C::NIT];
@@ -374,7 +380,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
   for (int j = 0; j < NI; ++j) {
     int ty, tx;
     tile_pix<TW, RP, NI>(wave, j, l32, ty, tx);
-    bbase[j] = lds_h + (h * C::NPOS + ty * C::RW + tx) * 16;
+    bbase[j] = lds_h + (h * C::NPOS + S * ty * C::RW + S * tx) * 16;
   }
   const char* abase = lds_w + (h * BM + l32) * 16;
 
@@ -504,7 +510,7 @@ static int dbg_mode() {
 
 template <int TW, int LM, int NI>
 static int launch16(const stx_conv_params& p, hipStream_t st) {
-  using C = C16<TW, NI>;
+  using C = C16<TW, NI, LM == LM_S2 ? 2 : 1>;
   const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
   dim3 grid(tiles_x * tiles_y, cdiv(p.cout, C::BM), p.n);
   if constexpr (TW == 64 && LM == STX_IN_RELU && NI == 2) {
@@ -680,11 +686,17 @@ __global__ void __launch_bounds__(1024) amax_slots_kernel(const float* __restric
 }
 
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st) {
-  switch (p.in_mode) {
+  switch (p.stride == 2 ? LM_S2 : p.in_mode) {
     case STX_IN_RAW: return dispatch16_tw<STX_IN_RAW>(p, st);
     case STX_IN_RELU: return dispatch16_tw<STX_IN_RELU>(p, st);
     case STX_IN_RELU_POOL2: return dispatch16_tw<STX_IN_RELU_POOL2>(p, st);
     case STX_IN_UPSAMPLE2: return dispatch16_tw<STX_IN_UPSAMPLE2>(p, st);
+    case LM_S2:  // stride 2 (raw input): 32 x 4 output tiles, two blocks per CU
+      if (p.pool_out || p.p2_z) {
+        set_error("stx_conv2d: stride 2 takes no fused pool output / Gram phase");
+        return STX_E_INVALID;
+      }
+      return launch16<32, LM_S2, 1>(p, st);
     default: return dispatch16_tw<STX_IN_DILATE2>(p, st);
   }
 }

@@ -9,6 +9,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import os
+
 import torch
 
 from . import _native as N
@@ -171,9 +173,14 @@ def conv_weight_prep16_pair(w: torch.Tensor):
     return (wt16, w_amax), (wtT16, w_amax)
 
 
+_S2_FWD = os.environ.get("STX_S2_FWD", "1") != "0"
+
+
 def split_eligible(cin, cout, ks, stride=1):
     """Shapes stx_conv2d runs on the fp16 hi/lo split MFMA kernel (conv16.hip)."""
-    return ks == 3 and stride == 1 and cin >= 16 and cout > 4
+    # stride 2 (raw input only): STX_S2_FWD=0 keeps it on the fp32 kernel (A/B switch)
+    return ks == 3 and cin >= 16 and cout > 4 and (
+        stride == 1 or (stride == 2 and _S2_FWD))
 
 
 def amax(x: torch.Tensor, out=None):

@@ -73,6 +73,32 @@ def test_split_conv_fwd(dev, case):
     assert float(amax.max()) == float(y.abs().max())
 
 
+@pytest.mark.parametrize("case", [(2, 32, 64, 64, 64), (1, 64, 128, 34, 70), (3, 16, 24, 9, 13),
+                                  (8, 32, 64, 256, 256)])
+def test_split_conv_stride2(dev, case):
+    """3x3 stride-2 pad-1 forward (ITN downsampling convs, loader mode LM_S2) vs fp64,
+    ragged output tiles included; out_amax is the exact max|y|."""
+    n, cin, cout, h, w = case
+    x = rnd(n, cin, h, w, dev=dev, seed=7, scale=2, shift=-1)
+    wgt = rnd(cout, cin, 3, 3, dev=dev, seed=8, scale=0.2, shift=-0.1)
+    b = rnd(cout, dev=dev, seed=9)
+    assert ops.split_eligible(cin, cout, 3, 2)
+    wt = ops.conv_weight_prep(wgt)
+    w16 = ops.conv_weight_prep16(wgt)
+    amax = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    y = ops.conv2d(x, wt, cin, cout, 3, stride=2, bias=b, wt16=w16, out_amax=amax)
+    y32 = ops.conv2d(x, wt, cin, cout, 3, stride=2, bias=b)
+    if n * h * w > 100_000:  # the ITN shape: against the fp32 MFMA kernel (no fp64 conv)
+        assert rel(y, y32) < 1e-5
+    else:
+        ref = F.conv2d(x.double().cpu(), wgt.double().cpu(), b.double().cpu(), stride=2,
+                       padding=1)
+        assert y.shape == ref.shape
+        assert rel(y, ref) < TOL64, (rel(y, ref), rel(y32, ref))
+    torch.cuda.synchronize()
+    assert float(amax.max()) == float(y.abs().max())
+
+
 @pytest.mark.parametrize("scale", [1e-9, 1.0, 3e4])
 def test_split_conv_scales(dev, scale):
     """Per-tensor power-of-two scaling: tiny and large inputs keep fp32 accuracy."""
