@@ -39,11 +39,12 @@ struct Wg16 {
   int n, cin, h, w, cout, mode, hv, wv;  // x physical [n][cin][h][w]; V/dY are hv x wv
   int ncot, ncit, nsplit, steps, steps_per_split;
   int cout32, cin32;
+  int ci2;  // cout <= 32: a wave takes 32 couts x 64 cins (two cin tiles), not 64 x 32
 };
 
 constexpr int WG16_S2 = 16;  // private mode: stride 2, pad 1, raw input (h = 2 hv, w = 2 wv)
 
-template <int PF, bool S2>
+template <int PF, bool S2, bool CI2 = false>
 __global__ void __launch_bounds__(256)
 wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ ws,
                const float* __restrict__ x_amax, const float* __restrict__ dy_amax, Wg16 g) {
@@ -62,8 +63,9 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
   const float sv = __builtin_ldexpf(1.f, 15 - ex), sd = __builtin_ldexpf(1.f, 15 - ed);
   const float descale = __builtin_ldexpf(1.f, ex + ed - 30);
 
-  const int co = cot * 64 + l32, ci = cit * 32 + l32;
+  const int co = cot * (CI2 ? 32 : 64) + l32, ci = cit * (CI2 ? 64 : 32) + l32;
   const bool co_ok = co < g.cout, co2_ok = co + 32 < g.cout, ci_ok = ci < g.cin;
+  const bool ci2_ok = ci + 32 < g.cin;
   const int H = g.hv, W = g.wv, wsteps = W / 16;
   const bool relu = g.mode == STX_IN_RELU, up = g.mode == STX_IN_UPSAMPLE2;
 
@@ -84,6 +86,7 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
     f32x4 b0, b1;   // V[ci][vy][x0+8h .. +7] (b1 unused for the upsample loader)
     float bl, br;   // V at x0+8h-1 and x0+8h+8
     f32x4 b2, b3;   // S2: x[ci][2y+kh-1][2x0+8 .. +15] (b0/b1: 2x0 .. 2x0+7; bl: 2x0-1)
+    float bl2, br2; // CI2: neighbours of the second cin row (c0/c1 hold its 8 pixels)
   };
   // running (image, row, 16-pixel column step) of the next load: loads are issued in
   // step order, so no integer division per step
@@ -103,9 +106,11 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
     const uint32_t oa = (uint32_t)((((size_t)n * g.cout + co) * H + y) * W + x0) * 4u;
     t.a0 = buf_ld4(rdy, co_ok ? oa : BUF_OOB);
     t.a1 = buf_ld4(rdy, co_ok ? oa + 16u : BUF_OOB);
-    const uint32_t oc = oa + (uint32_t)32 * H * W * 4u;
-    t.c0 = buf_ld4(rdy, co2_ok ? oc : BUF_OOB);
-    t.c1 = buf_ld4(rdy, co2_ok ? oc + 16u : BUF_OOB);
+    if constexpr (!CI2) {
+      const uint32_t oc = oa + (uint32_t)32 * H * W * 4u;
+      t.c0 = buf_ld4(rdy, co2_ok ? oc : BUF_OOB);
+      t.c1 = buf_ld4(rdy, co2_ok ? oc + 16u : BUF_OOB);
+    }
     if constexpr (S2) {
       const int vy = 2 * y + kh - 1;
       const bool bok = ci_ok && vy >= 0 && vy < g.h;
@@ -125,6 +130,14 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
       t.b1 = buf_ld4(rx, bok ? ob + 16u : BUF_OOB);
       t.bl = buf_ld(rx, (bok && x0 > 0) ? ob - 4u : BUF_OOB);
       t.br = buf_ld(rx, (bok && x0 + 8 < W) ? ob + 32u : BUF_OOB);
+      if constexpr (CI2) {  // the same row of cin + 32
+        const bool bok2 = ci2_ok && vy >= 0 && vy < H;
+        const uint32_t ob2 = ob + (uint32_t)32 * g.h * g.w * 4u;
+        t.c0 = buf_ld4(rx, bok2 ? ob2 : BUF_OOB);
+        t.c1 = buf_ld4(rx, bok2 ? ob2 + 16u : BUF_OOB);
+        t.bl2 = buf_ld(rx, (bok2 && x0 > 0) ? ob2 - 4u : BUF_OOB);
+        t.br2 = buf_ld(rx, (bok2 && x0 + 8 < W) ? ob2 + 32u : BUF_OOB);
+      }
     } else {  // V[vy][vx] = x[vy/2][vx/2]; x0 is even
       const uint32_t ob =
           (uint32_t)((((size_t)n * g.cin + ci) * g.h + (vy >> 1)) * g.w + (x0 >> 1)) * 4u;
@@ -132,6 +145,14 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
       t.b1 = zero4;
       t.bl = buf_ld(rx, (bok && x0 > 0) ? ob - 4u : BUF_OOB);
       t.br = buf_ld(rx, (bok && x0 + 8 < W) ? ob + 16u : BUF_OOB);
+      if constexpr (CI2) {
+        const bool bok2 = ci2_ok && vy >= 0 && vy < H;
+        const uint32_t ob2 = ob + (uint32_t)32 * g.h * g.w * 4u;
+        t.c0 = buf_ld4(rx, bok2 ? ob2 : BUF_OOB);
+        t.c1 = zero4;
+        t.bl2 = buf_ld(rx, (bok2 && x0 > 0) ? ob2 - 4u : BUF_OOB);
+        t.br2 = buf_ld(rx, (bok2 && x0 + 8 < W) ? ob2 + 16u : BUF_OOB);
+      }
     }
   };
   // Packed split: pairs of scaled values -> (hi, lo) fp16 pairs with 2-wide VALU
@@ -156,7 +177,8 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
       const f2 va = {q < 2 ? t.a0[2 * q] : t.a1[2 * q - 4], q < 2 ? t.a0[2 * q + 1] : t.a1[2 * q - 3]};
       const f2 vc = {q < 2 ? t.c0[2 * q] : t.c1[2 * q - 4], q < 2 ? t.c0[2 * q + 1] : t.c1[2 * q - 3]};
       split2(va * sd2, ahs[0][q], als[0][q]);
-      split2(vc * sd2, ahs[1][q], als[1][q]);
+      if constexpr (!CI2) split2(vc * sd2, ahs[1][q], als[1][q]);
+      else ahs[1][q] = als[1][q] = 0u;
     }
     u4v ahu[2], alu[2];
 #pragma unroll
@@ -211,32 +233,34 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
       return;
     }
     // B: V[ci] at x0-1 .. x0+8 (10 values) -> 5 packed pairs
-    float bv[10];
-    bv[0] = t.bl;
-    bv[9] = t.br;
-    if (!up) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        bv[1 + e] = t.b0[e];
-        bv[5 + e] = t.b1[e];
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bv[1 + 2 * e] = bv[2 + 2 * e] = t.b0[e];
-    }
-    uint32_t ph[5], pl[5];
     const f2 sv2 = {sv, sv};
+    auto bpairs = [&](const f32x4& b0, const f32x4& b1, float bl, float br, uint32_t (&ph)[5],
+                      uint32_t (&pl)[5]) {
+      float bv[10];
+      bv[0] = bl;
+      bv[9] = br;
+      if (!up) {
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      f2 v = {bv[2 * q], bv[2 * q + 1]};
-      if (relu) {
-        v.x = fmaxf(v.x, 0.f);
-        v.y = fmaxf(v.y, 0.f);
+        for (int e = 0; e < 4; ++e) {
+          bv[1 + e] = b0[e];
+          bv[5 + e] = b1[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[1 + 2 * e] = bv[2 + 2 * e] = b0[e];
       }
-      split2(v * sv2, ph[q], pl[q]);
-    }
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
+      for (int q = 0; q < 5; ++q) {
+        f2 v = {bv[2 * q], bv[2 * q + 1]};
+        if (relu) {
+          v.x = fmaxf(v.x, 0.f);
+          v.y = fmaxf(v.y, 0.f);
+        }
+        split2(v * sv2, ph[q], pl[q]);
+      }
+    };
+    // kw-shifted fragments: kw = 0, 2 reuse the pairs, kw = 1 takes halves (2q+1, 2q+2)
+    auto kwfrag = [&](const uint32_t (&ph)[5], const uint32_t (&pl)[5], int kw, h8& fh, h8& fl) {
       uint32_t fh4[4], fl4[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -246,13 +270,38 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
         } else if (kw == 2) {
           fh4[q] = ph[q + 1];
           fl4[q] = pl[q + 1];
-        } else {  // halves (2q+1, 2q+2)
+        } else {
           fh4[q] = __builtin_amdgcn_alignbit(ph[q + 1], ph[q], 16);
           fl4[q] = __builtin_amdgcn_alignbit(pl[q + 1], pl[q], 16);
         }
       }
       const u4v fhu = {fh4[0], fh4[1], fh4[2], fh4[3]}, flu = {fl4[0], fl4[1], fl4[2], fl4[3]};
-      const h8 fh = __builtin_bit_cast(h8, fhu), fl = __builtin_bit_cast(h8, flu);
+      fh = __builtin_bit_cast(h8, fhu);
+      fl = __builtin_bit_cast(h8, flu);
+    };
+    if constexpr (CI2) {  // one dY row against two cin rows: acc[cin tile][kw]
+      uint32_t ph[2][5], pl[2][5];
+      bpairs(t.b0, t.b1, t.bl, t.br, ph[0], pl[0]);
+      bpairs(t.c0, t.c1, t.bl2, t.br2, ph[1], pl[1]);
+      const h8 ah = __builtin_bit_cast(h8, ahu[0]), al = __builtin_bit_cast(h8, alu[0]);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          h8 fh, fl;
+          kwfrag(ph[i], pl[i], kw, fh, fl);
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, fh, acc[i][kw], 0, 0, 0);
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, fl, acc[i][kw], 0, 0, 0);
+          acc[i][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, fh, acc[i][kw], 0, 0, 0);
+        }
+      return;
+    }
+    uint32_t ph[5], pl[5];
+    bpairs(t.b0, t.b1, t.bl, t.br, ph, pl);
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      h8 fh, fl;
+      kwfrag(ph, pl, kw, fh, fl);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const h8 ah = __builtin_bit_cast(h8, ahu[i]), al = __builtin_bit_cast(h8, alu[i]);
@@ -290,8 +339,9 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
-      float* out = ws + (((size_t)split * 9 + kh * 3 + kw) * g.cout32 + cot * 64 + i * 32) *
-                            g.cin32 + cit * 32 + l32;
+      const int orow = CI2 ? cot * 32 : cot * 64 + i * 32;
+      const int ocol = CI2 ? cit * 64 + i * 32 : cit * 32;
+      float* out = ws + (((size_t)split * 9 + kh * 3 + kw) * g.cout32 + orow) * g.cin32 + ocol + l32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -325,6 +375,47 @@ __global__ void wgrad16_reduce_kernel(const float* __restrict__ ws, float* __res
   }
 }
 
+// Small outputs with many splits (the cout <= 64 layers: < 512 blocks of the kernel
+// above, latency-bound): 4 thread groups per output each sum a contiguous quarter of
+// the splits (8 running sums), combined in LDS as (q0 + q1) + (q2 + q3) -- fixed order
+__global__ void __launch_bounds__(256)
+wgrad16_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg16 g,
+                       int accumulate) {
+  __shared__ float part[4][64];
+  const long long per = (long long)g.cout * g.cin;
+  const long long total = per * 9;
+  const int q = threadIdx.x >> 6;
+  const long long i = blockIdx.x * 64ll + (threadIdx.x & 63);
+  float s = 0.f;
+  int tap = 0, co = 0, ci = 0;
+  if (i < total) {
+    tap = (int)(i / per);
+    const long long rem = i - tap * per;
+    co = (int)(rem / g.cin);
+    ci = (int)(rem - (long long)co * g.cin);
+    const size_t sstride = (size_t)9 * g.cout32 * g.cin32;
+    const float* src = ws + ((size_t)tap * g.cout32 + co) * g.cin32 + ci;
+    const int quarter = (g.nsplit + 3) / 4;
+    const int k0 = q * quarter, k1 = min(g.nsplit, k0 + quarter);
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int k = k0;
+    for (; k + 7 < k1; k += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += src[(size_t)(k + u) * sstride];
+    }
+    for (int u = 0; k < k1; ++k, ++u) a[u] += src[(size_t)k * sstride];
+    s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  }
+  part[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && i < total) {
+    const int j = threadIdx.x;
+    const float t = (part[0][j] + part[1][j]) + (part[2][j] + part[3][j]);
+    float* d = dw + ((size_t)co * g.cin + ci) * 9 + tap;
+    *d = accumulate ? *d + t : t;
+  }
+}
+
 static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg16& g) {
   if (wv % 16 != 0 || cin < 16 || cout < 16 || n <= 0 || hv <= 0) return false;
   // 32-bit buffer offsets over the whole dy / x tensors
@@ -338,10 +429,22 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   g.mode = in_mode;
   g.hv = hv;
   g.wv = wv;
-  g.ncot = cdiv(cout, 64);  // a wave takes 64 couts (two 32-row MFMA tiles)
-  g.ncit = cdiv(cin, 32);
-  g.cout32 = g.ncot * 64;
-  g.cin32 = g.ncit * 32;
+  static const bool ci2_on = [] {  // STX_WG16_CI2=0: the 64 x 32 tiling for every cout
+    const char* e = getenv("STX_WG16_CI2");
+    return e ? atoi(e) != 0 : true;
+  }();
+  g.ci2 = ci2_on && cout <= 32 && in_mode != WG16_S2;
+  if (g.ci2) {  // 32 couts x two 32-cin tiles per wave (no all-zero second cout tile)
+    g.ncot = 1;
+    g.ncit = cdiv(cin, 64);
+    g.cout32 = 32;
+    g.cin32 = g.ncit * 64;
+  } else {
+    g.ncot = cdiv(cout, 64);  // a wave takes 64 couts (two 32-row MFMA tiles)
+    g.ncit = cdiv(cin, 32);
+    g.cout32 = g.ncot * 64;
+    g.cin32 = g.ncit * 32;
+  }
   g.steps = n * hv * (wv / 16);
   const int units = 3 * g.ncot * g.ncit;
   static const int target = [] {
@@ -399,7 +502,10 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
     const char* e = getenv("STX_WG16_PF");
     return e ? atoi(e) : 4;
   }();
-  if (g.mode == WG16_S2)
+  if (g.ci2)
+    hipLaunchKernelGGL((wgrad16_kernel<4, false, true>), dim3(cdiv(units, 4)), dim3(256), 0, st,
+                       x, dy, (float*)ws, x_amax, dy_amax, g);
+  else if (g.mode == WG16_S2)
     hipLaunchKernelGGL((wgrad16_kernel<4, true>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
                        (float*)ws, x_amax, dy_amax, g);
   else if (pf >= 12)
@@ -413,8 +519,12 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
                        (float*)ws, x_amax, dy_amax, g);
   const long long total = (long long)cout * cin * 9;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(wgrad16_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws, dw,
-                     g, accumulate);
+  if (blocks < 512 && g.nsplit >= 32)
+    hipLaunchKernelGGL(wgrad16_reduce4_kernel, dim3((int)((total + 63) / 64)), dim3(256), 0, st,
+                       (const float*)ws, dw, g, accumulate);
+  else
+    hipLaunchKernelGGL(wgrad16_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws,
+                       dw, g, accumulate);
   return check_launch("stx_conv2d_wgrad16");
 }
 

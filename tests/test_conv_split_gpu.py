@@ -280,7 +280,11 @@ def test_split_gram_bwd_window_ties(dev, c):
 @pytest.mark.parametrize("case", [(8, 128, 128, 16, 32, N.STX_IN_RAW),
                                   (2, 64, 32, 20, 16, N.STX_IN_RELU),
                                   (2, 128, 64, 8, 16, N.STX_IN_UPSAMPLE2),
-                                  (3, 40, 24, 9, 48, N.STX_IN_RAW)])
+                                  (3, 40, 24, 9, 48, N.STX_IN_RAW),
+                                  # cout <= 32: 32 x 64 wave tiles (two cin rows per lane)
+                                  (2, 64, 32, 8, 16, N.STX_IN_UPSAMPLE2),
+                                  (2, 72, 32, 12, 32, N.STX_IN_RAW),
+                                  (1, 64, 16, 16, 32, N.STX_IN_RELU)])
 def test_split_wgrad(dev, case):
     """3x3 weight gradient on the split MFMA vs fp64 (and the fp32 MFMA kernel)."""
     n, cin, cout, h, w, mode = case
