@@ -29,3 +29,6 @@ step rocprof-fast_st
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/proff -o run \
   -- python3 bench.py --fast-only --steps 30 --warmup 2 > gpurun_out/proff.log 2>&1 || { tail -20 gpurun_out/proff.log; exit 1; }
 step done-fast
+step smoke
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
