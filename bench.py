@@ -175,11 +175,22 @@ def fast_st_leg(args, world, rank, dev):
     tr = FastStTrainer(itn, style, world_size=world)
     batch = torch.from_numpy(W.synthetic_image(4000 + rank, (B, 3, 256, 256))).to(dev)
     steps = args.fast_steps or max(2, args.steps // 10)
+    graph = not args.no_graph and os.environ.get("STX_FAST_GRAPH", "1") != "0"
+    if graph:  # hipGraph replays per training step (FastStTrainer.capture)
+        try:
+            replay, static, _ = tr.capture(batch, warmup=max(1, min(args.warmup, 2)))
+        except RuntimeError as e:  # defensive: fall back to eager steps, say so
+            print(f"fast_st capture failed ({e}); eager steps", file=sys.stderr)
+            graph = False
+    if graph:
+        replay()
+        dt = timed(replay, steps, world, dev)
+        return dict(rate=world * B * steps / dt, dt=dt, steps=steps, batch=B, graph=True)
     for _ in range(max(1, min(args.warmup, 2))):
         tr.step(batch)
     dt = timed(lambda: tr.step(batch), steps, world, dev)
     ips = world * B * steps / dt
-    return dict(rate=ips, dt=dt, steps=steps, batch=B)
+    return dict(rate=ips, dt=dt, steps=steps, batch=B, graph=False)
 
 
 def video_leg(args, world, rank, dev):
@@ -256,10 +267,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    # rehearsal knobs (1-GPU box): STX_BENCH_SAME_DEVICE=1 puts every rank on cuda:0,
+    # STX_BENCH_BACKEND=gloo exchanges through the host; the driver's runs use neither
+    if os.environ.get("STX_BENCH_SAME_DEVICE", "0") != "0":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("STX_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     N.lib()
     if args.fast_only:
         fs = fast_st_leg(args, world, rank, dev)
@@ -342,6 +361,7 @@ def main():
                 "collective": "RCCL all_reduce(SUM) of 1,679,235 fp32 grads per step"
                               if world > 1 else None,
                 "tflops_per_gpu": round(FAST_ST_GFLOP_PER_IMAGE * fs["rate"] / world / 1e3, 3),
+                "graph": fs["graph"],
             }
         if vid:
             res["video_st"] = {

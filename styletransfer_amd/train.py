@@ -82,8 +82,8 @@ class FastStTrainer:
         w = self.world
         return (self.sw / w) * losses[:5].sum() + (self.cw / w) * losses[5] + tv
 
-    def step(self, batch: torch.Tensor) -> torch.Tensor:
-        batch = batch.to(self.device, torch.float32).contiguous()
+    def _fwd_bwd(self, batch: torch.Tensor) -> torch.Tensor:
+        """Local loss and gradient (into flat_grad) of one batch."""
         self.flat_grad.zero_()
         ops.ARENA.begin(self.device)  # InstanceNorm outputs carry their max|.| to the convs
         try:
@@ -92,10 +92,47 @@ class FastStTrainer:
             total.backward()
         finally:
             ops.ARENA.end()
+        return total.detach()
+
+    def _exchange(self):
         if self.world > 1:
             dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
+
+    def step(self, batch: torch.Tensor) -> torch.Tensor:
+        batch = batch.to(self.device, torch.float32).contiguous()
+        total = self._fwd_bwd(batch)
+        self._exchange()
         self.opt.step()
-        return total.detach()
+        return total
+
+    def capture(self, batch: torch.Tensor, warmup: int = 1):
+        """Capture the training step into hipGraphs over a static copy of `batch` --
+        the fast_st analogue of vgg.GatysEngine's per-iteration graph: the ~240
+        launches of a step replay without per-op host work.  Two graphs: (zero grad,
+        ITN forward, VGG losses, backward) and the flat Adam update; the RCCL
+        all-reduce of the flat gradient (world > 1) runs eagerly between them, so no
+        collective is ever captured.  `warmup` eager steps run first (they train like
+        any step and size every workspace).  Returns (replay, static_batch,
+        static_loss): copy the next batch into static_batch, then call replay()."""
+        static = batch.to(self.device, torch.float32).contiguous().clone()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self.step(static)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        g_fb, g_up = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        # thread_local: a process-group watchdog thread may query its events meanwhile
+        with torch.cuda.graph(g_fb, capture_error_mode="thread_local"):
+            loss = self._fwd_bwd(static)
+        with torch.cuda.graph(g_up, pool=g_fb.pool(), capture_error_mode="thread_local"):
+            self.opt.step()
+
+        def replay():
+            g_fb.replay()
+            self._exchange()
+            g_up.replay()
+        return replay, static, loss
 
     @torch.no_grad()
     def evaluate(self, batch: torch.Tensor) -> torch.Tensor:

@@ -307,6 +307,34 @@ def test_determinism(itn_case, dev):
     assert torch.equal(xs[0], xs[1])
 
 
+def test_fast_st_graph_replay_equals_eager(itn_case, dev):
+    """FastStTrainer.capture: hipGraph replays of the training step (forward/backward
+    graph + Adam graph) train bit-identically to eager steps, on fresh batches copied
+    into the static input."""
+    from styletransfer_amd.train import FastStTrainer
+    d, _ = itn_case
+    style = T(d["style"], dev)
+    batch = T(d["batch"], dev)
+    batches = [batch, batch.flip(3).contiguous(), batch.flip(2).contiguous()]
+    sd = {k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)}
+    na, nb = network.ImageTransformNet(style, 2), network.ImageTransformNet(style, 2)
+    na.load_state_dict(sd)
+    nb.load_state_dict(sd)
+    ta, tb = FastStTrainer(na, style), FastStTrainer(nb, style)
+    ta.step(batch)  # = tb's capture warm-up step
+    la = [ta.step(x) for x in batches]
+    replay, static, loss = tb.capture(batch, warmup=1)
+    lb = []
+    for x in batches:
+        static.copy_(x)
+        replay()
+        lb.append(loss.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(ta.flat, tb.flat)
+    for u, v in zip(la, lb):
+        assert torch.equal(u, v)
+
+
 def test_dp_gradient_equivalence(itn_case, dev):
     """W shards with the (mean/W + sum) scaling, summed, == the full-batch gradient."""
     from styletransfer_amd.train import FastStTrainer
