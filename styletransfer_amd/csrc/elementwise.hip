@@ -391,6 +391,25 @@ plane_sum_kernel(const float* __restrict__ x, float* __restrict__ out, int hw) {
   if (threadIdx.x == 0) out[blockIdx.x] = s;
 }
 
+// small planes: one block per channel sums its n planes in one pass (fixed order:
+// per-thread float4 running sums over the planes in order, then the block tree)
+__global__ void __launch_bounds__(RB)
+bias_grad_c_kernel(const float* __restrict__ x, float* __restrict__ db, int n, int c, int hw,
+                   int accumulate) {
+  __shared__ float red[RB / 64];
+  const int ch = blockIdx.x;
+  const int n4 = hw >> 2;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < n; ++k) {
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(x + ((size_t)k * c + ch) * hw);
+#pragma unroll 4
+    for (int i = threadIdx.x; i < n4; i += RB) a += s4[i];
+  }
+  float s = (a[0] + a[1]) + (a[2] + a[3]);
+  s = block_sum<RB>(s, red);
+  if (threadIdx.x == 0) db[ch] = accumulate ? db[ch] + s : s;
+}
+
 __global__ void sum_over_n_kernel(const float* __restrict__ parts, float* __restrict__ out, int n,
                                   int c, int accumulate) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -581,6 +600,14 @@ extern "C" int stx_tv_loss(const float* y, float* loss, float* grad, float gscal
 
 extern "C" size_t stx_bias_grad_ws(int n, int c) { return (size_t)n * c * sizeof(float) + 64; }
 
+static bool one_pass_bias() {  // STX_BIAS_ONEPASS=0: always the two-pass path (A/B)
+  static const bool on = [] {
+    const char* e = getenv("STX_BIAS_ONEPASS");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return on;
+}
+
 extern "C" int stx_bias_grad(const float* dy, float* db, int n, int c, int hw, int accumulate,
                              void* ws, size_t ws_bytes, void* stream) {
   if (!ws || ws_bytes < stx_bias_grad_ws(n, c)) {
@@ -588,6 +615,13 @@ extern "C" int stx_bias_grad(const float* dy, float* db, int n, int c, int hw, i
     return STX_E_WORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
+  if ((hw & 3) == 0 && (reinterpret_cast<uintptr_t>(dy) & 15) == 0 &&
+      (long long)n * hw <= 64 * 1024 && c >= 16 && one_pass_bias()) {
+    // <= 256 KB per channel: one launch (the two-pass path below is launch-bound there)
+    hipLaunchKernelGGL(bias_grad_c_kernel, dim3(c), dim3(RB), 0, st, dy, db, n, c, hw,
+                       accumulate);
+    return check_launch("stx_bias_grad");
+  }
   hipLaunchKernelGGL(plane_sum_kernel, dim3(n * c), dim3(RB), 0, st, dy, (float*)ws, hw);
   hipLaunchKernelGGL(sum_over_n_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st, (const float*)ws,
                      db, n, c, accumulate);
