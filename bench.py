@@ -23,7 +23,8 @@ import subprocess
 import sys
 import time
 
-import numpy as np
+import socket
+
 import torch
 import torch.distributed as dist
 
@@ -31,10 +32,18 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 os.environ.setdefault("STX_NO_LOGFILE", "1")
 
-from styletransfer_amd import ops  # noqa: E402
-from styletransfer_amd import vgg as V  # noqa: E402
-from styletransfer_amd import weights as W  # noqa: E402
-from styletransfer_amd import _native as N  # noqa: E402
+# libstx-facing modules are imported by _imports(), after the launcher decision: the
+# parent of a `--gpus N` run must not touch the GPU before it starts its N ranks
+ops = V = W = N = None
+
+
+def _imports():
+    global ops, V, W, N
+    from styletransfer_amd import ops as _ops
+    from styletransfer_amd import vgg as _V
+    from styletransfer_amd import weights as _W
+    from styletransfer_amd import _native as _N
+    ops, V, W, N = _ops, _V, _W, _N
 
 METRIC = ("Gatys iters/sec at 512×512 + fast_st images/sec at 256×256, "
           "1/2/4/8 GPUs")
@@ -81,12 +90,17 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--fast-batch", type=int, default=8, help="fast_st images per GPU")
-    ap.add_argument("--fast-steps", type=int, default=0, help="default: max(2, steps//10)")
+    ap.add_argument("--fast-steps", type=int, default=50, help="timed fast_st train steps")
+    ap.add_argument("--fast-b64-steps", type=int, default=10,
+                    help="timed steps of the B=64-on-one-GPU fast_st leg (world 1; 0 = skip)")
+    ap.add_argument("--gatys-run-iters", type=int, default=500,
+                    help="config 2 as written: one timed run of this many Gatys iterations")
     ap.add_argument("--skip-fast", action="store_true")
     ap.add_argument("--fast-only", action="store_true", help="profiling: fast_st leg only")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-infer", action="store_true", help="skip the video/convert legs")
     ap.add_argument("--cpu-iters", type=int, default=4)
+    ap.add_argument("--cpu-fast-batch", type=int, default=8, help="fast_st CPU leg batch")
     ap.add_argument("--no-graph", action="store_true")
     return ap.parse_args()
 
@@ -138,6 +152,12 @@ def gatys_leg(args, world, rank, dev):
         eng.capture(warmup=max(1, args.warmup))
     dt = timed(eng.step, args.steps, world, dev)
     rate = world * args.steps / dt
+    run = None
+    if args.gatys_run_iters > 0:
+        # BASELINE config 2 as written: one gatys_st run of 500 Adam iterations
+        n = args.gatys_run_iters
+        dtr = timed(eng.step, n, world, dev)
+        run = dict(iters=n, s=dtr, rate=world * n / dtr)
     # dominant kernel: the 3x3 implicit-GEMM conv at 64 channels, 512x512 (conv1_2
     # forward, the single launch with this kernel instance in a Gatys iteration, so
     # the rocprof average of the same command is directly comparable)
@@ -159,30 +179,29 @@ def gatys_leg(args, world, rank, dev):
     zam = V.slot(eng.st.amax, 2).clone()
     gram_ms = event_avg_ms(lambda: ops.gram(z2, z_amax=zam), reps=20)
     loss = float(eng.total)
-    return dict(rate=rate, dt=dt, loss=loss, kernel=dict(fwd_ms=fwd_ms, gflop=gf,
+    return dict(rate=rate, dt=dt, loss=loss, run=run, kernel=dict(fwd_ms=fwd_ms, gflop=gf,
                                                          tflops=achieved),
                 gram=dict(ms=gram_ms, gflop=2.0 * 64 * 64 * H * H / 1e9,
                           bytes=64 * H * H * 4))
 
 
-def fast_st_leg(args, world, rank, dev):
+def fast_st_leg(args, world, rank, dev, B=None, steps=None):
+    """fast_st train steps (config 4 shape): per-rank batch B, one SUM all-reduce of the
+    flat gradient per step at world > 1.  A failed hipGraph capture is an error (no
+    silent fall-back to eager steps in a process whose stream may be left in a failed
+    capture state); --no-graph times eager steps."""
     from styletransfer_amd import network
     from styletransfer_amd.train import FastStTrainer
-    B = args.fast_batch
+    B = B or args.fast_batch
     style = torch.from_numpy(W.synthetic_image(3000, (1, 3, 256, 256))).to(dev)
     itn = network.ImageTransformNet(style, batch_size=B).to(dev)
     itn.load_state_dict({k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)})
     tr = FastStTrainer(itn, style, world_size=world)
     batch = torch.from_numpy(W.synthetic_image(4000 + rank, (B, 3, 256, 256))).to(dev)
-    steps = args.fast_steps or max(2, args.steps // 10)
+    steps = steps or args.fast_steps
     graph = not args.no_graph and os.environ.get("STX_FAST_GRAPH", "1") != "0"
     if graph:  # hipGraph replays per training step (FastStTrainer.capture)
-        try:
-            replay, static, _ = tr.capture(batch, warmup=max(1, min(args.warmup, 2)))
-        except RuntimeError as e:  # defensive: fall back to eager steps, say so
-            print(f"fast_st capture failed ({e}); eager steps", file=sys.stderr)
-            graph = False
-    if graph:
+        replay, static, _ = tr.capture(batch, warmup=max(1, min(args.warmup, 2)))
         replay()
         dt = timed(replay, steps, world, dev)
         return dict(rate=world * B * steps / dt, dt=dt, steps=steps, batch=B, graph=True)
@@ -230,10 +249,41 @@ def convert_leg(args, world, rank, dev):
     return dict(rate=world * B * n / dt, dt=dt, steps=n, batch=B)
 
 
+def _host_cpu():
+    """(threads to use, description): the CPUs this process may run on (affinity /
+    cgroup cpuset), which on a shared GPU box is the box's CPU share, not the
+    whole machine's os.cpu_count()."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    threads = min(aff, quota) if quota else aff
+    model = ""
+    try:
+        out = subprocess.check_output(["lscpu"], text=True)
+        model = next((l.split(":", 1)[1].strip() for l in out.splitlines()
+                      if l.startswith("Model name")), "")
+    except Exception:  # noqa: BLE001
+        model = platform.processor()
+    return threads, (f"{model}; {threads} threads = usable CPUs (affinity {aff}, cgroup quota "
+                     f"{quota}, os.cpu_count {os.cpu_count()})")
+
+
 def cpu_baseline(args):
-    """The oracle (torch-CPU restatement of the reference schedule) on host cores."""
+    """The oracle (torch-CPU restatement of the reference schedule) on the host cores:
+    the Gatys Adam loop at 512^2 (the `value` metric), plus the fast_st train step and
+    the convert-image forward at 256^2 (north_star: images/s next to the reference CPU
+    path timed on the same box)."""
     from oracle import reference_cpu as O
-    threads = min(16, os.cpu_count() or 1)
+    threads, host = _host_cpu()
     torch.set_num_threads(threads)
     H = args.size
     s = torch.from_numpy(W.synthetic_image(1000, (1, 3, H, H)))
@@ -247,30 +297,80 @@ def cpu_baseline(args):
     for _ in range(n):
         O.gatys_adam_iter(net, x, c, opt)
     dt = time.perf_counter() - t0
-    model = ""
-    try:
-        out = subprocess.check_output(["lscpu"], text=True)
-        model = next((l.split(":", 1)[1].strip() for l in out.splitlines()
-                      if l.startswith("Model name")), "")
-    except Exception:  # noqa: BLE001
-        model = platform.processor()
+    # fast_st train step (static_train closure + Adam) and ITN forward at 256^2
+    B = args.cpu_fast_batch
+    itn = O.image_transform_net(4321)
+    st = torch.from_numpy(W.synthetic_image(3000, (1, 3, 256, 256)))
+    ln = O.StyleNetwork(st, torch.rand([1, 3, 256, 256]))
+    batch = torch.from_numpy(W.synthetic_image(4000, (B, 3, 256, 256)))
+    aopt = torch.optim.Adam(itn.parameters())
+
+    def fast_step():
+        aopt.zero_grad()
+        O.fast_st_closure(itn, ln, batch)
+        aopt.step()
+    fast_step()  # warm-up
+    t1 = time.perf_counter()
+    fast_step()
+    dtf = time.perf_counter() - t1
+    with torch.no_grad():
+        itn(batch)
+        t2 = time.perf_counter()
+        itn(batch)
+        dtc = time.perf_counter() - t2
     return dict(value=n / dt, unit="iters/s", cores=threads, kind="port",
                 sample=f"oracle/reference_cpu.py Gatys Adam loop {H}x{H}, {n} timed iters "
                        f"after 1 warm-up ({dt:.1f} s), reference schedule incl. prefix "
-                       f"re-runs and VGG wgrad; torch {torch.__version__} CPU, {model}")
+                       f"re-runs and VGG wgrad; torch {torch.__version__} CPU, {host}",
+                fast_st=dict(value=B / dtf, unit="images/s", batch=B, s=round(dtf, 2),
+                             sample=f"oracle fast_st_closure + torch.optim.Adam, B={B} 256^2, "
+                                    "1 timed step after 1 warm-up"),
+                convert=dict(value=B / dtc, unit="images/s", batch=B, s=round(dtc, 2),
+                             sample=f"oracle ImageTransformNet forward, B={B} 256^2, no_grad, "
+                                    "1 timed pass after 1 warm-up"))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n):
+    """`python bench.py --gpus N` without a launcher: start N rank processes (the
+    torchrun environment contract, one per GPU) and exit with the worst exit code.
+    This parent process never touches the GPU."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus))
+    _imports()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    # rehearsal knobs (1-GPU box): STX_BENCH_SAME_DEVICE=1 puts every rank on cuda:0,
-    # STX_BENCH_BACKEND=gloo exchanges through the host; the driver's runs use neither
-    if os.environ.get("STX_BENCH_SAME_DEVICE", "0") != "0":
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # more ranks than visible GPUs (a same-device rehearsal on a 1-GPU box; or
+    # STX_BENCH_SAME_DEVICE=1): ranks share cuda:0 and exchange over gloo, and the line
+    # says so ("devices"); the driver's 8-GPU runs have one GPU per rank and use RCCL
+    ndev = torch.cuda.device_count()
+    same = os.environ.get("STX_BENCH_SAME_DEVICE", "0") != "0" or ndev < world
+    if same:
         local = 0
+        os.environ.setdefault("STX_BENCH_BACKEND", "gloo" if world > 1 else "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -288,6 +388,10 @@ def main():
         return
     g = gatys_leg(args, world, rank, dev)
     fs = None if args.skip_fast else fast_st_leg(args, world, rank, dev)
+    fs64 = None
+    if not args.skip_fast and world == 1 and args.fast_b64_steps > 0:
+        # at 1 GPU the config-4 global batch of 64 on one device
+        fs64 = fast_st_leg(args, world, rank, dev, B=64, steps=args.fast_b64_steps)
     vid = conv = None
     if not args.skip_infer:
         vid = video_leg(args, world, rank, dev)
@@ -303,6 +407,7 @@ def main():
             "value": round(g["rate"], 3),
             "unit": "iters/s",
             "n_gpus": world,
+            "devices": 1 if same else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * g["dt"] / args.steps, 4),
@@ -352,17 +457,31 @@ def main():
             "cpu_baseline": cpu,
             "gatys_loss": g["loss"],
         }
+        if g["run"]:
+            r = g["run"]
+            res["gatys_config2_run"] = {
+                "iters": r["iters"], "seconds": round(r["s"], 4), "value": round(r["rate"], 3),
+                "unit": "iters/s", "note": "BASELINE config 2 as written: one timed run of "
+                "500 Adam iterations at 512^2 (hipGraph replays), after the K timed steps"}
         if fs:
             res["fast_st"] = {
                 "value": round(fs["rate"], 3), "unit": "images/s",
                 "per_gpu_batch": fs["batch"], "global_batch": fs["batch"] * world,
                 "steps": fs["steps"], "ms_per_step": round(1e3 * fs["dt"] / fs["steps"], 3),
                 "parallelism": f"dp{world}", "scaling": "weak",
-                "collective": "RCCL all_reduce(SUM) of 1,679,235 fp32 grads per step"
+                "collective": (f"{os.environ.get('STX_BENCH_BACKEND', 'nccl').replace('nccl', 'RCCL')}"
+                               " all_reduce(SUM) of 1,679,235 fp32 grads per step")
                               if world > 1 else None,
                 "tflops_per_gpu": round(FAST_ST_GFLOP_PER_IMAGE * fs["rate"] / world / 1e3, 3),
                 "graph": fs["graph"],
             }
+        if fs64:
+            res["fast_st_b64"] = {
+                "value": round(fs64["rate"], 3), "unit": "images/s", "batch": 64,
+                "steps": fs64["steps"], "ms_per_step": round(1e3 * fs64["dt"] / fs64["steps"], 3),
+                "tflops": round(FAST_ST_GFLOP_PER_IMAGE * fs64["rate"] / 1e3, 3),
+                "graph": fs64["graph"], "note": "config-4 global batch 64 on one GPU (the "
+                "1-GPU point of the strong-scaling view; the weak-scaling legs keep 8/GPU)"}
         if vid:
             res["video_st"] = {
                 "value": round(vid["rate"], 2), "unit": "frames/s", "frame": vid["size"],

@@ -26,12 +26,15 @@ def fast_st():
               help="Train on N synthetic images instead of local COCO (no network here)")
 def train(style_image_path, epochs, batch_size, content_weight, style_weight, synthetic):
     """Train the fast style transfer network (checkpoint per epoch in data/models/)."""
+    from .. import distributed
+    distributed.from_env()  # torchrun: one rank per GPU, bound before anything allocates
     style_name = style_image_path.split("/")[-1]
     LOGGER.info("Training fast style transfer network with style name: %s", style_name)
     style_image = img_utils.image_loader(
         os.path.join(constants.PROJECT_ROOT_PATH, style_image_path))
     net = network.ImageTransformNet(style_image, batch_size)
-    loaders = (dataset.get_synthetic_loader(batch_size, n_train=synthetic)
+    loaders = ((lambda shard: dataset.get_synthetic_loader(batch_size, n_train=synthetic,
+                                                            shard=shard))
                if synthetic else None)
     net.static_train(style_name=style_name, epochs=epochs, style_weight=style_weight,
                      content_weight=content_weight, loaders=loaders)

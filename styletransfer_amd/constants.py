@@ -16,7 +16,10 @@ LOG_PATH = os.path.join(RUNS_PATH, "runtime.log")
 IMAGENET_MEAN = [0.485, 0.456, 0.406]
 IMAGENET_STD = [0.229, 0.224, 0.225]
 
-DEVICE = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+# device_count() (not is_available()) so that importing the package does not initialise
+# the HIP runtime: launchers (bench.py --gpus N, the DP tests) spawn their GPU ranks from
+# a parent that must never touch the GPU
+DEVICE = torch.device("cuda" if torch.cuda.device_count() > 0 else "cpu")
 
 IMSIZE = int(os.environ.get("STX_IMSIZE", "256"))
 

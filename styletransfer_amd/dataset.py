@@ -50,8 +50,20 @@ class CocoDataset(Dataset):
             return self[random.randrange(len(self))]
 
 
-def get_coco_loader(batch_size=4, test_split=0.10, test_limit=None, path=None):
-    """(test_loader, train_loader) over local COCO images (stransfer/dataset.py:314-360)."""
+def _train_loader(ds, batch_size, shard, shuffle=True, seed=0):
+    """DataLoader over `ds` whose batches are this rank's shard of each global batch
+    of `batch_size` (distributed.ShardedBatchSampler); at world 1 a plain batch."""
+    from .distributed import Shard, ShardedBatchSampler
+    shard = shard or Shard()
+    sampler = ShardedBatchSampler(len(ds), batch_size, shard.rank, shard.world,
+                                  shuffle=shuffle, seed=seed)
+    return DataLoader(ds, batch_sampler=sampler)
+
+
+def get_coco_loader(batch_size=4, test_split=0.10, test_limit=None, path=None, shard=None):
+    """(test_loader, train_loader) over local COCO images (stransfer/dataset.py:314-360).
+    `batch_size` is the global batch; with a data-parallel `shard` each rank's train
+    loader yields its batch_size/world slice of every global batch."""
     path = path or os.path.join(constants.PROJECT_ROOT_PATH, IMAGE_FOLDER_PATH)
     if not os.path.isdir(path) or not os.listdir(path):
         raise FileNotFoundError(
@@ -63,7 +75,7 @@ def get_coco_loader(batch_size=4, test_split=0.10, test_limit=None, path=None):
     if test_limit:
         test_imgs = test_imgs[:test_limit]
     test = DataLoader(CocoDataset(test_imgs, path=path), batch_size=batch_size, shuffle=False)
-    train = DataLoader(CocoDataset(train_imgs, path=path), batch_size=batch_size, shuffle=True)
+    train = _train_loader(CocoDataset(train_imgs, path=path), batch_size, shard)
     return test, train
 
 
@@ -82,7 +94,10 @@ class SyntheticImageDataset(Dataset):
         return torch.from_numpy(x)
 
 
-def get_synthetic_loader(batch_size=4, n_train=64, n_test=8, size=None, seed=0):
+def get_synthetic_loader(batch_size=4, n_train=64, n_test=8, size=None, seed=0, shard=None,
+                         shuffle=False):
+    """(test, train) loaders of SyntheticImageDataset; train sharded like get_coco_loader."""
     test = DataLoader(SyntheticImageDataset(n_test, size, seed + 1), batch_size=batch_size)
-    train = DataLoader(SyntheticImageDataset(n_train, size, seed), batch_size=batch_size)
+    train = _train_loader(SyntheticImageDataset(n_train, size, seed), batch_size, shard,
+                          shuffle=shuffle, seed=seed)
     return test, train

@@ -19,8 +19,10 @@ Documented differences (all numerics-neutral):
 """
 from __future__ import annotations
 
+import logging
 import os
 import shutil
+import weakref
 
 import numpy as np
 import torch
@@ -253,15 +255,18 @@ class StyleNetwork(nn.Module):
         return self._feat
 
     def _set_content_targets(self, content_image):
-        key = (content_image.data_ptr(), content_image._version, tuple(content_image.shape))
-        if key == self._content_key:
+        # keyed on the tensor object itself (a weak reference) and its version: a new
+        # tensor that lands in a recycled allocator block (same data_ptr, version 0)
+        # is a different content image and must be re-targeted
+        key = self._content_key
+        if key is not None and key[0]() is content_image and key[1] == content_image._version:
             return
         feat = self.features()
         with torch.no_grad():
             c4 = V.content_target(feat, content_image).clone()
             self.content_losses[0][0].set_target(c4)
             self.feature_losses[0][0].set_target(A.ReLUFn.apply(c4))
-        self._content_key = key
+        self._content_key = (weakref.ref(content_image), content_image._version)
 
     def forward(self, input_image: torch.Tensor, content_image=None, style_image=None) -> None:
         """stransfer/network.py:366-401.  Sets `.loss` on every loss module."""
@@ -337,7 +342,8 @@ class StyleNetwork(nn.Module):
             total = (self.get_total_current_style_loss(weight=style_weight)
                      + self.get_total_current_content_loss(weight=content_weight))
             total.backward()
-            LOGGER.info("Loss: %s", total)
+            if LOGGER.isEnabledFor(logging.DEBUG):  # formatting a device tensor syncs
+                LOGGER.debug("Loss: %s", total)
             return total
 
         for _ in tqdm(range(steps)):
@@ -443,44 +449,73 @@ class ImageTransformNet(nn.Sequential):
 
     # ---------------------------------------------------------------- workflows
     def static_train(self, style_name="nsp", epochs=50, style_weight=100_000, content_weight=1,
-                     loaders=None):
-        """stransfer/network.py:651-770.  `loaders=(test, train)` overrides COCO
-        (e.g. dataset.get_synthetic_loader())."""
+                     loaders=None, graph=True):
+        """stransfer/network.py:651-770, data-parallel when launched with torchrun.
+
+        One process per GPU (styletransfer_amd/distributed.py): `batch_size` is the
+        global batch, each rank trains on its batch_size/world shard of it, the flat
+        gradient is SUM-all-reduced once per step (train.FastStTrainer) and every rank
+        applies the same Adam update.  Rank 0 alone logs, runs static_test and writes
+        the per-epoch checkpoint.  `loaders=(test, train)` (or a callable taking the
+        Shard and returning them) overrides COCO, e.g. dataset.get_synthetic_loader.
+        graph=True replays each step as hipGraphs (FastStTrainer.train_step)."""
+        from . import distributed as D
         from .train import FastStTrainer
-        tb_writer = get_tensorboard_writer(f"runs/fast-image-style-transfer-still-image_{style_name}")
-        trainer = FastStTrainer(self, self.style_image, style_weight=style_weight,
-                                content_weight=content_weight)
-        loss_network = trainer.loss_network()
-        LOGGER.info('Training network with "%s" optimizer', type(trainer.opt))
+        shard = D.from_env()
+        dev = D.device_for(shard)
+        if next(self.parameters()).device != dev:
+            self.to(dev)
+        main = shard.is_main
+        tb_writer = (get_tensorboard_writer(f"runs/fast-image-style-transfer-still-image_{style_name}")
+                     if main else _NullWriter())
+        trainer = FastStTrainer(self, self.style_image.to(dev), style_weight=style_weight,
+                                content_weight=content_weight, world_size=shard.world,
+                                process_group=shard.group)
+        loss_network = trainer.loss_network() if main else None
+        if main:
+            LOGGER.info('Training network with "%s" optimizer on %d data-parallel rank(s)',
+                        type(trainer.opt), shard.world)
+        if callable(loaders):
+            loaders = loaders(shard)
         test_loader, train_loader = loaders or dataset.get_coco_loader(
-            test_split=0.10, test_limit=20, batch_size=self.batch_size)
+            test_split=0.10, test_limit=20, batch_size=self.batch_size, shard=shard)
         iteration = 0
-        os.makedirs("data/models", exist_ok=True)
+        if main:
+            os.makedirs("data/models", exist_ok=True)
         for epoch in range(epochs):
-            LOGGER.info("Starting epoch %d", epoch)
+            if main:
+                LOGGER.info("Starting epoch %d", epoch)
             ckpt = f"data/models/fast_st_{style_name}_epoch{epoch}.pth"
             if os.path.isfile(ckpt):
                 self.load_state_dict(adaptive_torch_load(ckpt))
                 trainer.resync_params()
                 continue
-            for batch in tqdm(train_loader):
-                batch = _dev(batch.squeeze(1)).contiguous()
+            sampler = getattr(train_loader, "batch_sampler", None)
+            if hasattr(sampler, "set_epoch"):
+                sampler.set_epoch(epoch)
+            for batch in tqdm(train_loader, disable=not main):
+                batch = batch.squeeze(1).to(dev, torch.float32).contiguous()
                 if iteration % 20 == 0:
-                    total = trainer.evaluate(batch)
-                    tb_writer.add_scalar("data/fst_train_loss", total, iteration)
-                    LOGGER.info("Batch Loss: %.8f", float(total))
-                if iteration % 150 == 0:
+                    # local (mean/W + TV-sum) losses summed over ranks = the global-batch loss
+                    total = shard.sum_(trainer.evaluate(batch).reshape(1))[0]
+                    if main:
+                        tb_writer.add_scalar("data/fst_train_loss", total, iteration)
+                        LOGGER.info("Batch Loss: %.8f", float(total))
+                if main and iteration % 150 == 0:
                     avg = self.static_test(test_loader, loss_network)
                     tb_writer.add_scalar("data/fst_test_loss", avg, iteration)
-                if iteration % 50 == 0:
+                if main and iteration % 50 == 0:
                     with torch.no_grad():
                         img = torch.clamp(self(batch), min=0, max=255)[0]
                     tb_writer.add_image("data/fst_images",
                                         img_utils.concat_images(img.squeeze(), batch[0].squeeze()),
                                         iteration)
                 iteration += 1
-                trainer.step(batch)
-            torch.save(self.state_dict(), ckpt)
+                trainer.train_step(batch, graph=graph)
+            if main:
+                torch.save(self.state_dict(), ckpt)
+            shard.barrier()
+        return trainer
 
     def static_test(self, test_loader, loss_network, style_weight=100_000, feature_weight=1):
         """stransfer/network.py:772-796."""

@@ -46,17 +46,27 @@ def _req(t: torch.Tensor, name: str = "tensor"):
 
 class _Workspace:
     """Per-device scratch buffer, grown on demand.  All users are stream-ordered
-    on the same stream and finish with the scratch inside one C call."""
+    on the same stream and finish with the scratch inside one C call.
+
+    A captured hipGraph (GatysEngine, FastStTrainer.capture, FrameEngine) bakes the
+    scratch pointer of its capture into its kernels, so a buffer is never freed
+    once handed out: when a larger one is needed the old one is retired, not
+    released to the caching allocator (growth is geometric, so the retired
+    buffers sum to less than the live one)."""
 
     def __init__(self):
         self.buf = {}
+        self.retired = []
 
     def get(self, nbytes: int, device) -> tuple:
         nbytes = max(int(nbytes), 256)
         key = (device.index if isinstance(device, torch.device) else device)
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
-            b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            size = max(nbytes, 1 << 20) if b is None else max(nbytes, 2 * b.numel())
+            if b is not None:
+                self.retired.append(b)
+            b = torch.empty(size, dtype=torch.uint8, device=device)
             self.buf[key] = b
         return b.data_ptr(), b.numel()
 

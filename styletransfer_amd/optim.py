@@ -8,8 +8,17 @@ device so the update can live inside a captured hipGraph.
 from __future__ import annotations
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import ops
+
+
+def bump_versions(params):
+    """In-place updates through the C ABI are invisible to autograd's version counters;
+    bump them so caches keyed on `_version` (layers.Conv2d.prepped: the weight slabs)
+    see the new values."""
+    for p in params:
+        increment_version(p)
 
 
 class Adam(torch.optim.Optimizer):
@@ -45,14 +54,17 @@ class Adam(torch.optim.Optimizer):
                 st = self._state(p)
                 ops.adam_step(p, p.grad, st["exp_avg"], st["exp_avg_sq"], st["step_dev"],
                               st["ws"], group["lr"], b1, b2, group["eps"])
+                increment_version(p)
         return loss
 
 
 class FlatAdam:
     """Adam over one flat parameter buffer (single launch for all tensors)."""
 
-    def __init__(self, flat_param, flat_grad, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+    def __init__(self, flat_param, flat_grad, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                 params=()):
         self.p, self.g = flat_param, flat_grad
+        self.params = list(params)  # the nn.Parameter views (version bumps)
         self.m = torch.zeros_like(flat_param)
         self.v = torch.zeros_like(flat_param)
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=flat_param.device)
@@ -62,6 +74,7 @@ class FlatAdam:
     def step(self):
         ops.adam_step(self.p, self.g, self.m, self.v, self.step_dev, self.ws, self.lr,
                       self.betas[0], self.betas[1], self.eps)
+        bump_versions(self.params)
 
 
 class LBFGS(torch.optim.Optimizer):
@@ -122,6 +135,18 @@ class LBFGS(torch.optim.Optimizer):
     def _host(self, i):
         return float(self._S[i])
 
+    def _hosts(self, *idx):
+        """Several scalar slots in one device->host read."""
+        return self._S[list(idx)].tolist()
+
+    def _loss_slot(self, loss, i=10):
+        """Park the closure's loss in slot i (device copy, no sync); returns a thunk
+        for python-number losses, which have no device value."""
+        if torch.is_tensor(loss):
+            self._S[i:i + 1].copy_(loss.detach().reshape(1))
+            return None
+        return float(loss)
+
     def _grad(self):
         g = self._p.grad
         if g is None:
@@ -149,13 +174,15 @@ class LBFGS(torch.optim.Optimizer):
         st.setdefault("n_iter", 0)
         with torch.enable_grad():
             orig_loss = closure()
-        loss = float(orig_loss)
+        hl = self._loss_slot(orig_loss)
         current_evals = 1
         st["func_evals"] += 1
         g = self._grad()
         n = g.numel()
-        self._red(g, None, 2, self._sp(5))
-        if self._host(5) <= tol_grad:
+        self._red(g, None, 2, self._sp(11))
+        loss, gmax = self._hosts(10, 11)                  # one sync: loss, max|g|
+        loss = loss if hl is None else hl
+        if gmax <= tol_grad:
             return orig_loss
         d = st.get("d")
         prev_g = st.get("prev_flat_grad")
@@ -216,26 +243,32 @@ class LBFGS(torch.optim.Optimizer):
                 self._sc(1, 3, 7, 3)                           # t *= lr
             else:
                 self._sc(3, 7, 8, 3)                           # t = lr
-            t_host = self._host(3)
             self._red(g, d, 0, self._sp(4))                    # gtd
-            if self._host(4) > -tol_change:
+            t_host, gtd = self._hosts(3, 4)                    # one sync: t, g.d
+            if gtd > -tol_change:
                 break
             ls_evals = 0
             self._axpby(p.data.view(-1), d, 1.0, self._sp(3), b=1.0)   # x += t d
+            increment_version(p)
             opt_cond = False
+            self._red(d, None, 2, self._sp(12))                # max|d| (for the last test)
+            dmax = None
             if n_iter != max_iter:
                 with torch.enable_grad():
-                    loss = float(closure())
+                    hl = self._loss_slot(closure())
                 g = self._grad()
-                self._red(g, None, 2, self._sp(5))
-                opt_cond = self._host(5) <= tol_grad
+                self._red(g, None, 2, self._sp(11))
+                loss, gmax, dmax = self._hosts(10, 11, 12)     # one sync: loss, max|g|, max|d|
+                loss = loss if hl is None else hl
+                opt_cond = gmax <= tol_grad
                 ls_evals = 1
             current_evals += ls_evals
             st["func_evals"] += ls_evals
             if n_iter == max_iter or current_evals >= max_eval or opt_cond:
                 break
-            self._red(d, None, 2, self._sp(5))
-            if abs(t_host) * self._host(5) <= tol_change:      # max|d * t|
+            if dmax is None:
+                dmax = self._host(12)
+            if abs(t_host) * dmax <= tol_change:               # max|d * t|
                 break
             if abs(loss - prev_loss) < tol_change:
                 break

@@ -25,7 +25,7 @@ from . import ops
 from . import autograd as A
 from . import constants
 from . import vgg as V
-from .optim import FlatAdam
+from .optim import FlatAdam, bump_versions
 
 
 def flatten_parameters(module: torch.nn.Module, device):
@@ -61,8 +61,21 @@ class FastStTrainer:
         self.world = int(world_size)
         self.pg = process_group
         self.flat, self.flat_grad = flatten_parameters(itn, self.device)
-        self.opt = FlatAdam(self.flat, self.flat_grad, lr=lr)
+        self.params = list(itn.parameters())
+        if self.world > 1:
+            # replicas must start identical (e.g. static_train's default torch init is
+            # drawn independently per process): rank 0's parameters win
+            dist.broadcast(self.flat, src=self._src(), group=self.pg)
+            bump_versions(self.params)
+        self.opt = FlatAdam(self.flat, self.flat_grad, lr=lr, params=self.params)
         self.vgg_weights = vgg_weights
+        self._graph = None  # (replay, static batch, static loss) of train_step
+
+    def _src(self):
+        """Global rank of the group's rank 0."""
+        if self.pg is None:
+            return 0
+        return dist.get_global_rank(self.pg, 0)
 
     def resync_params(self):
         """No-op: load_state_dict copies into the flat views in place."""
@@ -119,7 +132,7 @@ class FastStTrainer:
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for _ in range(max(1, warmup)):
-                self.step(static)
+                self.warmup_loss = self.step(static)
         torch.cuda.current_stream(self.device).wait_stream(side)
         g_fb, g_up = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         # thread_local: a process-group watchdog thread may query its events meanwhile
@@ -132,7 +145,27 @@ class FastStTrainer:
             g_fb.replay()
             self._exchange()
             g_up.replay()
+            bump_versions(self.params)  # the graph's Adam is invisible to autograd
         return replay, static, loss
+
+    def train_step(self, batch: torch.Tensor, graph: bool = True) -> torch.Tensor:
+        """step() for a stream of batches: the first batch of a shape is trained by the
+        capture's warm-up step (eager) and the step is captured; every later batch of
+        that shape is copied into the static input and replayed.  Other shapes (a
+        short last batch) run eagerly.  Returns the local loss (device tensor; a
+        view of the graph's static output on replays)."""
+        batch = batch.to(self.device, torch.float32).contiguous()
+        if not graph:
+            return self.step(batch)
+        if self._graph is None:
+            self._graph = self.capture(batch, warmup=1)
+            return self.warmup_loss
+        replay, static, loss = self._graph
+        if static.shape != batch.shape:
+            return self.step(batch)
+        static.copy_(batch)
+        replay()
+        return loss
 
     @torch.no_grad()
     def evaluate(self, batch: torch.Tensor) -> torch.Tensor:

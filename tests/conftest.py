@@ -16,7 +16,7 @@ def pytest_configure(config):
 
 def pytest_collection_modifyitems(config, items):
     import torch
-    if torch.cuda.is_available():
+    if torch.cuda.device_count() > 0:  # (does not initialise the HIP runtime)
         return
     skip = pytest.mark.skip(reason="no GPU visible")
     for it in items:

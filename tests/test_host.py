@@ -87,7 +87,7 @@ def test_itn_structure_cpu():
     assert vnet[0].in_channels == 6 and not vnet.has_external_weights
 
 
-@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+@pytest.mark.skipif(torch.cuda.device_count() > 0, reason="checks the no-GPU failure mode")
 def test_product_path_fails_loudly_without_gpu():
     from styletransfer_amd import _native as N
     from styletransfer_amd import network

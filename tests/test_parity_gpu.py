@@ -216,24 +216,94 @@ def test_itn_forward_backward_golden(itn_case, dev):
     assert rel(cl, d["content_loss"]) < 1e-4
     assert rel(tv, d["tv_loss"]) < 1e-4
     assert rel(total, d["total"]) < 1e-4
-    norms = d["grad_proj"][:, 0]
-    for i, p in enumerate(net.parameters()):
-        gp = p.grad.detach().cpu().numpy()
-        ref = d["grad_proj"][i]
-        if ref[0] < 1e-7 * norms.max():
+    # parameter gradients, three-way against fp64 truth (itn_fp64.npz: the pinned
+    # oracle evaluated in float64 on the same inputs).  The fp32 reference itself is
+    # ~7e-4 from fp64 here (rounding propagated through 15 InstanceNorm layers).
+    # Walking from the output back towards the input, the HIP gradient is within
+    # 2.5x of that until the backward crosses a ReLU boundary element (an IN output
+    # within rounding of 0 whose mask the fp32-class forward decides differently
+    # from fp64; measured: block 11's insn1, 11.insn1.bias 2.4e-2).  Every parameter
+    # upstream of that single flip inherits its effect, bounded here by 3e-2, and
+    # there must be no second jump.  Each layer's kernels are held to 3x the fp32
+    # error vs fp64 in isolation by tests/test_itn_layers_gpu.py, which has no such
+    # cascade.
+    f64 = g("itn_fp64")
+    norms = f64["grad64_proj"][:, 0]
+    params = list(net.parameters())
+    flipped, errs = False, []
+    for i in reversed(range(len(params))):          # output side first
+        gp = params[i].grad.detach().cpu().numpy()
+        if norms[i] < 1e-7 * norms.max():
             # conv bias followed by InstanceNorm: exactly 0 in exact arithmetic (fp64
-            # oracle |g|~1e-14; fp32 rounding noise ~1e-5 in the reference)
+            # |g| ~ 1e-14; fp32 rounding noise ~1e-5 in the reference)
             assert np.linalg.norm(gp) < 1e-6 * norms.max(), i
             continue
-        # norm + 8 random projections of each parameter gradient.  Tolerance 5e-2:
-        # back-propagating through 15 InstanceNorm+ReLU layers, a ReLU input within
-        # ~1e-6 of 0 can land on the other side of the mask in any fp32
-        # implementation (tools/diag_itn_grad.py: the fp32 reference itself is
-        # 6e-4 from an fp64 oracle, one mask flip moves upstream gradients ~1.5e-2).
-        assert abs(np.linalg.norm(gp) - ref[0]) <= 5e-2 * ref[0], i
-        assert rel(proj(gp), ref[1:]) < 5e-2, i
+        e64 = rel(proj32(gp), f64["grad64_proj"][i, 1:])
+        r32 = float(f64["ref32_err"][i])
+        errs.append((e64, r32, i))
+        if not flipped and e64 > max(2.5 * r32, 1e-5):
+            flipped = True                             # the one boundary crossing
+        assert e64 <= (3e-2 if flipped else max(2.5 * r32, 1e-5)), (i, e64, r32)
+    print("ITN grad error vs fp64 (hip, fp32-ref, param):", sorted(errs)[-3:])
     with torch.no_grad():
         assert rel(net(batch[:1]), d["y_single"]) < 1e-4
+
+
+def proj32(a, seed=77):
+    a = np.asarray(a, np.float64).ravel()
+    r = W.hash_normal(seed, a.size * 32).astype(np.float64).reshape(32, a.size)
+    return r @ a
+
+
+def itn_flipped_params(net):
+    """Indices of the parameters upstream of the backward's first ReLU-boundary flip
+    (test_itn_forward_backward_golden), from the gradients held in net."""
+    f64 = g("itn_fp64")
+    norms = f64["grad64_proj"][:, 0]
+    params = list(net.parameters())
+    for i in reversed(range(len(params))):
+        if norms[i] < 1e-7 * norms.max():
+            continue
+        e64 = rel(proj32(params[i].grad.detach().cpu().numpy()), f64["grad64_proj"][i, 1:])
+        if e64 > max(2.5 * float(f64["ref32_err"][i]), 1e-5):
+            return set(range(i + 1))
+    return set()
+
+
+def test_itn_adam_step_golden(itn_case, dev):
+    """itn.npz["adam1_proj"]: the reference's ImageTransformNet.get_optimizer() Adam
+    step (stransfer/network.py:643-649) after the golden forward/backward."""
+    d, _ = itn_case
+    net = network.ImageTransformNet(T(d["style"], dev), batch_size=2)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)})
+    batch = T(d["batch"], dev)
+    ln = network.StyleNetwork(T(d["style"], dev), T(W.synthetic_image(23, (1, 3, 64, 64)), dev))
+    opt = net.get_optimizer()
+    opt.zero_grad()
+    y = net(batch)
+    ln(y, content_image=batch)
+    (ln.get_total_current_style_loss(100_000) + ln.get_total_current_content_loss(1)
+     + net.get_total_variation_regularization_loss(y)).backward()
+    gnorm = [float(p.grad.norm()) for p in net.parameters()]
+    flipped = itn_flipped_params(net)
+    p0 = [p.detach().clone() for p in net.parameters()]
+    opt.step()
+    errs = []
+    for i, p in enumerate(net.parameters()):
+        assert float((p.detach() - p0[i]).abs().max()) <= 1.001e-3  # |step 1| <= lr
+        if gnorm[i] < 1e-6 * max(gnorm):
+            # zero-gradient biases: step 1 is lr*sign(rounding noise) on both sides
+            continue
+        # Adam step 1 moves every element by ~lr*sign(g).  Downstream of the backward's
+        # ReLU-boundary flip the gradients match the reference to ~1e-3 and so do the
+        # steps; upstream, elements whose gradient sign the flip changes step the other
+        # way (2e-3 each; measured <= 9e-3 of the parameter norm).  A missing or
+        # doubled step or a wrong lr moves a parameter by ~1e-2 of its norm.
+        e = rel(proj(p.detach().cpu().numpy()), d["adam1_proj"][i])
+        errs.append((e, i))
+        assert e < (2e-2 if i in flipped else 2e-3), (i, e)
+    print("ITN Adam step vs reference (rel err, param):", sorted(errs)[-3:],
+          "flip-affected params:", len(flipped))
 
 
 def test_fast_st_trainer_matches_api(itn_case, dev):
