@@ -19,6 +19,7 @@
  *   residual add            <- ResidualBlock.forward `out += residual` :502
  *   upsample nearest x2     <- nn.Upsample(mode='nearest', scale_factor=2) :580-581,592-593
  *   total variation         <- get_total_variation_regularization_loss :621-641
+ *   temporal loss           <- VideoTransformNet.get_temporal_loss :885-903
  */
 #ifndef STX_H_
 #define STX_H_
@@ -304,6 +305,21 @@ size_t stx_tv_ws(int n, int c, int h, int w);
 int stx_tv_loss(const float* y, float* loss, float* grad, float gscale, const float* gscale_dev,
                 int n, int c, int h, int w, float factor, void* ws, size_t ws_bytes,
                 void* stream);
+
+/* Temporal loss of the video network (VideoTransformNet.get_temporal_loss,
+ * stransfer/network.py:885-903), Frobenius norms over the whole batch:
+ *   out[0] = ||y - y_old|| / (||x - x_old|| + 1) * weight,  out[1] = ||y - y_old||,
+ *   out[2] = ||x - x_old||   (one streaming pass, fixed-order reduction)
+ * Backward: grad (+)= (*g_dev or 1) * weight / ((out[2] + 1) * out[1]) * (y - y_old)
+ * (0 where out[1] == 0, torch's norm backward); fwd = the forward's out.
+ * All four tensors hold n floats, 16-byte aligned. */
+size_t stx_temporal_loss_ws(void);
+int stx_temporal_loss(const float* y, const float* y_old, const float* x, const float* x_old,
+                      long long n, float weight, float* out, void* ws, size_t ws_bytes,
+                      void* stream);
+int stx_temporal_loss_bwd(const float* y, const float* y_old, long long n, const float* fwd,
+                          float weight, const float* g_dev, float* grad, int accumulate,
+                          void* stream);
 
 #ifdef __cplusplus
 }

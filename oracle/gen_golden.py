@@ -451,6 +451,100 @@ def case_config1(N, I, iters=50):
             "image_u8": np.asarray(Image.open(path))}
 
 
+def case_video_train(N, H=64, B=3, T=3, epochs=2):
+    """The reference's own VideoTransformNet.video_train (stransfer/network.py:905-1069)
+    for 2 epochs over one batch of B=3 synthetic clips of T=3 frames at 64^2 (B >= 3:
+    the reference logs sample 2 of the batch),
+    starting from fast_st weights (so epoch 0 trains only the 6-channel head conv and
+    epoch 1 everything).  Its VideoDataset / iterate_on_video_batches (imageio +
+    download) are replaced by the pre-conditioned frames; everything else is the
+    reference's code.  Records the closure-loss trace (its DEBUG 'Closure loss'),
+    the two epoch checkpoints, and the same run through the oracle in fp32 (asserted
+    equal) and fp64 (truth for the chaotic multi-step comparison)."""
+    import logging
+    import stransfer.dataset as RD
+    style = t(W.synthetic_image(71, (1, 3, H, H)))
+    frames = np.stack([W.synthetic_image(80 + k, (B, 3, H, H)) for k in range(T)])
+    frames[1:] = 0.8 * frames[:1] + 0.2 * frames[1:]  # temporally coherent clips
+    fr = [t(f) for f in frames]
+    fast = {k: torch.from_numpy(v) for k, v in W.itn_synthetic(ITN_SEED)}
+    head = dict(W.itn_synthetic(4322, in_channels=6))
+    full = dict(fast, **{"0.weight": torch.from_numpy(head["0.weight"]),
+                         "0.bias": torch.from_numpy(head["0.bias"])})
+    orig = (RD.VideoDataset, RD.iterate_on_video_batches)
+    RD.VideoDataset = lambda batch_size=3, **k: [["clips"]]
+    RD.iterate_on_video_batches = lambda batch, max_frames=0: iter(fr)
+    cwd = os.getcwd()
+    work = tempfile.mkdtemp(prefix="stx_vid_")
+    os.chdir(work)
+    os.makedirs("data/models", exist_ok=True)
+    vals = []
+
+    class H_(logging.Handler):
+        def emit(self, rec):
+            if isinstance(rec.msg, str) and rec.msg.startswith("Closure loss") and rec.args:
+                vals.append(float(rec.args[0]))
+    lg = logging.getLogger("StyleTransfer")
+    h, lvl = H_(), lg.level
+    lg.addHandler(h)
+    lg.setLevel(logging.DEBUG)
+    try:
+        torch.manual_seed(0)
+        net = N.VideoTransformNet(style, batch_size=B, fast_transfer_dict=dict(fast))
+        assert net.has_external_weights
+        net.load_state_dict(full)
+        net.video_train(style_name="synth", epochs=epochs)
+        ck = [torch.load(f"data/models/video_st_synth_epoch{e}.pth", weights_only=True)
+              for e in range(epochs)]
+    finally:
+        lg.removeHandler(h)
+        lg.setLevel(lvl)
+        os.chdir(cwd)
+        RD.VideoDataset, RD.iterate_on_video_batches = orig
+    res = {}
+    for dt in (torch.float32, torch.float64):
+        itn = O.image_transform_net(4322, in_channels=6).to(dt)
+        itn.load_state_dict({k: v.to(dt) for k, v in full.items()})
+        ln = O.StyleNetwork(style.to(dt), torch.rand([1, 3, 256, 256]).to(dt),
+                            vgg=O.vgg19_features(VGG_SEED).to(dt))
+        tr = []
+        states = O.video_train(itn, ln, [[f.to(dt) for f in fr]], epochs=epochs,
+                               has_external_weights=True, trace=tr)
+        res[dt] = (tr, states)
+    tr32, st32 = res[torch.float32]
+    close(tr32, vals, rtol=1e-5, what="video_train loss trace")
+    for e in range(epochs):
+        for k in full:
+            close(O.to_np(st32[e][k]), O.to_np(ck[e][k]), rtol=1e-5, what=f"video {e} {k}")
+    keys = list(full)
+    flat = lambda sd: np.concatenate([np.asarray(sd[k].detach().cpu().numpy(), np.float64).ravel()
+                                      for k in keys])  # noqa: E731
+    init = flat(full)
+    n0 = full["0.weight"].numel() + full["0.bias"].numel()
+    out = {"style": style.numpy(), "frames": frames, "losses": np.array(vals),
+           "losses64": np.array(res[torch.float64][0]), "epochs": np.array(epochs),
+           "n_head": np.array(n0)}
+    # epoch 0 moves only the head (n0 values, stored whole); the full update after
+    # the last epoch as 64 fixed random projections (reference fp32 and fp64)
+    out["head0"] = flat(ck[0])[:n0]
+    out["head0_64"] = flat(res[torch.float64][1][0])[:n0]
+    out["upd_proj"] = proj64(flat(ck[-1]) - init)
+    out["upd_proj_64"] = proj64(flat(res[torch.float64][1][-1]) - init)
+    return out
+
+
+def proj64(a, seed=91):
+    """64 fixed random projections of a long vector, in chunks (bounded memory)."""
+    a = np.asarray(a, np.float64).ravel()
+    out = np.zeros(64)
+    step = 1 << 16
+    for o in range(0, a.size, step):
+        blk = a[o:o + step]
+        r = W.hash_normal(seed * 1_000_003 + o, blk.size * 64).astype(np.float64)
+        out += r.reshape(64, blk.size) @ blk
+    return out
+
+
 def case_tv(N):
     y = t(W.synthetic_image(31, (2, 3, 20, 24), normalise=False) * 3 - 1)
     net = N.ImageTransformNet(y[:1], 2)
@@ -499,6 +593,7 @@ def main():
         "itn_fp64": case_itn_fp64,
         "lbfgs": lambda: case_lbfgs(N),
         "config1": lambda: case_config1(N, I),
+        "video_train": lambda: case_video_train(N),
     }
     os.makedirs(GOLDEN, exist_ok=True)
     only = [c for c in args.only.split(",") if c]

@@ -245,6 +245,59 @@ def fast_st_closure(itn, loss_net, batch, style_weight=100_000, content_weight=1
     return total, y
 
 
+def temporal_loss(old_content, old_stylized, current_content, current_stylized, w=1.0):
+    """`VideoTransformNet.get_temporal_loss` — stransfer/network.py:885-903."""
+    return ((current_stylized - old_stylized).norm()
+            / ((current_content - old_content).norm() + 1)) * w
+
+
+def video_train(itn6, loss_net, video_batches, epochs=1, has_external_weights=False,
+                style_weight=100_000, content_weight=1, temporal_weight=0.8, trace=None):
+    """`VideoTransformNet.video_train` — stransfer/network.py:905-1069 (the loop body;
+    tensorboard and checkpoint files dropped): `video_batches` is a list of video
+    batches, each a list of [B, 3, H, W] frame batches.  Epoch 0 trains only the
+    first conv when starting from fast_st weights (:958-971); the closure runs an
+    extra time every 20 iterations (:1030-1037).  Closure losses are appended to
+    `trace`.  Returns the per-epoch state_dicts."""
+    opt = torch.optim.Adam(itn6.parameters())
+    it, states = 0, []
+    for epoch in range(epochs):
+        if epoch == 0 and has_external_weights:
+            for name, p in itn6.named_parameters():
+                if not name.startswith("0."):
+                    p.requires_grad = False
+        if epoch == 1 and has_external_weights:
+            for p in itn6.parameters():
+                p.requires_grad = True
+        for frames in video_batches:
+            old = None
+            for batch in frames:
+                if old is None:
+                    old = [batch, batch]
+                oc, os_ = old
+                x6 = torch.cat([batch, os_], dim=1)
+
+                def closure():
+                    opt.zero_grad()
+                    y = itn6(x6)
+                    loss_net(y, content_image=batch)
+                    total = (loss_net.get_total_current_style_loss(style_weight)
+                             + loss_net.get_total_current_content_loss(content_weight)
+                             + total_variation(y)
+                             + temporal_loss(oc, os_, batch, y, temporal_weight))
+                    old[0], old[1] = batch.detach(), y.detach()
+                    total.backward()
+                    if trace is not None:
+                        trace.append(float(total))
+                    return total
+                if it % 20 == 0:
+                    closure()
+                it += 1
+                opt.step(closure)
+        states.append({k: v.detach().clone() for k, v in itn6.state_dict().items()})
+    return states
+
+
 def adam_reference_step(p, g, m, v, step, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
     """Single-tensor Adam exactly as torch.optim.Adam (the in-container oracle,
     torch 2.10; `stransfer/network.py:403-409`, `:643-649` use its defaults)."""

@@ -101,6 +101,9 @@ SIGNATURES = {
     "stx_upsample2x_bwd": (i32, [vp, vp, i32, i32, i32, vp]),
     "stx_tv_ws": (sz, [i32, i32, i32, i32]),
     "stx_tv_loss": (i32, [vp, vp, vp, f32, vp, i32, i32, i32, i32, f32, vp, sz, vp]),
+    "stx_temporal_loss_ws": (sz, []),
+    "stx_temporal_loss": (i32, [vp, vp, vp, vp, i64, f32, vp, vp, sz, vp]),
+    "stx_temporal_loss_bwd": (i32, [vp, vp, i64, vp, f32, vp, vp, i32, vp]),
 }
 
 _lib = None

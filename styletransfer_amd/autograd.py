@@ -316,6 +316,26 @@ class TVLossFn(torch.autograd.Function):
         return grad, None
 
 
+class TemporalLossFn(torch.autograd.Function):
+    """VideoTransformNet.get_temporal_loss (stransfer/network.py:885-903):
+    ||y - y_old|| / (||x - x_old|| + 1) * w, differentiable in y (the reference's
+    old frames are detached tensors; content frames carry no gradient)."""
+
+    @staticmethod
+    def forward(ctx, y, y_old, x, x_old, weight):
+        y, y_old = _c(y), _c(y_old.detach())
+        out = ops.temporal_loss(y, y_old, _c(x.detach()), _c(x_old.detach()), weight)
+        ctx.save_for_backward(y, y_old, out)
+        ctx.weight = weight
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        y, y_old, out = ctx.saved_tensors
+        dy = ops.temporal_loss_bwd(y, y_old, out, ctx.weight, g=_c(g.reshape(1)))
+        return dy, None, None, None, None
+
+
 class VGGLossFn(torch.autograd.Function):
     """All 7 StyleNetwork losses of a batch in one fused forward/backward:
     returns [style1..5, content, feature] for input x given the style targets and

@@ -1,19 +1,12 @@
-"""`video_st` commands (mirror of stransfer/clis/video_st.py).  Video I/O needs
-imageio, which this image lacks; the per-frame network is VideoTransformNet
-(a "next" row)."""
+"""`video_st` commands (mirror of stransfer/clis/video_st.py:11-87).  Decoding
+video files needs imageio, which this image lacks; frame directories and .npy
+frame arrays work without it."""
 import click
 
 
 @click.group()
 def video_st():
     """Video Style Transfer"""
-
-
-def _need_imageio():
-    try:
-        import imageio  # noqa: F401
-    except ImportError as e:
-        raise click.ClickException("video_st needs imageio (not installed in this image)") from e
 
 
 @video_st.command()
@@ -24,11 +17,37 @@ def _need_imageio():
 @click.option("-sw", "--style-weight", default=100_000)
 @click.option("-tw", "--temporal-weight", default=0.8)
 @click.option("--use-pretrained-fast-st", is_flag=True)
+@click.option("--synthetic", default=0, type=int,
+              help="Train on N synthetic clips instead of data/video/ (no network here)")
 def train(style_image_path, epochs, batch_size, content_weight, style_weight, temporal_weight,
-          use_pretrained_fast_st):
-    """Train the video style transfer network."""
-    _need_imageio()
-    raise click.ClickException("video_st train is not implemented yet (SURVEY.md §8f row 1)")
+          use_pretrained_fast_st, synthetic):
+    """Train the video style transfer network (checkpoint per epoch in data/models/).
+
+    Videos come from data/video/: video files (need imageio), directories of frames
+    or .npy [T, H, W, 3] uint8 arrays."""
+    import os
+
+    from .. import c_logging, constants, dataset, img_utils, network
+    log = c_logging.get_logger()
+    style_name = style_image_path.split("/")[-1]
+    log.info("Training video style transfer network with style name: %s", style_name)
+    ft = None
+    if use_pretrained_fast_st:
+        log.info("Trying to load pretrained fast ST weights")
+        try:
+            ft = network._load_latest_model_weigths("fast_st", style_name)
+        except AssertionError:
+            log.warning("Couldn't load pretrained weights")
+    style_image = img_utils.image_loader(os.path.join(constants.PROJECT_ROOT_PATH,
+                                                      style_image_path))
+    net = network.VideoTransformNet(style_image, batch_size, fast_transfer_dict=ft)
+    loader = None
+    if synthetic:
+        clips = [dataset.synthetic_video(16, constants.IMSIZE, seed=i) for i in range(synthetic)]
+        loader = dataset.VideoDataset(videos=clips, batch_size=batch_size)
+    net.video_train(style_name=style_name, epochs=epochs, style_weight=style_weight,
+                    content_weight=content_weight, temporal_weight=temporal_weight,
+                    video_loader=loader)
 
 
 @video_st.command()

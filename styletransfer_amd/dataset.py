@@ -101,3 +101,69 @@ def get_synthetic_loader(batch_size=4, n_train=64, n_test=8, size=None, seed=0, 
     train = _train_loader(SyntheticImageDataset(n_train, size, seed), batch_size, shard,
                           shuffle=shuffle, seed=seed)
     return test, train
+
+
+# ------------------------------------------------------------------------------ video
+VIDEO_SOURCE_EXTS = (".mp4", ".avi", ".mov", ".mkv", ".gif", ".webm", ".npy")
+
+
+def make_batches(items, batch_size):
+    """Consecutive chunks of `batch_size` (stransfer/dataset.py make_batches)."""
+    return [items[i:i + batch_size] for i in range(0, len(items), batch_size)]
+
+
+class VideoDataset:
+    """Batches of videos (stransfer/dataset.py:200-277).  The reference downloads four
+    sample videos into data/video/ and opens each with imageio; here every entry of
+    data/video/ (or of `videos`) is a video source video.iterate_frames reads: a
+    video file (needs imageio), a directory of frame images or a .npy [T, H, W, 3]
+    uint8 array (or an in-memory array).  Iterating yields, per batch, one frame
+    reader per video; a trailing partial batch is dropped, as the reference does."""
+
+    def __init__(self, videos=None, data_limit=None, batch_size=3, imsize=None,
+                 max_frames=90 * 24):
+        if videos is None:
+            root = os.path.join(constants.PROJECT_ROOT_PATH, VIDEO_DATA_PATH)
+            names = sorted(os.listdir(root)) if os.path.isdir(root) else []
+            videos = [os.path.join(root, n) for n in names
+                      if n.lower().endswith(VIDEO_SOURCE_EXTS) or
+                      os.path.isdir(os.path.join(root, n))]
+            if not videos:
+                raise FileNotFoundError(
+                    f"No videos under {root}. The reference downloads its sample videos on "
+                    "demand; this build has no network access -- place videos, frame "
+                    "directories or .npy frame arrays there.")
+        self.videos = list(videos)[:data_limit] if data_limit else list(videos)
+        if batch_size > len(self.videos):
+            LOGGER.warning("The batch size is larger than the amount of videos in the video "
+                           "set. Will use complete set as a batch of size %d", len(self.videos))
+            batch_size = len(self.videos)
+        self.batch_size = batch_size
+        self.imsize, self.max_frames = imsize, max_frames
+        self.video_paths = make_batches(self.videos, self.batch_size)
+        if self.video_paths and len(self.video_paths[-1]) != self.batch_size:
+            self.video_paths = self.video_paths[:-1]
+
+    def __len__(self):
+        return len(self.video_paths)
+
+    def __iter__(self):
+        from . import video
+        for group in self.video_paths:
+            yield [video.iterate_frames(v, self.max_frames, self.imsize) for v in group]
+
+
+def iterate_on_video_batches(batch, max_frames=90 * 24):
+    """One [B, 3, H, W] frame batch per time step: frame t of every video in the batch,
+    until the shortest video ends (stransfer/dataset.py:280-311)."""
+    for _, frames in zip(range(max_frames), zip(*batch)):
+        yield torch.cat([f.cpu() for f in frames], dim=0)
+
+
+def synthetic_video(n_frames=8, size=64, seed=0, shift=1):
+    """A [T, size, size, 3] uint8 clip: one seeded image translated by `shift` pixels a
+    frame (temporally coherent content for video_train smoke runs and tests)."""
+    import numpy as np
+    base = W.synthetic_image(seed, (1, 3, size, size + shift * n_frames), normalise=False)[0]
+    base = (np.clip(base, 0, 1) * 255).astype(np.uint8).transpose(1, 2, 0)
+    return np.stack([base[:, t * shift:t * shift + size] for t in range(n_frames)])

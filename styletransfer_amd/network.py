@@ -545,9 +545,10 @@ class ImageTransformNet(nn.Sequential):
 
 
 class VideoTransformNet(ImageTransformNet):
-    """stransfer/network.py:835-903: 6-channel first conv ([frame, previous
-    stylised frame]); temporal loss; process_video on the graph-captured per-frame
-    engine (video.py).  video_train (COCO-like video dataset) stays a next row."""
+    """stransfer/network.py:835-1158: 6-channel first conv ([frame, previous
+    stylised frame]); temporal loss (one fused HIP reduction); video_train on
+    train.VideoTrainer; process_video on the graph-captured per-frame engine
+    (video.py)."""
 
     def __init__(self, style_image: torch.Tensor, batch_size=4, fast_transfer_dict=None):
         super().__init__(style_image, batch_size)
@@ -578,6 +579,57 @@ class VideoTransformNet(ImageTransformNet):
 
     def get_temporal_loss(self, old_content, old_stylized, current_content, current_stylized,
                           temporal_weight=1) -> torch.Tensor:
-        change_in_style = (current_stylized - old_stylized).norm()
-        change_in_content = (current_content - old_content).norm()
-        return (change_in_style / (change_in_content + 1)) * temporal_weight
+        """||stylized - old_stylized|| / (||content - old_content|| + 1) * w
+        (stransfer/network.py:885-903), differentiable in current_stylized."""
+        return A.TemporalLossFn.apply(current_stylized, old_stylized, current_content,
+                                      old_content, float(temporal_weight))
+
+    def video_train(self, style_name="nsp", epochs=50, temporal_weight=0.8, style_weight=100_000,
+                    feature_weight=1, content_weight=1, video_loader=None):
+        """stransfer/network.py:905-1069 on train.VideoTrainer.  `video_loader`
+        overrides dataset.VideoDataset(batch_size=self.batch_size) (an iterable of
+        per-batch frame readers, e.g. VideoDataset(videos=[...]))."""
+        from .train import VideoTrainer
+        tb_writer = get_tensorboard_writer(f"runs/video-style-transfer_{style_name}")
+        video_folder = f"video_samples_{style_name}/"
+        shutil.rmtree(video_folder, ignore_errors=True)
+        os.makedirs(video_folder, exist_ok=True)
+        trainer = VideoTrainer(self, self.style_image, style_weight=style_weight,
+                               content_weight=content_weight, temporal_weight=temporal_weight)
+        LOGGER.info('Training video network with "%s" optimizer', type(trainer.opt_head))
+        iteration = 0
+        video_loader = video_loader if video_loader is not None else \
+            dataset.VideoDataset(batch_size=self.batch_size)
+        for epoch in range(epochs):
+            if epoch == 0 and self.has_external_weights:
+                LOGGER.info("Freezing weights imported from fast transfer network for the "
+                            "first epoch")
+                trainer.set_frozen(True)
+            if epoch == 1 and self.has_external_weights:
+                LOGGER.info("Unfreezing all weights")
+                trainer.set_frozen(False)
+            ckpt = f"data/models/video_st_{style_name}_epoch{epoch}.pth"
+            if os.path.isfile(ckpt):
+                self.load_state_dict(adaptive_torch_load(ckpt))
+                continue
+            LOGGER.info("Starting epoch %d", epoch)
+            for video_batch in video_loader:
+                trainer.reset_sequence()
+                for batch in dataset.iterate_on_video_batches(video_batch):
+                    batch = batch.to(trainer.device, torch.float32).contiguous()
+                    if iteration % 20 == 0:
+                        total = trainer.evaluate(batch)
+                        tb_writer.add_scalar("data/fst_train_loss", total, iteration)
+                        LOGGER.info("Epoch: %d\tBatch Loss: %.4f", epoch, float(total))
+                    if iteration % 50 == 0 and not isinstance(tb_writer, _NullWriter):
+                        old = trainer.old[1] if trainer.old is not None else batch
+                        with torch.no_grad():
+                            img = torch.clamp(self(torch.cat([batch, old], dim=1)), 0, 255)
+                        k = min(2, img.shape[0] - 1)  # the reference logs sample 2
+                        tb_writer.add_image("data/fst_images",
+                                            img_utils.concat_images(img[k], batch[k]), iteration)
+                    iteration += 1
+                    trainer.step(batch)
+            os.makedirs("data/models", exist_ok=True)
+            torch.save(self.state_dict(), ckpt)
+        return trainer

@@ -22,6 +22,7 @@ __all__ = [
     "bias_grad", "gram", "style_loss", "gram_bwd", "mse", "diff_scale", "loss_combine",
     "maxpool2x2", "maxpool2x2_bwd", "relupool_bwd", "relu", "relu_bwd", "adam_step",
     "instnorm_fwd", "instnorm_bwd", "upsample2x", "upsample2x_bwd", "tv_loss",
+    "temporal_loss", "temporal_loss_bwd",
 ]
 
 
@@ -596,3 +597,31 @@ def tv_loss(y, factor=1e-6, grad=None, gscale=1.0, gscale_dev=None, out=None):
     check(L.stx_tv_loss(y.data_ptr(), out.data_ptr(), _p(grad), float(gscale), _p(gscale_dev),
                         n, c, h, w, float(factor), wp, wn, _stream()), "stx_tv_loss")
     return out
+
+
+# ----------------------------------------------------------------------- temporal loss
+def temporal_loss(y, y_old, x, x_old, weight=1.0, out=None):
+    """[loss, ||y - y_old||, ||x - x_old||] (device [3]), loss =
+    ||y - y_old|| / (||x - x_old|| + 1) * weight (get_temporal_loss)."""
+    for t, nm in ((y, "y"), (y_old, "y_old"), (x, "x"), (x_old, "x_old")):
+        _req(t, nm)
+    assert y.numel() == y_old.numel() == x.numel() == x_old.numel(), \
+        (y.shape, y_old.shape, x.shape, x_old.shape)
+    if out is None:
+        out = torch.empty(3, device=y.device, dtype=torch.float32)
+    L = lib()
+    wp, wn = WS.get(L.stx_temporal_loss_ws(), y.device)
+    check(L.stx_temporal_loss(y.data_ptr(), y_old.data_ptr(), x.data_ptr(), x_old.data_ptr(),
+                              y.numel(), float(weight), out.data_ptr(), wp, wn, _stream()),
+          "stx_temporal_loss")
+    return out
+
+
+def temporal_loss_bwd(y, y_old, fwd, weight=1.0, g=None, grad=None, accumulate=False):
+    """d loss / d y of temporal_loss (fwd: its output), times the device scalar g."""
+    if grad is None:
+        grad = torch.empty_like(y)
+    check(lib().stx_temporal_loss_bwd(y.data_ptr(), y_old.data_ptr(), y.numel(), fwd.data_ptr(),
+                                      float(weight), _p(g), grad.data_ptr(), int(accumulate),
+                                      _stream()), "stx_temporal_loss_bwd")
+    return grad

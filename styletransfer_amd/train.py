@@ -171,3 +171,76 @@ class FastStTrainer:
     def evaluate(self, batch: torch.Tensor) -> torch.Tensor:
         batch = batch.to(self.device, torch.float32).contiguous()
         return self._total(batch, self.itn(batch))
+
+
+class VideoTrainer(FastStTrainer):
+    """One `video_train` step of VideoTransformNet (stransfer/network.py:905-1069):
+
+        y = net(cat([batch, old_stylised], dim=1))
+        total = style_weight*style + content_weight*content + TV(y)
+                + ||y - old_stylised|| / (||batch - old_content|| + 1) * temporal_weight
+        total.backward(); Adam;  (old_content, old_stylised) <- (batch, y)
+
+    on the same flat-buffer machinery as FastStTrainer (the temporal term is one
+    fused HIP reduction, autograd.TemporalLossFn).  A new video batch starts with
+    old = (batch, batch) (reset_sequence).  The reference freezes every parameter
+    but the first conv's during epoch 0 when it starts from fast_st weights: Adam
+    then keeps no state for the frozen tensors, so here the flat buffers are split
+    into two Adam instances (the 6-channel head conv, the rest) whose step counters
+    advance independently -- the same bias correction as torch's per-parameter
+    state."""
+
+    def __init__(self, net, style_image, style_weight=100_000, content_weight=1,
+                 temporal_weight=0.8, lr=1e-3, vgg_weights=None, tv_factor=1e-6):
+        super().__init__(net, style_image, style_weight=style_weight,
+                         content_weight=content_weight, lr=lr, vgg_weights=vgg_weights,
+                         tv_factor=tv_factor)
+        self.tw = float(temporal_weight)
+        head = [net[0].weight, net[0].bias]
+        assert all(a is b for a, b in zip(head, self.params[:2])), "first conv must lead"
+        n0 = sum(p.numel() for p in head)
+        self.opt_head = FlatAdam(self.flat[:n0], self.flat_grad[:n0], lr=lr, params=head)
+        self.opt_rest = FlatAdam(self.flat[n0:], self.flat_grad[n0:], lr=lr,
+                                 params=self.params[2:])
+        self.frozen = False
+        self.old = None
+
+    def set_frozen(self, frozen: bool):
+        """Freeze (requires_grad=False, no Adam step) every parameter but the head's."""
+        self.frozen = bool(frozen)
+        for name, p in self.itn.named_parameters():
+            if not name.startswith("0."):
+                p.requires_grad = not self.frozen
+
+    def reset_sequence(self):
+        self.old = None
+
+    def _video_total(self, batch, y, old_c, old_s):
+        return self._total(batch, y) + A.TemporalLossFn.apply(y, old_s, batch, old_c, self.tw)
+
+    def _inputs(self, batch):
+        batch = batch.to(self.device, torch.float32).contiguous()
+        old_c, old_s = self.old if self.old is not None else (batch, batch)
+        return batch, old_c, old_s, torch.cat([batch, old_s], dim=1)
+
+    def step(self, batch: torch.Tensor) -> torch.Tensor:
+        batch, old_c, old_s, x6 = self._inputs(batch)
+        self.flat_grad.zero_()
+        ops.ARENA.begin(self.device)
+        try:
+            y = self.itn(x6)
+            total = self._video_total(batch, y, old_c, old_s)
+            total.backward()
+        finally:
+            ops.ARENA.end()
+        self.old = (batch, y.detach())
+        self.opt_head.step()
+        if not self.frozen:
+            self.opt_rest.step()
+        return total.detach()
+
+    @torch.no_grad()
+    def evaluate(self, batch: torch.Tensor) -> torch.Tensor:
+        """The closure's loss for `batch` without a step (the sequence is unchanged)."""
+        batch, old_c, old_s, x6 = self._inputs(batch)
+        return self._video_total(batch, self.itn(x6), old_c, old_s)

@@ -85,7 +85,7 @@ class FrameEngine:
         self.prev = self.x6[:, 3:]
         self.prev_frame = torch.zeros((n, 3, h, w), device=self.dev, dtype=torch.float32)
         self.out = None
-        # device scalars: ||y_t - y_{t-1}||^2, ||x_t - x_{t-1}||^2, temporal loss
+        # device scalars: temporal loss (weight 1), ||y_t - y_{t-1}||, ||x_t - x_{t-1}||
         self.scal = torch.zeros(4, device=self.dev, dtype=torch.float32)
         self.graph = None
         self.use_graph = graph
@@ -96,13 +96,10 @@ class FrameEngine:
             y = self.net(self.x6)
         if self.out is None:
             self.out = torch.empty_like(y)
-            self.dy = torch.empty_like(y)
-            self.dx = torch.empty_like(y)
-        # temporal-loss terms of this step (stransfer/network.py:885-903)
-        ops.diff_scale(y, self.prev, 1.0, out=self.dy)
-        ops.diff_scale(self.frame, self.prev_frame, 1.0, out=self.dx)
-        ops.vdot(self.dy, self.dy, self.scal[0:1])
-        ops.vdot(self.dx, self.dx, self.scal[1:2])
+        # temporal-loss terms of this step (stransfer/network.py:885-903): one fused
+        # pass, [loss(w=1), ||y - y_prev||, ||x - x_prev||]
+        ops.temporal_loss(y, self.prev, self.frame, self.prev_frame, 1.0,
+                          out=self.scal[:3])
         self.out.copy_(y)
         self.prev.copy_(y)                 # next step's "old stylised" channels
         self.prev_frame.copy_(self.frame)
@@ -129,8 +126,7 @@ class FrameEngine:
 
     def temporal_loss(self, temporal_weight=1.0) -> float:
         """||y_t - y_{t-1}|| / (||x_t - x_{t-1}|| + 1) * w of the last step."""
-        dy, dx = float(self.scal[0]), float(self.scal[1])
-        return float(np.sqrt(dy) / (np.sqrt(dx) + 1.0) * temporal_weight)
+        return float(self.scal[0]) * temporal_weight
 
 
 def process_video(net, video_path, style_name="nsp", working_dir="workdir/", out_dir="results/",

@@ -4,10 +4,13 @@ VideoTransformNet.process_video (stransfer/network.py:1071-1158): frame t runs
 through the 6-channel ImageTransformNet on cat([frame_t, out_{t-1}]) (frame 0 with
 itself).  The graph-captured FrameEngine must reproduce that recurrence; the
 temporal loss is ||dy|| / (||dx|| + 1) (stransfer/network.py:885-903)."""
+import os
+
 import numpy as np
 import pytest
 import torch
 
+from conftest import GOLDEN
 from oracle import reference_cpu as O
 from styletransfer_amd import network, video
 from styletransfer_amd import weights as W
@@ -74,3 +77,102 @@ def test_frame_engine_replay_after_idle(dev):
             outs[graph].append(eng.step(f.to(dev)).cpu())
     for a, b in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
+
+
+def test_temporal_loss_vs_oracle(dev):
+    """get_temporal_loss (one fused HIP reduction) and its gradient vs the oracle's
+    torch expression (stransfer/network.py:885-903) in fp64."""
+    shp = (3, 3, 40, 48)
+    ys = [torch.from_numpy(W.synthetic_image(950 + i, shp)) for i in range(4)]
+    net = network.VideoTransformNet(torch.rand([3, 8, 8]))
+    y = ys[0].to(dev).requires_grad_()
+    loss = net.get_temporal_loss(ys[1].to(dev), ys[2].to(dev), ys[3].to(dev), y, 0.8)
+    loss.backward()
+    yd = ys[0].double().requires_grad_()
+    ref = O.temporal_loss(ys[1].double(), ys[2].double(), ys[3].double(), yd, 0.8)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) <= 1e-6 * float(ref)
+    assert rel(y.grad, yd.grad) < 1e-6
+    # zero change in the stylised frames: loss 0, gradient 0 (torch's norm backward)
+    z = ys[2].to(dev).clone().requires_grad_()
+    l0 = net.get_temporal_loss(ys[1].to(dev), ys[2].to(dev), ys[3].to(dev), z)
+    l0.backward()
+    assert float(l0) == 0.0 and float(z.grad.abs().max()) == 0.0
+
+
+class _Clips:
+    """video_loader for video_train: per epoch one batch of B frame readers over the
+    fixture's pre-conditioned frames [T, B, 3, H, W]."""
+
+    def __init__(self, frames):
+        self.frames = frames
+
+    def __iter__(self):
+        T, B = self.frames.shape[:2]
+        yield [iter([torch.from_numpy(self.frames[t, b:b + 1]) for t in range(T)])
+               for b in range(B)]
+
+
+def test_video_train_reference(dev, tmp_path, monkeypatch):
+    """The reference's own VideoTransformNet.video_train (video_train.npz: 2 epochs from
+    fast_st weights over 3 clips x 3 frames at 64^2 -- epoch 0 trains only the
+    6-channel head, epoch 1 everything).
+
+    * losses before any step and after head-only steps match the reference to 1e-4;
+    * epoch 0 leaves every non-head parameter bit-identical (frozen) and moves the
+      head like the reference: against the fp64 run, no further than 5x the fp32
+      reference;
+    * epoch 1 (all 1.68M parameters taking ~lr*sign(g) Adam steps) is chaotic in
+      fp32 -- the reference's own update is 54 % from its fp64 run -- so its losses
+      are held to 5x the reference's distance from fp64, and the checkpoints must
+      carry the reference's names and keys."""
+    d = np.load(os.path.join(GOLDEN, "video_train.npz"))
+    monkeypatch.chdir(tmp_path)
+    sd = {k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)}
+    head = dict(W.itn_synthetic(4322, in_channels=6))
+    full = dict(sd, **{"0.weight": torch.from_numpy(head["0.weight"]),
+                       "0.bias": torch.from_numpy(head["0.bias"])})
+    style = torch.from_numpy(d["style"]).to(dev)
+    net = network.VideoTransformNet(style, batch_size=3, fast_transfer_dict=dict(sd))
+    assert net.has_external_weights
+    net.load_state_dict(full)
+    # the closure losses, in the reference's order: evaluate() is the extra closure
+    # call every 20 iterations, step() the optimiser's
+    from styletransfer_amd import train as T
+    vals = []
+    orig_step, orig_eval = T.VideoTrainer.step, T.VideoTrainer.evaluate
+
+    def step(self, batch):
+        out = orig_step(self, batch)
+        vals.append(float(out))
+        return out
+
+    def evaluate(self, batch):
+        out = orig_eval(self, batch)
+        vals.append(float(out))
+        return out
+    monkeypatch.setattr(T.VideoTrainer, "step", step)
+    monkeypatch.setattr(T.VideoTrainer, "evaluate", evaluate)
+    net.video_train(style_name="synth", epochs=int(d["epochs"]), video_loader=_Clips(d["frames"]))
+    ref, r64 = d["losses"], d["losses64"]
+    got = np.array(vals)
+    assert len(got) == len(ref), (got, ref)
+    e_ref = np.abs(got - ref) / np.abs(ref)
+    print("video_train losses:", got, "\n  rel err vs reference:", e_ref)
+    assert e_ref[:5].max() < 1e-4                      # before / after head-only steps
+    e64 = np.abs(got - r64) / np.abs(r64)
+    e32 = np.abs(ref - r64) / np.abs(r64)
+    assert (e64[5:] <= np.maximum(5.0 * e32[5:], 1e-5)).all(), (e64, e32)
+    ck = [torch.load(tmp_path / "data" / "models" / f"video_st_synth_epoch{e}.pth",
+                     weights_only=True) for e in range(int(d["epochs"]))]
+    assert list(ck[0]) == list(full)
+    n0 = int(d["n_head"])
+    flat = lambda s: torch.cat([s[k].reshape(-1).cpu().double() for k in full])  # noqa: E731
+    init = flat(full)
+    c0 = flat(ck[0])
+    assert torch.equal(c0[n0:], init[n0:])             # frozen during epoch 0
+    h, h32, h64 = c0[:n0], torch.from_numpy(d["head0"]), torch.from_numpy(d["head0_64"])
+    eh = float((h - h64).norm() / (h64 - init[:n0]).norm())
+    er = float((h32 - h64).norm() / (h64 - init[:n0]).norm())
+    print(f"video_train head after epoch 0 vs fp64: hip {eh:.2e}, reference {er:.2e}")
+    assert eh <= max(5.0 * er, 1e-5)
