@@ -20,6 +20,8 @@
  *   upsample nearest x2     <- nn.Upsample(mode='nearest', scale_factor=2) :580-581,592-593
  *   total variation         <- get_total_variation_regularization_loss :621-641
  *   temporal loss           <- VideoTransformNet.get_temporal_loss :885-903
+ *   image conditioning      <- img_utils.image_loader_transform stransfer/img_utils.py:13-44
+ *                              (COCO loader stransfer/dataset.py:141-197)
  */
 #ifndef STX_H_
 #define STX_H_
@@ -320,6 +322,31 @@ int stx_temporal_loss(const float* y, const float* y_old, const float* x, const 
 int stx_temporal_loss_bwd(const float* y, const float* y_old, long long n, const float* fwd,
                           float weight, const float* g_dev, float* grad, int accumulate,
                           void* stream);
+
+/* Image conditioning (img_utils.image_loader_transform, stransfer/img_utils.py:13-44)
+ * of a batch of decoded 8-bit RGB images on the GPU: centre crop, Pillow-exact
+ * BILINEAR resize to size x size (its 8-bit fixed-point two-pass resampler: output
+ * bytes equal PIL's), ToTensor (/255) and (x - mean) / std -> out [b][3][size][size].
+ * src: device buffer of packed HWC uint8 images; meta: device array of b entries;
+ * coef: device int tables, per axis [out][2] bounds (first tap, taps) followed by
+ * [out][k] coefficients, built with stx_resample_coeffs (host function: returns the
+ * kernel size k, or with NULL outputs only the size query); mean/std: HOST arrays
+ * of 3; tmp: device workspace holding every image's horizontally resampled rows
+ * (max_rows = the largest y1 - y0; 0 when no image needs the horizontal pass). */
+typedef struct {
+  long long offset;        /* byte offset of the image in src */
+  int h, w;                /* decoded size */
+  int top, left;           /* centre-crop origin */
+  int y0, y1;              /* crop rows read by the vertical pass */
+  int resize_w, resize_h;  /* passes needed (0: the crop side already equals size) */
+  int xcoef, ycoef;        /* int offsets of the two axis tables in coef */
+  int xk, yk;              /* their kernel sizes */
+  long long tmp_offset;    /* byte offset of this image's rows in tmp ([rows][size][3]) */
+} stx_image_meta;
+int stx_resample_coeffs(int in_size, int out_size, int* bounds, int* kk, int kk_stride);
+int stx_image_condition(const void* src, const stx_image_meta* meta, int b, int max_rows,
+                        const int* coef, int size, const float* mean, const float* std_,
+                        float* out, void* tmp, size_t tmp_bytes, void* stream);
 
 #ifdef __cplusplus
 }

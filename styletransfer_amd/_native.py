@@ -40,6 +40,13 @@ class ConvParams(C.Structure):
     ]
 
 
+class ImageMeta(C.Structure):
+    """Mirror of `stx_image_meta` (include/stx.h)."""
+    _fields_ = [("offset", i64), ("h", i32), ("w", i32), ("top", i32), ("left", i32),
+                ("y0", i32), ("y1", i32), ("resize_w", i32), ("resize_h", i32),
+                ("xcoef", i32), ("ycoef", i32), ("xk", i32), ("yk", i32), ("tmp_offset", i64)]
+
+
 class LossParts(C.Structure):
     """Mirror of `stx_loss_parts` (include/stx.h)."""
     _fields_ = [("parts", vp * 8), ("nparts", i32 * 8), ("inv", f32 * 8), ("k", i32)]
@@ -101,6 +108,8 @@ SIGNATURES = {
     "stx_upsample2x_bwd": (i32, [vp, vp, i32, i32, i32, vp]),
     "stx_tv_ws": (sz, [i32, i32, i32, i32]),
     "stx_tv_loss": (i32, [vp, vp, vp, f32, vp, i32, i32, i32, i32, f32, vp, sz, vp]),
+    "stx_resample_coeffs": (i32, [i32, i32, vp, vp, i32]),
+    "stx_image_condition": (i32, [vp, vp, i32, i32, vp, i32, vp, vp, vp, vp, sz, vp]),
     "stx_temporal_loss_ws": (sz, []),
     "stx_temporal_loss": (i32, [vp, vp, vp, vp, i64, f32, vp, vp, sz, vp]),
     "stx_temporal_loss_bwd": (i32, [vp, vp, i64, vp, f32, vp, vp, i32, vp]),
@@ -130,7 +139,12 @@ def lib():
                 L = C.CDLL(LIB_PATH)
             except OSError as e:  # pragma: no cover
                 raise NativeError(f"failed to load {LIB_PATH}: {e}") from e
+            # STX_LIB_PARTIAL=1: an older library build for same-box A/B timing
+            # (tools/ab_conv.sh) may lack newer entry points
+            partial = os.environ.get("STX_LIB_PARTIAL") == "1"
             for name, (res, args) in SIGNATURES.items():
+                if partial and not hasattr(L, name):
+                    continue
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args

@@ -269,6 +269,20 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
+  {  // experiment: stagger co-resident blocks (mode in tiles_x's top byte)
+    const int mode = tiles_x >> 24;
+    tiles_x &= 0xffffff;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    bool late = false;
+    if (mode == 1) late = bid & 1;
+    else if (mode == 2) late = (bid >> 3) & 1;
+    else if (mode == 3) late = (bid >> 8) & 1;
+    else if (mode == 4) late = (blockIdx.x >> 4) & 1;
+    if (late) {
+      __builtin_amdgcn_s_sleep(31);
+      __builtin_amdgcn_s_sleep(31);
+    }
+  }
 
   const int tile = blockIdx.x;
   const int ty0 = (tile / tiles_x) * C::TH, tx0 = (tile % tiles_x) * TW;
@@ -390,45 +404,58 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
     if (!(DBG & 2) || chunk == 0) store();
     __syncthreads();
     if (chunk + 1 < nchunks && !(DBG & 2)) fetch(chunk + 1);  // in flight across the MFMA loop
-    f16x8 ra[2][2][2], rb[2][NI][2];           // [slot][tile][hi/lo]
-    auto rd = [&](int tap, f16x8 (&a)[2][2], f16x8 (&b)[NI][2]) {
+    // Operand reads run one product phase ahead of their use: a tap's three phases
+    // (hi*hi, hi*lo, lo*hi; 2 x NI MFMAs each) are each preceded by the reads the NEXT
+    // phase needs (B lo, then A lo, then the next tap's A hi + B hi), so every LDS
+    // read has a whole phase of MFMAs (>= 4 x 32 cycles) to land, with at most
+    // 2 x (2 + NI) operand registers live -- the register budget of two waves per SIMD
+    // leaves no room for a whole second tap of operands.
+    auto rdA = [&](int tap, int P, f16x8 (&a)[2]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        a[i] = *reinterpret_cast<const f16x8*>(abase + (tap * 4 * BM + P * 2 * BM + i * 32) * 16);
+    };
+    auto rdB = [&](int tap, int P, f16x8 (&b)[NI]) {
       const int kh = tap / 3, kw = tap % 3;
 #pragma unroll
+      for (int j = 0; j < NI; ++j)
+        b[j] = *reinterpret_cast<const f16x8*>(bbase[j] + (P * C::NITP + kh * C::RW + kw) * 16);
+    };
+    auto phase = [&](const f16x8 (&a)[2], const f16x8 (&b)[NI]) {
+#pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int P = 0; P < 2; ++P)
-          a[i][P] = *reinterpret_cast<const f16x8*>(abase + (tap * 4 * BM + P * 2 * BM + i * 32) * 16);
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int P = 0; P < 2; ++P)
-          b[j][P] = *reinterpret_cast<const f16x8*>(bbase[j] +
-                                                    (P * C::NITP + kh * C::RW + kw) * 16);
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
     };
-    rd(0, ra[0], rb[0]);
+    f16x8 ahi[2], alo[2], bhi[NI], blo[NI];
+    rdA(0, 0, ahi);
+    rdB(0, 0, bhi);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      const int s = tap & 1;
-      if (tap + 1 < 9) rd(tap + 1, ra[s ^ 1], rb[s ^ 1]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][i][0], rb[s][j][0], acc[i][j],
-                                                             0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][i][0], rb[s][j][1], acc[i][j],
-                                                             0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][i][1], rb[s][j][0], acc[i][j],
-                                                             0, 0, 0);
+      rdB(tap, 1, blo);
+      __builtin_amdgcn_sched_group_barrier(0x100, NI, 0);      // the reads, then
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);  // the phase's MFMAs
+      phase(ahi, bhi);
+      rdA(tap, 1, alo);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
+      phase(ahi, blo);
+      f16x8 nah[2], nbh[NI];
+      if (tap + 1 < 9) {
+        rdA(tap + 1, 0, nah);
+        rdB(tap + 1, 0, nbh);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 + NI, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
+      phase(alo, bhi);
       __builtin_amdgcn_sched_barrier(0);
+      if (tap + 1 < 9) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ahi[i] = nah[i];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) bhi[j] = nbh[j];
+      }
     }
   }
   if ((DBG & 1) && P2 != 2) {
@@ -496,6 +523,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
                                            reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
     return;
   }
+  if (conv_epilogue_plain<TW, NI, RP>(acc, p, et, descale)) return;
   conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, false>(acc, p, et, descale, reinterpret_cast<float*>(smem),
                                          reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
 }
@@ -508,11 +536,20 @@ static int dbg_mode() {
   return m;
 }
 
+static int stagger_mode() {
+  static const int m = [] {
+    const char* e = getenv("STX_STAGGER");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
 template <int TW, int LM, int NI>
 static int launch16(const stx_conv_params& p, hipStream_t st) {
   using C = C16<TW, NI, LM == LM_S2 ? 2 : 1>;
-  const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
-  dim3 grid(tiles_x * tiles_y, cdiv(p.cout, C::BM), p.n);
+  const int tiles_x0 = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
+  const int tiles_x = tiles_x0 | (stagger_mode() << 24);
+  dim3 grid(tiles_x0 * tiles_y, cdiv(p.cout, C::BM), p.n);
   if constexpr (TW == 64 && LM == STX_IN_RELU && NI == 2) {
     switch (dbg_mode()) {
       case 1: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 1>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");

@@ -68,6 +68,105 @@ __device__ __forceinline__ void block_max_to(float* group, float m) {
   }
 }
 
+// The forward-conv epilogue (no mask, aux, accumulate, acc_scale, unpool or Gram
+// phase -- every VGG / ITN forward launch): v = acc * scale + bias [, relu]; y = v;
+// optional fused ReLU + MaxPool2d output; optional out_amax.  Specialised because the
+// generic epilogue's per-element feature tests and the pooled output's 64-bit
+// address arithmetic cost more VALU issue per wave than the main loop's staging
+// (PMC, conv1_2 fwd @ 512^2: ~3,400 VALU instructions per wave for 432 MFMAs).
+// All stores go through buffer descriptors: a per-lane pixel offset plus a per-
+// register row constant, rows past cout / pixels past the image dropped by the
+// hardware range check.
+template <int TW, int NI, bool ROWPAIR, bool RELU>
+__device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
+                                                         const stx_conv_params& p,
+                                                         const EpiTile& t, float scale) {
+  const size_t plane = (size_t)p.ho * p.wo;
+  const int h = t.h, l32 = t.l32;
+  const int co_w = t.co0 + t.wm * 64;
+  const int rows = max(0, p.cout - co_w);
+  const uint32_t pb = (uint32_t)plane * 4u;
+  const auto ry = make_srd(p.y + ((size_t)t.n * p.cout + co_w) * plane, (uint32_t)rows * pb);
+  uint32_t vo[NI];
+  bool lane_ok[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    int ty, tx;
+    tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
+    const int oy = t.ty0 + ty, ox = t.tx0 + tx;
+    lane_ok[j] = oy < p.ho && ox < p.wo;
+    vo[j] = lane_ok[j] ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
+  }
+  float bias_r[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      bias_r[i][r] = (p.bias && co < p.cout) ? p.bias[co] : 0.f;
+    }
+  // rows past cout exist only in a ragged last 64-row tile: then count per element
+  const bool rows_full = rows >= 64;
+  uint32_t vmax_u = 0u;  // max |v| as IEEE bits: NaN (above inf) propagates
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = i * 32 + (r & 3) + 8 * (r >> 2);
+        float v = fmaf(acc[i][j][r], scale, bias_r[i][r]);
+        if (RELU) v = fmaxf(v, 0.f);
+        buf_st(ry, vo[j] + (uint32_t)row * pb, v);
+        acc[i][j][r] = v;  // kept for the fused pooled output
+        const bool ok = lane_ok[j] && (rows_full || row + 4 * h < rows);
+        if (ok) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
+      }
+    }
+  }
+  if constexpr (ROWPAIR) if (p.pool_out) {
+    // relu(maxpool2x2(y)) = maxpool2x2(relu(y)) -> pool_out [n][cout][ho/2][wo/2]
+    // (torch MaxPool2d floor mode: a window needs both rows and both columns).  On
+    // IEEE bit patterns: relu is max_i32(bits, 0) and the max of non-negative floats
+    // is the unsigned max, under which a NaN (exponent all ones, non-zero mantissa)
+    // beats every number -- so the window max propagates NaN like torch.
+    const int hp = p.ho >> 1, wp = p.wo >> 1;
+    const int py = (t.ty0 + (t.wn >> 1) * 2) >> 1;
+    const int px = (t.tx0 + (t.wn & 1) * 32 + l32) >> 1;
+    const bool ok = py < hp && px < wp && !(l32 & 1);
+    const uint32_t ppb = (uint32_t)hp * (uint32_t)wp * 4u;
+    const auto rp = make_srd(p.pool_out + ((size_t)t.n * p.cout + co_w) * hp * wp,
+                             (uint32_t)rows * ppb);
+    const uint32_t po = ok ? (uint32_t)(4 * h * hp * wp + py * wp + px) * 4u : BUF_OOB;
+    auto rb = [](float v) -> uint32_t {
+      const int b = __float_as_int(v);
+      const uint32_t a = (uint32_t)b & 0x7fffffffu;
+      return a > 0x7f800000u ? a : (uint32_t)max(b, 0);  // NaN stays NaN (sign dropped)
+    };
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t m2 = max(rb(acc[i][0][r]), rb(acc[i][1][r]));
+        const uint32_t m = max(m2, (uint32_t)__shfl_xor((int)m2, 1, 64));
+        const int row = i * 32 + (r & 3) + 8 * (r >> 2);
+        buf_st(rp, po + (uint32_t)row * ppb, __uint_as_float(m));
+      }
+  }
+  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
+}
+
+template <int TW, int NI, bool ROWPAIR>
+__device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const stx_conv_params& p,
+                                                    const EpiTile& t, float scale) {
+  if (p.mask || p.aux || p.accumulate || p.acc_scale || p.up_dp || p.p2_z) return false;
+  if (p.relu_out)
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, true>(acc, p, t, scale);
+  else
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false>(acc, p, t, scale);
+  return true;
+}
+
 template <int BM, int TW, int NPIX, int CIS2, bool ROWPAIR = false, int NI = 2,
           bool HAS_P2 = true>
 // (NI: 32-pixel N-tiles per wave; ROWPAIR needs NI == 2)
@@ -99,19 +198,26 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][NI], const stx_co
           for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
     }
     if (p.mask) {
+      // descriptor at this wave's first row: per-lane pixel offset + per-register row
+      // constant (no 64-bit address math); rows past cout / pixels past the image
+      // read 0 (their outputs are dropped by the final stores anyway)
+      const int co_m = t.co0 + t.wm * 64;
+      const uint32_t mpb = (uint32_t)plane * 4u;
+      const auto rm = make_srd(p.mask + ((size_t)n * p.cout + co_m) * plane,
+                               (uint32_t)max(0, p.cout - co_m) * mpb);
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         int ty, tx;
         tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
-        const int oy = min(t.ty0 + ty, p.ho - 1), ox = min(t.tx0 + tx, p.wo - 1);
-        const size_t pofs = (size_t)oy * p.wo + ox;
+        const int oy = t.ty0 + ty, ox = t.tx0 + tx;
+        const uint32_t mo = (oy < p.ho && ox < p.wo)
+                                ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int co = min(t.co0 + t.wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h,
-                               p.cout - 1);
-            if (!(p.mask[((size_t)n * p.cout + co) * plane + pofs] > 0.f)) acc[i][j][r] = 0.f;
+            const uint32_t row = (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2));
+            if (!(buf_ld(rm, mo + row * mpb) > 0.f)) acc[i][j][r] = 0.f;
           }
       }
     }
@@ -181,6 +287,14 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][NI], const stx_co
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
       }
     }
+  }
+
+  if (HAS_P2 && mask_done && !p.up_dp && !p.aux && !p.accumulate && !p.relu_out &&
+      !p.pool_out) {
+    // data gradient + Gram-backward phase (the Gatys dZ1 / dZ3 launches): bias and
+    // out_amax only
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false>(acc, p, t, 1.f);
+    return;
   }
 
   // ReLU + MaxPool2d(2,2) backward (unpool(up_dp) * (up_z > 0), argmax of the

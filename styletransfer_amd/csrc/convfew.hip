@@ -16,10 +16,14 @@
 // A wave owns 2 output rows x 64 columns (4 N-blocks of 32 pixels) for all cout
 // (MT = cout/32 M-tiles); a block is 4 waves = 8 rows x 64 columns.  Epilogue: bias,
 // optional ReLU, plain stores (128-B rows per half-wave), optional amax group.
+#include <stdlib.h>
+
 #include "common.h"
 #include "conv_epi.h"
 
 namespace stx {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
@@ -124,11 +128,191 @@ __global__ void __launch_bounds__(256, 2) conv_fewin_kernel(stx_conv_params p, i
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
+// ---------------------------------------------------------------------------------
+// The same convolutions on the fp16 hi/lo split MFMA (v_mfma_f32_32x32x16_f16, three
+// products per K=16 step; conv16.hip explains the split).  The scales are block-local:
+// every block computes max|x| over its own input tile and max|W| over the weights
+// before splitting, so no producer has to annotate the input -- each block's outputs
+// depend only on its tile, and the de-scale 2^(ex + ew - 30) is exact.  The input
+// tile is split once into fp16 hi/lo planes in LDS; a lane's B fragment (8 im2col
+// rows k = 16t + 8h + e at its pixel) is 8 16-bit LDS reads per plane at compile-time
+// offsets (one of two per element, by lane half); the A fragments (weights,
+// [t][plane][h][co][8]) are one ds_read_b128 each.  A wave owns 2 output rows x 64
+// columns as 4 N-blocks of 32 pixels and stores each N-block's outputs right after
+// its MFMAs, so the store stream overlaps the next N-block's matrix work.  K = 27
+// (3x3) is 2 steps, K = 243 (9x9) 16: 5x fewer matrix cycles than the fp32 MFMA.
+template <int KS>
+struct Few16 {
+  static constexpr int KK = KS * KS, K = CF_CIN * KK, KST = (K + 15) / 16;
+  static constexpr int RH = CF_TH + KS - 1, RW = CF_TW + KS - 1, RWP = RW + 1;
+  static constexpr int NT = CF_CIN * RH * RWP;        // LDS tile elements per plane
+  static constexpr int NIN = CF_CIN * RH * RW;        // loaded tile elements
+  static constexpr int NR = (NIN + 255) / 256;
+  // LDS offset of im2col row k relative to the pixel's (0, 0) tap, or -1 past K
+  static constexpr int koff(int k) {
+    return k < K ? ((k / KK) * RH + (k % KK) / KS) * RWP + (k % KS) : -1;
+  }
+};
+
+template <int KS, int MT>
+__global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p, int tiles_x) {
+  using F = Few16<KS>;
+  constexpr int KST = F::KST, NCO = 32 * MT;
+  constexpr int NW = KST * 2 * NCO * 8;                // A elements (t, h, co, e)
+  constexpr int NWR = (NW + 255) / 256;
+  __shared__ _Float16 tile16[2][F::NT];
+  __shared__ __attribute__((aligned(16))) _Float16 wa[KST][2][2][NCO][8];  // [t][P][h][co][e]
+  __shared__ float red[8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x, n = blockIdx.z;
+  const int oy0 = ty * CF_TH, ox0 = tx * CF_TW;
+  constexpr int pad = KS / 2;
+  const int plane_in = p.h * p.w;
+  const float* __restrict__ xn = p.x + (size_t)n * CF_CIN * plane_in;
+
+  // input tile (zero halo through the descriptor's range check) and weights into
+  // registers, with their maxima
+  float xv[F::NR], wv[NWR];
+  float mx = 0.f, mw = 0.f;
+  {
+    const auto rx = make_srd(xn, (uint32_t)(CF_CIN * plane_in) * 4u);
+#pragma unroll
+    for (int r = 0; r < F::NR; ++r) {
+      const int i = tid + 256 * r;
+      const int ci = i / (F::RH * F::RW), rr = (i / F::RW) % F::RH, cc = i % F::RW;
+      const int y = oy0 - pad + rr, x = ox0 - pad + cc;
+      const bool ok = i < F::NIN && y >= 0 && y < p.h && x >= 0 && x < p.w;
+      xv[r] = buf_ld(rx, ok ? (uint32_t)(ci * plane_in + y * p.w + x) * 4u : BUF_OOB);
+      mx = fmaxf(mx, fabsf(xv[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < NWR; ++r) {
+      const int u = tid + 256 * r;
+      const int e = u & 7, co = (u >> 3) % NCO, hh = (u / (8 * NCO)) & 1, t = u / (16 * NCO);
+      const int k = 16 * t + 8 * hh + e;
+      const bool ok = u < NW && k < F::K && co < p.cout;
+      wv[r] = ok ? p.wt[(size_t)k * p.cout_pad + co] : 0.f;
+      mw = fmaxf(mw, fabsf(wv[r]));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    mw = fmaxf(mw, __shfl_xor(mw, o, 64));
+  }
+  if (lane == 0) {
+    red[wave] = mx;
+    red[4 + wave] = mw;
+  }
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  mw = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+  int ex = 0, ew = 0;
+  frexpf(mx, &ex);
+  frexpf(mw, &ew);
+  ex = min(max(ex, -60), 60);
+  ew = min(max(ew, -60), 60);
+  const float sx = __builtin_ldexpf(1.f, 15 - ex), sw = __builtin_ldexpf(1.f, 15 - ew);
+  const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
+  // split into the LDS planes
+#pragma unroll
+  for (int r = 0; r < F::NR; ++r) {
+    const int i = tid + 256 * r;
+    if (i < F::NIN) {
+      const int ci = i / (F::RH * F::RW), rr = (i / F::RW) % F::RH, cc = i % F::RW;
+      const int o = (ci * F::RH + rr) * F::RWP + cc;
+      const float v = xv[r] * sx;
+      const _Float16 vh = (_Float16)v;
+      tile16[0][o] = vh;
+      tile16[1][o] = (_Float16)(v - (float)vh);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NWR; ++r) {
+    const int u = tid + 256 * r;
+    if (u < NW) {
+      const int e = u & 7, co = (u >> 3) % NCO, hh = (u / (8 * NCO)) & 1, t = u / (16 * NCO);
+      const float v = wv[r] * sw;
+      const _Float16 vh = (_Float16)v;
+      wa[t][0][hh][co][e] = vh;
+      wa[t][1][hh][co][e] = (_Float16)(v - (float)vh);
+    }
+  }
+  __syncthreads();
+
+  const size_t plane = (size_t)p.ho * p.wo;
+  float* __restrict__ yn = p.y + (size_t)n * p.cout * plane;
+  uint32_t vmax_u = 0u;
+#pragma unroll 1
+  for (int b = 0; b < 4; ++b) {
+    const int row = 2 * wave + (b >> 1), col = 32 * (b & 1) + l32;
+    const int base = row * F::RWP + col;
+    f32x16 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < KST; ++t) {
+      f16x8 bh, bl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int o0 = F::koff(16 * t + e), o1 = F::koff(16 * t + 8 + e);
+        const int o = h ? o1 : o0;
+        const bool ok = o >= 0;
+        const int oo = ok ? o : 0;
+        const _Float16 zh = (_Float16)0.f;
+        bh[e] = ok ? tile16[0][base + oo] : zh;
+        bl[e] = ok ? tile16[1][base + oo] : zh;
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(&wa[t][0][h][32 * mt + l32][0]);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(&wa[t][1][h][32 * mt + l32][0]);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[mt], 0, 0, 0);
+      }
+    }
+    // this N-block's outputs: rows co = 32 mt + 8 (r/4) + 4h + r%4, pixel (row, col)
+    const int oy = oy0 + row, ox = ox0 + col;
+    const bool in = oy < p.ho && ox < p.wo;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = 32 * mt + 8 * (r >> 2) + 4 * h + (r & 3);
+        float v = acc[mt][r] * descale;
+        if (p.bias) v += p.bias[co];
+        if (p.relu_out) v = fmaxf(v, 0.f);
+        if (in && co < p.cout) {
+          yn[(size_t)co * plane + (size_t)oy * p.wo + ox] = v;
+          vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
+        }
+      }
+  }
+  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
+}
+
+static bool few16_on() {
+  static const bool on = [] {
+    const char* e = getenv("STX_FEW16");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 template <int KS, int MT>
 int launch_fewin(const stx_conv_params& p, hipStream_t st) {
   const int tiles_x = (p.wo + CF_TW - 1) / CF_TW, tiles_y = (p.ho + CF_TH - 1) / CF_TH;
-  hipLaunchKernelGGL((conv_fewin_kernel<KS, MT>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0,
-                     st, p, tiles_x);
+  // 9x9 (K = 243) stays on the fp32 kernel: its B gathers (16 16-bit LDS reads per
+  // K step) cost more than the matrix cycles saved (150 vs 105 us, ITN conv0 B8 256^2)
+  if (KS == 3 && few16_on())
+    hipLaunchKernelGGL((conv_fewin16_kernel<KS, MT>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256),
+                       0, st, p, tiles_x);
+  else
+    hipLaunchKernelGGL((conv_fewin_kernel<KS, MT>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0,
+                       st, p, tiles_x);
   return check_launch("stx_conv2d(fewin)");
 }
 
@@ -251,10 +435,139 @@ __global__ void __launch_bounds__(256, 2) conv_fewout3_kernel(stx_conv_params p,
   }
 }
 
+// The same GEMM + col2im on the fp16 hi/lo split MFMA when the caller gives a bound
+// on max|x| (p.in_amax, e.g. the producing conv's out_amax): K = 64 channels is 4
+// K=16 steps x 3 products per item instead of 32 fp32 K=2 steps (5.3x fewer matrix
+// cycles).  The weights' scale is block-local (max over the 27 x 64 slab entries).
+// A lane's B fragment is 8 channels 16t + 8h + e of its pixel, loaded straight from
+// global memory and split in registers.
+template <int CIN>
+__global__ void __launch_bounds__(256, 2) conv_fewout16_kernel(stx_conv_params p, int tiles_x) {
+  constexpr int KST = CIN / 16;
+  __shared__ float dt[27 * FO_RH * FO_RWP];
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x, n = blockIdx.z;
+  const int oy0 = ty * FO_TH, ox0 = tx * FO_TW;
+  const int plane_in = p.h * p.w;
+  const float* __restrict__ xn = p.x + (size_t)n * CIN * plane_in;
+  const bool relu_in = p.in_mode == STX_IN_RELU;
+  // A: row m = co*9 + tap (rows >= 9*cout are 0), channel c = 16t + 8h + e
+  const int m = l32, mco = m / 9, mt = m - mco * 9;
+  const int mcl = min(mco, p.cout - 1);
+  float wr[KST][8];
+  float mw = 0.f;
+#pragma unroll
+  for (int t = 0; t < KST; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = 16 * t + 8 * h + e;
+      const float v = p.wt[(size_t)(c * 9 + mt) * p.cout_pad + mcl];
+      wr[t][e] = mco < p.cout ? v : 0.f;
+      mw = fmaxf(mw, fabsf(wr[t][e]));
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mw = fmaxf(mw, __shfl_xor(mw, o, 64));
+  if (lane == 0) red[wave] = mw;
+  __syncthreads();
+  mw = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int ew = 0;
+  frexpf(mw, &ew);
+  ew = min(max(ew, -60), 60);
+  int ex = 0;
+  frexpf(read_amax(p.in_amax), &ex);
+  ex = min(max(ex, -60), 60);
+  const float sw = __builtin_ldexpf(1.f, 15 - ew), sx = __builtin_ldexpf(1.f, 15 - ex);
+  const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
+  f16x8 ah[KST], al[KST];
+#pragma unroll
+  for (int t = 0; t < KST; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = wr[t][e] * sw;
+      const _Float16 vh = (_Float16)v;
+      ah[t][e] = vh;
+      al[t][e] = (_Float16)(v - (float)vh);
+    }
+  const auto rx = make_srd(xn, (uint32_t)(CIN * plane_in) * 4u);
+  constexpr int NITEM = FO_RH * 3;
+  auto load_item = [&](int item, float (&buf)[KST][8]) {
+    const int r = item / 3, nb = item - r * 3;
+    const int c0 = nb == 0 ? 0 : (nb == 1 ? 32 : FO_RW - 32);
+    const int iy = oy0 - 1 + r, ix = ox0 - 1 + c0 + l32;
+    const bool ok = iy >= 0 && iy < p.h && ix >= 0 && ix < p.w;
+    const uint32_t vo = ok ? (uint32_t)(8 * h * plane_in + iy * p.w + ix) * 4u : BUF_OOB;
+#pragma unroll
+    for (int t = 0; t < KST; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, (uint32_t)(16 * t + e) * plane_in * 4u, 0));
+        buf[t][e] = relu_in ? fmaxf(v, 0.f) : v;
+      }
+  };
+  auto run_item = [&](int item, const float (&buf)[KST][8]) {
+    f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int t = 0; t < KST; ++t) {
+      f16x8 bh, bl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = buf[t][e] * sx;
+        const _Float16 vh = (_Float16)v;
+        bh[e] = vh;
+        bl[e] = (_Float16)(v - (float)vh);
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], bl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t], bh, acc, 0, 0, 0);
+    }
+    const int r = item / 3, nb = item - r * 3;
+    const int c0 = nb == 0 ? 0 : (nb == 1 ? 32 : FO_RW - 32);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = 8 * (q >> 2) + 4 * h + (q & 3);
+      if (row < 27) dt[(row * FO_RH + r) * FO_RWP + c0 + l32] = acc[q] * descale;
+    }
+  };
+  float b0[KST][8], b1[KST][8];
+  load_item(wave, b0);
+  for (int it = wave; it < NITEM; it += 8) {
+    if (it + 4 < NITEM) load_item(it + 4, b1);
+    run_item(it, b0);
+    if (it + 8 < NITEM) load_item(it + 8, b0);
+    if (it + 4 < NITEM) run_item(it + 4, b1);
+  }
+  __syncthreads();
+  const int ox = ox0 + (tid & 63), g = tid >> 6;
+  const size_t plane = (size_t)p.ho * p.wo;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ry = 2 * g + j, oy = oy0 + ry;
+    if (oy >= p.ho || ox >= p.wo) continue;
+    for (int co = 0; co < p.cout; ++co) {
+      float v = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+          v += dt[((co * 9 + kh * 3 + kw) * FO_RH + ry + kh) * FO_RWP + (tid & 63) + kw];
+      const size_t o = ((size_t)n * p.cout + co) * plane + (size_t)oy * p.wo + ox;
+      if (p.bias) v += p.bias[co];
+      if (p.accumulate) v += p.y[o];
+      if (p.relu_out) v = fmaxf(v, 0.f);
+      p.y[o] = v;
+    }
+  }
+}
+
 }  // namespace
 
 // cout <= 3, 3x3 stride 1 pad 1, raw/relu input, cin = 64; bias / accumulate / relu_out
-// epilogue only.  Returns -1 when not covered.
+// epilogue only.  Returns -1 when not covered.  With p.in_amax (a device bound on
+// max|x|) the split-MFMA kernel runs.
 int conv2d_fewout(const stx_conv_params& p, hipStream_t st) {
   const bool ok = p.cout >= 1 && p.cout <= 3 && p.ks == 3 && p.stride == 1 && p.pad == 1 &&
                   (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) && p.cin == 64 &&
@@ -262,8 +575,12 @@ int conv2d_fewout(const stx_conv_params& p, hipStream_t st) {
                   !p.out_amax && p.wt_batch_stride == 0 && p.wt && p.hv == p.h && p.wv == p.w;
   if (!ok) return -1;
   const int tiles_x = (p.wo + FO_TW - 1) / FO_TW, tiles_y = (p.ho + FO_TH - 1) / FO_TH;
-  hipLaunchKernelGGL((conv_fewout3_kernel<64>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0, st,
-                     p, tiles_x);
+  if (p.in_amax && few16_on())
+    hipLaunchKernelGGL((conv_fewout16_kernel<64>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0,
+                       st, p, tiles_x);
+  else
+    hipLaunchKernelGGL((conv_fewout3_kernel<64>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0,
+                       st, p, tiles_x);
   return check_launch("stx_conv2d(fewout)");
 }
 

@@ -13,6 +13,7 @@ from __future__ import annotations
 import os
 import random
 
+import numpy as np
 import torch
 from PIL import Image
 from torch.utils.data import DataLoader, Dataset
@@ -29,41 +30,73 @@ VIDEO_DATA_PATH = "data/video/"
 
 class CocoDataset(Dataset):
     """Images under `path` (jpg/png), loaded like stransfer/dataset.py:141-197
-    (a corrupt image is replaced by a random other one, as the reference does)."""
+    (a corrupt image is replaced by a random other one, as the reference does).
+    decode_only=True returns the decoded HxWx3 uint8 array instead of the
+    conditioned tensor: the conditioning then runs on the GPU for the whole batch
+    (img_utils.ImageConditioner, bit-identical to the PIL path)."""
 
-    def __init__(self, images=None, image_limit=None, path=None):
+    def __init__(self, images=None, image_limit=None, path=None, decode_only=False):
         path = path or os.path.join(constants.PROJECT_ROOT_PATH, IMAGE_FOLDER_PATH)
         if images is None:
             images = sorted(f for f in os.listdir(path)
                             if f.lower().endswith((".jpg", ".jpeg", ".png")))
         self.path = path
         self.images = images[:image_limit] if image_limit else images
+        self.decode_only = decode_only
 
     def __len__(self):
         return len(self.images)
 
     def __getitem__(self, idx):
         try:
-            img = Image.open(os.path.join(self.path, self.images[idx]))
-            return img_utils.image_loader_transform(img.convert("RGB")).cpu()
+            img = Image.open(os.path.join(self.path, self.images[idx])).convert("RGB")
+            if self.decode_only:
+                return np.asarray(img, dtype=np.uint8)
+            return img_utils.image_loader_transform(img).cpu()
         except Exception:  # noqa: BLE001  (reference behaviour, :186-197)
             return self[random.randrange(len(self))]
 
 
-def _train_loader(ds, batch_size, shard, shuffle=True, seed=0):
+def _list_collate(batch):
+    return list(batch)
+
+
+class GpuConditionedLoader:
+    """Wraps a DataLoader of decoded uint8 images (CocoDataset(decode_only=True),
+    list collate) and yields each batch conditioned on the GPU as [B, 1, 3, S, S]
+    -- the shape static_train squeezes (stransfer/network.py:688)."""
+
+    def __init__(self, loader, size=None, device=None):
+        self.loader = loader
+        self.batch_sampler = getattr(loader, "batch_sampler", None)
+        self.cond = img_utils.ImageConditioner(size, device)
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        for imgs in self.loader:
+            yield self.cond(imgs).unsqueeze(1)
+
+
+def _train_loader(ds, batch_size, shard, shuffle=True, seed=0, num_workers=0, collate=None):
     """DataLoader over `ds` whose batches are this rank's shard of each global batch
     of `batch_size` (distributed.ShardedBatchSampler); at world 1 a plain batch."""
     from .distributed import Shard, ShardedBatchSampler
     shard = shard or Shard()
     sampler = ShardedBatchSampler(len(ds), batch_size, shard.rank, shard.world,
                                   shuffle=shuffle, seed=seed)
-    return DataLoader(ds, batch_sampler=sampler)
+    kw = {"collate_fn": collate} if collate is not None else {}
+    return DataLoader(ds, batch_sampler=sampler, num_workers=num_workers, **kw)
 
 
-def get_coco_loader(batch_size=4, test_split=0.10, test_limit=None, path=None, shard=None):
+def get_coco_loader(batch_size=4, test_split=0.10, test_limit=None, path=None, shard=None,
+                    gpu_conditioning=None, num_workers=0):
     """(test_loader, train_loader) over local COCO images (stransfer/dataset.py:314-360).
     `batch_size` is the global batch; with a data-parallel `shard` each rank's train
-    loader yields its batch_size/world slice of every global batch."""
+    loader yields its batch_size/world slice of every global batch.  With
+    gpu_conditioning (default: when a GPU is present) the workers only decode and
+    the crop/resize/normalisation of each batch runs on the GPU (identical output)."""
     path = path or os.path.join(constants.PROJECT_ROOT_PATH, IMAGE_FOLDER_PATH)
     if not os.path.isdir(path) or not os.listdir(path):
         raise FileNotFoundError(
@@ -74,8 +107,20 @@ def get_coco_loader(batch_size=4, test_split=0.10, test_limit=None, path=None, s
     test_imgs, train_imgs = images[:n_test], images[n_test:]
     if test_limit:
         test_imgs = test_imgs[:test_limit]
-    test = DataLoader(CocoDataset(test_imgs, path=path), batch_size=batch_size, shuffle=False)
-    train = _train_loader(CocoDataset(train_imgs, path=path), batch_size, shard)
+    if gpu_conditioning is None:
+        gpu_conditioning = constants.DEVICE.type == "cuda"
+    if gpu_conditioning:
+        test = GpuConditionedLoader(DataLoader(CocoDataset(test_imgs, path=path, decode_only=True),
+                                               batch_size=batch_size, shuffle=False,
+                                               collate_fn=_list_collate, num_workers=num_workers))
+        train = GpuConditionedLoader(_train_loader(
+            CocoDataset(train_imgs, path=path, decode_only=True), batch_size, shard,
+            num_workers=num_workers, collate=_list_collate))
+        return test, train
+    test = DataLoader(CocoDataset(test_imgs, path=path), batch_size=batch_size, shuffle=False,
+                      num_workers=num_workers)
+    train = _train_loader(CocoDataset(train_imgs, path=path), batch_size, shard,
+                          num_workers=num_workers)
     return test, train
 
 

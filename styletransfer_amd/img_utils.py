@@ -8,6 +8,8 @@ uint8/255 tensors; ImageNet normalisation as :32-42; `imshow` de-normalises,
 clamps to [0, 255] (sic) and converts with mul(255).byte() (:95-117)."""
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import torch
 from PIL import Image
@@ -73,3 +75,90 @@ def imshow(image_tensor: torch.Tensor, ground_truth_image: torch.Tensor = None,
     if ground_truth_image is not None:
         image_tensor = concat_images(image_tensor, ground_truth_image)
     to_pil(image_tensor, denormalize).save(path)
+
+
+# ------------------------------------------------------------------ GPU conditioning
+class ImageConditioner:
+    """image_loader_transform for a batch of decoded images on the GPU
+    (csrc/image.hip, stx_image_condition): centre crop -> Pillow-exact BILINEAR
+    resize -> /255 -> ImageNet normalisation, bit-identical to the PIL path above
+    (tests/test_image_pipeline.py).  Host work per batch is the JPEG decode (done by
+    the loader's workers) and one copy of the packed uint8 images, so COCO-rate
+    training input does not bottleneck on PIL's resize."""
+
+    def __init__(self, size: int | None = None, device=None):
+        self.size = int(size or constants.IMSIZE)
+        self.device = torch.device(device) if device is not None else constants.DEVICE
+        self._tables = {}  # crop side -> (int32 table, ksize, y0, y1)
+        mean = np.asarray(constants.IMAGENET_MEAN, np.float32)
+        std = np.asarray(constants.IMAGENET_STD, np.float32)
+        self._mean = (C.c_float * 3)(*mean.tolist())
+        self._std = (C.c_float * 3)(*std.tolist())
+
+    def _table(self, m: int):
+        t = self._tables.get(m)
+        if t is None:
+            from ._native import lib
+            L, S = lib(), self.size
+            k = L.stx_resample_coeffs(m, S, None, None, 0)
+            bounds = np.zeros((S, 2), np.int32)
+            kk = np.zeros((S, k), np.int32)
+            if L.stx_resample_coeffs(m, S, bounds.ctypes.data, kk.ctypes.data, k) != k:
+                raise RuntimeError("stx_resample_coeffs failed")
+            y0, y1 = int(bounds[0, 0]), int(bounds[-1, 0] + bounds[-1, 1])
+            t = self._tables[m] = (np.concatenate([bounds.ravel(), kk.ravel()]), k, y0, y1)
+        return t
+
+    def __call__(self, images) -> torch.Tensor:
+        """images: sequence of HxWx3 uint8 arrays (or PIL images) -> [B, 3, S, S]."""
+        from ._native import ImageMeta, check, lib
+        arrs = [np.ascontiguousarray(np.asarray(im.convert("RGB") if isinstance(im, Image.Image)
+                                                else im, dtype=np.uint8)) for im in images]
+        B, S = len(arrs), self.size
+        if B == 0:
+            raise ValueError("empty image batch")
+        metas = (ImageMeta * B)()
+        tables, coef_off, chunks, max_rows = {}, 0, [], 0
+        src_off, tmp_off = 0, 0
+        for i, a in enumerate(arrs):
+            if a.ndim != 3 or a.shape[2] != 3:
+                raise ValueError(f"image {i}: HxWx3 uint8 expected, got {a.shape}")
+            h, w = a.shape[:2]
+            m = min(h, w)
+            top, left = int(round((h - m) / 2.0)), int(round((w - m) / 2.0))
+            md = metas[i]
+            md.offset, md.h, md.w, md.top, md.left = src_off, h, w, top, left
+            src_off += a.nbytes
+            if m == S:  # torchvision Resize is a no-op at the target size
+                md.y0, md.y1, md.resize_w, md.resize_h = 0, m, 0, 0
+            else:
+                if m not in tables:
+                    tab, k, y0, y1 = self._table(m)
+                    tables[m] = (coef_off, k, y0, y1)
+                    chunks.append(tab)
+                    coef_off += tab.size
+                off, k, y0, y1 = tables[m]
+                md.y0, md.y1, md.resize_w, md.resize_h = y0, y1, 1, 1
+                md.xcoef = md.ycoef = off
+                md.xk = md.yk = k
+                md.tmp_offset = tmp_off
+                tmp_off += (y1 - y0) * S * 3
+                max_rows = max(max_rows, y1 - y0)
+        dev = self.device
+        packed = torch.empty(src_off, dtype=torch.uint8, pin_memory=True)
+        pk = packed.numpy()
+        o = 0
+        for a in arrs:
+            pk[o:o + a.nbytes] = a.reshape(-1)
+            o += a.nbytes
+        src = packed.to(dev, non_blocking=True)
+        meta = torch.frombuffer(bytearray(bytes(metas)), dtype=torch.uint8).to(dev)
+        coef = torch.from_numpy(np.concatenate(chunks) if chunks else np.zeros(1, np.int32)).to(dev)
+        tmp = torch.empty(max(tmp_off, 16), dtype=torch.uint8, device=dev)
+        out = torch.empty((B, 3, S, S), dtype=torch.float32, device=dev)
+        check(lib().stx_image_condition(src.data_ptr(), meta.data_ptr(), B, max_rows,
+                                        coef.data_ptr(), S, self._mean, self._std,
+                                        out.data_ptr(), tmp.data_ptr(), tmp.numel(),
+                                        torch.cuda.current_stream(dev).cuda_stream),
+              "stx_image_condition")
+        return out

@@ -277,6 +277,10 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         assert ks == 1 and wt_batch_stride and mask is None and p2_z is None
         p.wt16 = 1
         p.in_amax = (in_amax if in_amax is not None else amax(x)).data_ptr()
+    if in_amax is not None and not p.in_amax:
+        # the non-split kernels that take an input bound (convfew.hip's split 64->3
+        # data gradient) read it too; the others ignore it
+        p.in_amax = in_amax.data_ptr()
     if out_amax is not None:
         p.out_amax = out_amax.data_ptr()
     if pool_out is not None:

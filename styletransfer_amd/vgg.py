@@ -304,7 +304,7 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
 
     folded = st.folded
     s = (lambda i: None) if folded else (lambda i: g[i:i + 1])
-    am = st.amax  # slots 0..5: forward; 6..9: backward split-conv inputs
+    am = st.amax  # slots 0..5: forward; 6..10: backward split-conv inputs
     # conv3_1 output: dZ5 = A5 Z5
     sp = feat.wt16[1] is not None  # split kernels in use
     dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4),
@@ -335,12 +335,13 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
                              up_dp=dp1, out_amax=slot(am, 9), z_amax=slot(am, 2) if sp else None)
     # dZ1 = conv1_2^T(dZ2)*[Z1>0] + A1 Z1
     dz1 = feat.dgrad(1, dz2, buf("dz1", z[0].shape), mask=z[0], p2_z=z[0],
-                     p2_coef=st.coef[0], p2_scale=s(0), in_amax=slot(am, 9), p2_amax=slot(am, 1))
-    # conv1_1 dgrad -> image
+                     p2_coef=st.coef[0], p2_scale=s(0), in_amax=slot(am, 9), p2_amax=slot(am, 1),
+                     out_amax=slot(am, 10) if sp else None)
+    # conv1_1 dgrad -> image (64 -> 3 GEMM + col2im; on the split MFMA given max|dZ1|)
     xs = (B, 3, z[0].shape[2], z[0].shape[3])
     if dx is None:
         dx = torch.empty(xs, device=z[0].device, dtype=torch.float32)
-    return feat.dgrad(0, dz1, dx)
+    return feat.dgrad(0, dz1, dx, in_amax=slot(am, 10) if sp else None)
 
 
 def content_target(feat: VGGFeatures, content, out=None, amax=None):

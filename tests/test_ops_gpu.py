@@ -286,8 +286,9 @@ def test_conv_fused_gram_phase_and_unpool(dev):
                                   (1, 32, 9, 9, 130), (3, 32, 3, 8, 8)])
 def test_conv_fewin(dev, case):
     """3-input-channel convs (convfew.hip: VGG conv1_1, ITN conv0 / conv22 dgrad) vs
-    fp64, ragged tiles, bias + relu_out + out_amax epilogue; equal to the generic
-    fp32 kernel path (STX_FEWIN=0 is not needed: compare with F.conv2d in fp64)."""
+    fp64, ragged tiles, bias + relu_out + out_amax epilogue.  They run on the fp16
+    hi/lo split MFMA with block-local scales (fp32-class: 2e-6 of fp64, as every
+    split kernel in test_conv_split_gpu.py)."""
     n, cout, ks, h, w = case
     x = rnd(n, 3, h, w, dev=dev, seed=21, scale=2, shift=-1)
     wgt = rnd(cout, 3, ks, ks, dev=dev, seed=22, scale=0.2, shift=-0.1)
@@ -296,10 +297,16 @@ def test_conv_fewin(dev, case):
     am = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
     y = ops.conv2d(x, wt, 3, cout, ks, bias=b, out_amax=am)
     ref = F.conv2d(x.double(), wgt.double(), b.double(), padding=ks // 2)
-    assert rel(y, ref) < 1e-6
+    assert rel(y, ref) < 2e-6
     assert float(am.max()) == float(y.abs().max())
     yr = ops.conv2d(x, wt, 3, cout, ks, bias=b, relu_out=True)
-    assert rel(yr, F.relu(ref)) < 1e-6
+    assert rel(yr, F.relu(ref)) < 2e-6
+    # an input tile of zeros next to a large one (block-local scales) stays exact
+    x2 = x.clone()
+    x2[..., : x.shape[-1] // 2] = 0
+    x2[..., x.shape[-1] // 2:] *= 1e4
+    y2 = ops.conv2d(x2, wt, 3, cout, ks, bias=b)
+    assert rel(y2, F.conv2d(x2.double(), wgt.double(), b.double(), padding=ks // 2)) < 2e-6
 
 
 @pytest.mark.parametrize("case", [(1, 3, 37, 70, N.STX_IN_RAW), (2, 3, 16, 64, N.STX_IN_RELU),
@@ -320,3 +327,12 @@ def test_conv_fewout(dev, case):
     ops.conv2d(x, wt, 64, cout, 3, in_mode=mode, bias=b, out=out, accumulate=True,
                relu_out=True)
     assert rel(out, F.relu(ref + old.double())) < 1e-6
+    # with a bound on max|x| (the Gatys backward passes conv1_2's out_amax): the split
+    # MFMA kernel, fp32-class (2e-6 of fp64)
+    am = ops.amax(x)
+    y16 = ops.conv2d(x, wt, 64, cout, 3, in_mode=mode, bias=b, in_amax=am)
+    assert rel(y16, ref) < 2e-6
+    out = old.clone()
+    ops.conv2d(x, wt, 64, cout, 3, in_mode=mode, bias=b, out=out, accumulate=True,
+               relu_out=True, in_amax=am)
+    assert rel(out, F.relu(ref + old.double())) < 2e-6
