@@ -97,16 +97,23 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
     lane_ok[j] = oy < p.ho && ox < p.wo;
     vo[j] = lane_ok[j] ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
   }
+  // biases of this lane's rows: branch-free descriptor loads (rows past cout read 0)
   float bias_r[2][16];
+  {
+    const auto rbias = make_srd(p.bias ? p.bias + co_w : p.y, p.bias ? (uint32_t)rows * 4u : 0u);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = co_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      bias_r[i][r] = (p.bias && co < p.cout) ? p.bias[co] : 0.f;
-    }
-  // rows past cout exist only in a ragged last 64-row tile: then count per element
+      for (int r = 0; r < 16; ++r)
+        bias_r[i][r] = buf_ld(rbias, (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 4u);
+  }
+  // max|v| over the valid outputs: a per-lane mask (pixel inside the image) ANDed
+  // into the IEEE bits; rows past cout exist only in a ragged last 64-row tile, where
+  // a per-row mask is added
   const bool rows_full = rows >= 64;
+  uint32_t lmask[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) lmask[j] = lane_ok[j] ? 0x7fffffffu : 0u;
   uint32_t vmax_u = 0u;  // max |v| as IEEE bits: NaN (above inf) propagates
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -119,8 +126,9 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
         if (RELU) v = fmaxf(v, 0.f);
         buf_st(ry, vo[j] + (uint32_t)row * pb, v);
         acc[i][j][r] = v;  // kept for the fused pooled output
-        const bool ok = lane_ok[j] && (rows_full || row + 4 * h < rows);
-        if (ok) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
+        uint32_t m = lmask[j];
+        if (!rows_full) m = (row + 4 * h < rows) ? m : 0u;
+        vmax_u = max(vmax_u, __float_as_uint(v) & m);
       }
     }
   }
@@ -148,7 +156,10 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const uint32_t m2 = max(rb(acc[i][0][r]), rb(acc[i][1][r]));
-        const uint32_t m = max(m2, (uint32_t)__shfl_xor((int)m2, 1, 64));
+        // partner column (lane ^ 1) by a DPP quad permutation [1,0,3,2]: one VALU
+        // move instead of an LDS bpermute
+        const uint32_t mp = (uint32_t)__builtin_amdgcn_mov_dpp((int)m2, 0xB1, 0xF, 0xF, false);
+        const uint32_t m = max(m2, mp);
         const int row = i * 32 + (r & 3) + 8 * (r >> 2);
         buf_st(rp, po + (uint32_t)row * ppb, __uint_as_float(m));
       }

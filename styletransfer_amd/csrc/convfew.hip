@@ -241,7 +241,18 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
   __syncthreads();
 
   const size_t plane = (size_t)p.ho * p.wo;
-  float* __restrict__ yn = p.y + (size_t)n * p.cout * plane;
+  const uint32_t pb = (uint32_t)plane * 4u;
+  // stores through a descriptor: per-lane pixel offset + per-register row constant
+  const auto ry = make_srd(p.y + (size_t)n * p.cout * plane, (uint32_t)p.cout * pb);
+  // this lane's output rows' biases, loaded once (not per stored element)
+  float bias_r[MT][16];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = 32 * mt + 8 * (r >> 2) + 4 * h + (r & 3);
+      bias_r[mt][r] = (p.bias && co < p.cout) ? p.bias[co] : 0.f;
+    }
   uint32_t vmax_u = 0u;
 #pragma unroll 1
   for (int b = 0; b < 4; ++b) {
@@ -277,18 +288,16 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
     // this N-block's outputs: rows co = 32 mt + 8 (r/4) + 4h + r%4, pixel (row, col)
     const int oy = oy0 + row, ox = ox0 + col;
     const bool in = oy < p.ho && ox < p.wo;
+    const uint32_t vo = in ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = 32 * mt + 8 * (r >> 2) + 4 * h + (r & 3);
-        float v = acc[mt][r] * descale;
-        if (p.bias) v += p.bias[co];
+        const int row_c = 32 * mt + 8 * (r >> 2) + (r & 3);  // co without the lane half
+        float v = fmaf(acc[mt][r], descale, bias_r[mt][r]);
         if (p.relu_out) v = fmaxf(v, 0.f);
-        if (in && co < p.cout) {
-          yn[(size_t)co * plane + (size_t)oy * p.wo + ox] = v;
-          vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
-        }
+        buf_st(ry, vo + (uint32_t)row_c * pb, v);
+        if (in && row_c + 4 * h < p.cout) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
       }
   }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
