@@ -134,6 +134,25 @@ int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax, int cout, 
  * two launches (one max pass, one conversion) -- a trained layer re-preps every step. */
 int stx_conv_weight_prep16_pair(const float* w, void* wt16, void* wtT16, float* w_amax,
                                 int cout, int cin, int ks, void* stream);
+/* Every slab of a trained network in two launches (one max|w| pass over the distinct
+ * split-slab weights, one conversion pass over all jobs) instead of two launches per
+ * slab: the per-step re-prep of ImageTransformNet's 14 conv weights after each Adam
+ * update (stransfer/network.py:765 optimizer.step -> the next static_train closure).
+ * kind STX_WPREP_F32: slab as stx_conv_weight_prep(w, slab, cout, cin, ks, transpose);
+ * kind STX_WPREP_F16: as stx_conv_weight_prep16(w, slab, w_amax, ...) (ks = 3).  The
+ * forward and data-gradient split slabs of one weight may share w_amax (computed
+ * once).  `jobs` is a host array read at call time (graph-capturable). */
+#define STX_WPREP_MAX 48
+#define STX_WPREP_F32 0
+#define STX_WPREP_F16 1
+typedef struct stx_wprep_job {
+  const float* w;
+  void* slab;
+  float* w_amax;
+  int kind, cout, cin, ks, transpose;
+  int pad_;
+} stx_wprep_job;
+int stx_conv_weight_prep_batch(const stx_wprep_job* jobs, int njobs, void* stream);
 /* *out = max |x[i]| over n floats (device scalar; NaN propagates). */
 int stx_amax(const float* x, long long n, float* out, void* stream);
 
@@ -287,12 +306,15 @@ int stx_instnorm_fwd(const float* x, const float* res, const float* gamma, const
                      float* y, float* mean, float* rstd, int n, int c, int hw, float eps,
                      int relu, float* out_amax, void* stream);
 /* backward: dy = grad wrt y; y needed when relu (mask).  du = grad wrt u (= grad of x
- * and of res).  dgamma/dbeta (may be NULL) (+)= sums over n (fixed order).  out_amax
- * (amax group or NULL) receives max|du| -- the split dgrad/wgrad scale of du. */
+ * and of res).  dgamma/dbeta (may be NULL) (+)= sums over n (fixed order).  dbias_in
+ * (may be NULL) (+)= sum_{n,p} du: the bias gradient of the conv that produced x
+ * (stransfer/network.py:471-611, every Conv2d followed by InstanceNorm2d), so that
+ * conv needs no separate bias-gradient pass.  out_amax (amax group or NULL) receives
+ * max|du| -- the split dgrad/wgrad scale of du. */
 size_t stx_instnorm_bwd_ws(int n, int c);
 int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
                      const float* gamma, const float* mean, const float* rstd, float* du,
-                     float* dgamma, float* dbeta, int n, int c, int hw, int relu,
+                     float* dgamma, float* dbeta, float* dbias_in, int n, int c, int hw, int relu,
                      int accumulate_params, float* out_amax, void* ws, size_t ws_bytes,
                      void* stream);
 

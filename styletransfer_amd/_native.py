@@ -47,6 +47,15 @@ class ImageMeta(C.Structure):
                 ("xcoef", i32), ("ycoef", i32), ("xk", i32), ("yk", i32), ("tmp_offset", i64)]
 
 
+class WprepJob(C.Structure):
+    """Mirror of `stx_wprep_job` (include/stx.h)."""
+    _fields_ = [("w", vp), ("slab", vp), ("w_amax", vp), ("kind", i32), ("cout", i32),
+                ("cin", i32), ("ks", i32), ("transpose", i32), ("pad_", i32)]
+
+
+STX_WPREP_MAX, STX_WPREP_F32, STX_WPREP_F16 = 48, 0, 1
+
+
 class LossParts(C.Structure):
     """Mirror of `stx_loss_parts` (include/stx.h)."""
     _fields_ = [("parts", vp * 8), ("nparts", i32 * 8), ("inv", f32 * 8), ("k", i32)]
@@ -63,6 +72,7 @@ SIGNATURES = {
     "stx_conv_weight_prep16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv_weight_prep16_pair": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
     "stx_amax": (i32, [vp, i64, vp, vp]),
+    "stx_conv_weight_prep_batch": (i32, [C.POINTER(WprepJob), i32, vp]),
     "stx_conv2d_wgrad_ws": (sz, [i32, i32, i32, i32, i32, i32, i32]),
     "stx_conv2d_wgrad": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                                i32, i32, i32, i32, vp, sz, vp]),
@@ -102,8 +112,8 @@ SIGNATURES = {
     "stx_adam_step": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp, vp]),
     "stx_instnorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp, vp]),
     "stx_instnorm_bwd_ws": (sz, [i32, i32]),
-    "stx_instnorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32,
-                               i32, vp, vp, sz, vp]),
+    "stx_instnorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,
+                               i32, i32, vp, vp, sz, vp]),
     "stx_upsample2x_fwd": (i32, [vp, vp, i32, i32, i32, vp]),
     "stx_upsample2x_bwd": (i32, [vp, vp, i32, i32, i32, vp]),
     "stx_tv_ws": (sz, [i32, i32, i32, i32]),

@@ -38,17 +38,19 @@ class Conv2dFn(torch.autograd.Function):
     (nn.Conv2d of VGG-19 and ImageTransformNet; zero padding.)"""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, in_mode, wt=None, wt16=None):
+    def forward(ctx, x, w, b, stride, pad, in_mode, wt=None, wt16=None, wtT=None, wtT16=None):
         x = _c(x)
         cout, cin, ks, _ = w.shape
         # 3x3 stride-1 layers with cin >= 16 run on the fp16 hi/lo split MFMA kernel
-        # (no fp32 slab needed); max|x| is computed once and kept for the wgrad
+        # (no fp32 slab needed); max|x| is computed once and kept for the wgrad.
+        # wtT / wtT16: prepped data-gradient slabs (ops.TrainedSlabs), else prepped here
         split = _split_on() and pad == 1 and ops.split_eligible(cin, cout, ks, stride)
         x_amax = None
-        ctx.wtT16 = None
+        ctx.wtT16, ctx.wtT = wtT16, wtT
         if split:
             if wt16 is None:
-                if w.requires_grad and stride == 1 and ops.split_eligible(cout, cin, ks, 1):
+                if w.requires_grad and stride == 1 and ops.split_eligible(cout, cin, ks, 1) \
+                        and wtT16 is None:
                     # trained layer: both slabs (forward + data gradient) in one go
                     wt16, ctx.wtT16 = ops.conv_weight_prep16_pair(w.detach().contiguous())
                 else:
@@ -93,18 +95,21 @@ class Conv2dFn(torch.autograd.Function):
                     wtT16 = ctx.wtT16 if ctx.wtT16 is not None else ops.conv_weight_prep16(
                         w.detach().contiguous(), transpose=True)
                 else:
-                    wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
+                    wtT = ctx.wtT if ctx.wtT is not None else ops.conv_weight_prep(
+                        w.detach().contiguous(), transpose=True)
                 dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16,
                                 in_amax=dy_amax)
             elif stride == 2:
                 # stride-1 conv over the zero-dilated dy; the split kernel takes it too
                 if _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1):
-                    wtT16 = ops.conv_weight_prep16(w.detach().contiguous(), transpose=True)
+                    wtT16 = ctx.wtT16 if ctx.wtT16 is not None else ops.conv_weight_prep16(
+                        w.detach().contiguous(), transpose=True)
                     dv = ops.conv2d(dy, None, cout, cin, ks, pad=ks - 1 - pad,
                                     in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv, wt16=wtT16,
                                     in_amax=dy_amax if dy_amax is not None else ops.amax(dy))
                 else:
-                    wtT = ops.conv_weight_prep(w.detach().contiguous(), transpose=True)
+                    wtT = ctx.wtT if ctx.wtT is not None else ops.conv_weight_prep(
+                        w.detach().contiguous(), transpose=True)
                     dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad,
                                     in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv)
             else:
@@ -129,12 +134,14 @@ class Conv2dFn(torch.autograd.Function):
             b = ctx.b_ref
             db = _grad_into(b, lambda: ops.bias_grad(dy),
                             lambda dst: ops.bias_grad(dy, db=dst, accumulate=True))
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
-def conv2d(x, w, b=None, stride=1, pad=None, in_mode=N.STX_IN_RAW, wt=None, wt16=None):
+def conv2d(x, w, b=None, stride=1, pad=None, in_mode=N.STX_IN_RAW, wt=None, wt16=None,
+           wtT=None, wtT16=None):
     ks = w.shape[-1]
-    return Conv2dFn.apply(x, w, b, stride, ks // 2 if pad is None else pad, in_mode, wt, wt16)
+    return Conv2dFn.apply(x, w, b, stride, ks // 2 if pad is None else pad, in_mode, wt, wt16,
+                          wtT, wtT16)
 
 
 # ----------------------------------------------------------------------- relu / pool
@@ -182,7 +189,9 @@ class InstanceNormFn(torch.autograd.Function):
     """y = [relu](IN(x (+ res)) * gamma + beta), per-instance stats (eps 1e-5)."""
 
     @staticmethod
-    def forward(ctx, x, res, gamma, beta, eps, relu):
+    def forward(ctx, x, res, gamma, beta, eps, relu, conv_bias=None):
+        # conv_bias: the bias of the conv that produced x, given when that conv ran with a
+        # detached bias -- its gradient sum(du) comes out of this backward's kernel
         x, res = _c(x), _c(res)
         g = ops.ARENA.take(x.device)
         y, mean, rstd = ops.instnorm_fwd(x, None if gamma is None else gamma.detach(),
@@ -191,6 +200,7 @@ class InstanceNormFn(torch.autograd.Function):
         ops.ARENA.annotate(y, g)
         ctx.save_for_backward(x, res, gamma, y, mean, rstd)
         ctx.beta_ref = beta
+        ctx.cb_ref = conv_bias
         ctx.relu = relu
         ctx.has_res = res is not None
         return y
@@ -199,30 +209,24 @@ class InstanceNormFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, res, gamma, y, mean, rstd = ctx.saved_tensors
         c = x.shape[1]
-        beta = ctx.beta_ref
-        dg = db = None
-        acc = False
-        if gamma is not None:
-            # straight into existing .grad buffers (FastStTrainer's flat gradient)
-            direct = all(p is not None and p.is_leaf and p.grad is not None and
-                         p.grad.is_contiguous() for p in (gamma, beta))
-            if direct:
-                dg, db, acc = gamma.grad, beta.grad, True
-            else:
-                dg = torch.empty(c, device=x.device)
-                db = torch.empty(c, device=x.device)
+        cb = ctx.cb_ref if ctx.needs_input_grad[6] else None
+        params = (gamma, ctx.beta_ref if gamma is not None else None, cb)
+        # straight into existing .grad buffers (FastStTrainer's flat gradient)
+        acc = all(p is None or (p.is_leaf and p.grad is not None and p.grad.is_contiguous())
+                  for p in params)
+        bufs = [None if p is None else (p.grad if acc else torch.empty(c, device=x.device))
+                for p in params]
         ga = ops.ARENA.take(x.device)
         du = ops.instnorm_bwd(_c(dy), y, x, res, None if gamma is None else gamma.detach(),
-                              mean, rstd, relu=ctx.relu, dgamma=dg, dbeta=db, accumulate=acc,
-                              out_amax=ga)
+                              mean, rstd, relu=ctx.relu, dgamma=bufs[0], dbeta=bufs[1],
+                              dbias_in=bufs[2], accumulate=acc, out_amax=ga)
         ops.ARENA.annotate(du, ga)
-        if acc:
-            dg = db = None
-        return du, (du if ctx.has_res else None), dg, db, None, None
+        dg, db, dcb = (None, None, None) if acc else bufs
+        return du, (du if ctx.has_res else None), dg, db, None, None, dcb
 
 
-def instance_norm(x, gamma, beta, res=None, eps=1e-5, relu=False):
-    return InstanceNormFn.apply(x, res, gamma, beta, eps, relu)
+def instance_norm(x, gamma, beta, res=None, eps=1e-5, relu=False, conv_bias=None):
+    return InstanceNormFn.apply(x, res, gamma, beta, eps, relu, conv_bias)
 
 
 # ----------------------------------------------------------------------- losses

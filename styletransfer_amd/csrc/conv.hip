@@ -22,6 +22,7 @@
 #include "common.h"
 #include "conv_epi.h"
 #include "gbwd16.h"
+#include "wprep.h"
 #include "../../include/stx.h"
 
 namespace stx {
@@ -503,24 +504,9 @@ static int launch_smallc(const stx_conv_params& p, hipStream_t st) {
 // ---------------------------------------------------------------- weight prep
 __global__ void weight_prep_kernel(const float* __restrict__ w, float* __restrict__ wt, int cout,
                                    int cin, int ks, int transpose, int rows_pad, int cols_pad) {
-  const long long total = (long long)rows_pad * cols_pad;
-  const int kk = ks * ks;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int col = (int)(i % cols_pad);
-    const int row = (int)(i / cols_pad);
-    const int c_in = row / kk, r = row % kk, kh = r / ks, kw = r % ks;
-    float v = 0.f;
-    if (!transpose) {
-      // row = ci*kk + kh*ks + kw, col = co
-      if (c_in < cin && col < cout) v = w[(((size_t)col * cin + c_in) * ks + kh) * ks + kw];
-    } else {
-      // dgrad weights: row = co*kk + kh*ks + kw, col = ci; flipped taps
-      if (c_in < cout && col < cin)
-        v = w[(((size_t)c_in * cin + col) * ks + (ks - 1 - kh)) * ks + (ks - 1 - kw)];
-    }
-    wt[i] = v;
-  }
+  weight_prep32_body(w, wt, cout, cin, ks, transpose, rows_pad, cols_pad,
+                     blockIdx.x * (long long)blockDim.x + threadIdx.x,
+                     (long long)gridDim.x * blockDim.x);
 }
 
 // input channels per K chunk; 3x3 convs over <= 4 channels (conv1_1, 3-channel
@@ -580,6 +566,10 @@ extern "C" int stx_conv_weight_prep(const float* w, float* wt, int cout, int cin
   int rc = stx_conv_weight_dims(gin, gout, ks, &rp, &cp);
   if (rc) return rc;
   const long long total = (long long)rp * ks * ks * cp;
+  if (total >= (1ll << 31)) {
+    set_error("stx_conv_weight_prep: slab too large");
+    return STX_E_INVALID;
+  }
   const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(weight_prep_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, wt,
                      cout, cin, ks, transpose, rp * ks * ks, cp);

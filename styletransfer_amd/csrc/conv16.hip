@@ -31,6 +31,7 @@
 
 #include "common.h"
 #include "conv_epi.h"
+#include "wprep.h"
 #include "../../include/stx.h"
 
 namespace stx {
@@ -615,21 +616,23 @@ static int dispatch16_tw(const stx_conv_params& p, hipStream_t st) {
 __device__ __forceinline__ void weight_prep16_body(const float* __restrict__ w,
                                                    _Float16* __restrict__ out,
                                                    const float* __restrict__ w_amax, int cout,
-                                                   int cin, int transpose, int gin16, int gout64) {
-  const long long total = (long long)gin16 * 9 * 2 * gout64;
+                                                   int cin, int transpose, int gin16, int gout64,
+                                                   long long i0, long long step) {
+  // 32-bit index math (slabs are < 2^31 elements; 64-bit div/mod is a long
+  // software sequence on the GPU)
+  const int total = gin16 * 9 * 2 * gout64;
   const float sw = __builtin_ldexpf(1.f, 15 - amax_exp(read_amax(w_amax)));
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int e = (int)(i & 7);
-    long long r = i >> 3;
-    const int co = (int)(r % gout64);
-    r /= gout64;
+  for (int i = (int)i0; i < total; i += (int)step) {
+    const int e = i & 7;
+    unsigned r = (unsigned)i >> 3;
+    const int co = (int)(r % (unsigned)gout64);
+    r /= (unsigned)gout64;
     const int cg = (int)(r & 1);
     r >>= 1;
     const int P = (int)(r & 1);
     r >>= 1;
-    const int tap = (int)(r % 9);
-    const int chunk = (int)(r / 9);
+    const int tap = (int)(r % 9u);
+    const int chunk = (int)(r / 9u);
     const int ci = chunk * 16 + cg * 8 + e;
     const int kh = tap / 3, kw = tap % 3;
     float v = 0.f;
@@ -648,17 +651,21 @@ __device__ __forceinline__ void weight_prep16_body(const float* __restrict__ w,
 __global__ void weight_prep16_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
                                      const float* __restrict__ w_amax, int cout, int cin,
                                      int transpose, int gin16, int gout64) {
-  weight_prep16_body(w, out, w_amax, cout, cin, transpose, gin16, gout64);
+  weight_prep16_body(w, out, w_amax, cout, cin, transpose, gin16, gout64,
+                     blockIdx.x * (long long)blockDim.x + threadIdx.x,
+                     (long long)gridDim.x * blockDim.x);
 }
 
 // both slabs of one weight in one launch: blockIdx.y 0 = forward, 1 = data gradient
 __global__ void weight_prep16_pair_kernel(const float* __restrict__ w, _Float16* __restrict__ fwd,
                                           _Float16* __restrict__ dgr,
                                           const float* __restrict__ w_amax, int cout, int cin) {
+  const long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long step = (long long)gridDim.x * blockDim.x;
   if (blockIdx.y == 0)
-    weight_prep16_body(w, fwd, w_amax, cout, cin, 0, rup(cin, 16), rup(cout, 64));
+    weight_prep16_body(w, fwd, w_amax, cout, cin, 0, rup(cin, 16), rup(cout, 64), i0, step);
   else
-    weight_prep16_body(w, dgr, w_amax, cout, cin, 1, rup(cout, 16), rup(cin, 64));
+    weight_prep16_body(w, dgr, w_amax, cout, cin, 1, rup(cout, 16), rup(cin, 64), i0, step);
 }
 
 // -------------------------------------------------------------------- amax
@@ -686,12 +693,12 @@ __global__ void amax_kernel(const float* __restrict__ x, long long n, float* __r
 
 // One launch, no clearing: exactly STX_AMAX_SLOTS blocks, block b reduces slice b of x
 // and stores its max into slot b (plain store), so the group's max is max|x|.
-__global__ void __launch_bounds__(1024) amax_slots_kernel(const float* __restrict__ x,
-                                                          long long n, float* __restrict__ out) {
+__device__ __forceinline__ void amax_slot_body(const float* __restrict__ x, long long n,
+                                               float* __restrict__ out, int slot) {
   __shared__ float red[16];
   const long long n4 = n >> 2;
   const long long per = (n4 + STX_AMAX_SLOTS - 1) / STX_AMAX_SLOTS;
-  const long long b0 = blockIdx.x * per, b1 = min(n4, b0 + per);
+  const long long b0 = slot * per, b1 = min(n4, b0 + per);
   float m = 0.f;
   auto upd = [&](float v) {
     const float a = fabsf(v);
@@ -705,7 +712,7 @@ __global__ void __launch_bounds__(1024) amax_slots_kernel(const float* __restric
     upd(v[2]);
     upd(v[3]);
   }
-  if (blockIdx.x == 0)
+  if (slot == 0)
     for (long long i = 4 * n4 + threadIdx.x; i < n; i += 1024) upd(x[i]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -718,8 +725,51 @@ __global__ void __launch_bounds__(1024) amax_slots_kernel(const float* __restric
     float r = red[0];
 #pragma unroll
     for (int i = 1; i < 16; ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
-    out[blockIdx.x] = r;
+    out[slot] = r;
   }
+}
+
+__global__ void __launch_bounds__(1024) amax_slots_kernel(const float* __restrict__ x,
+                                                          long long n, float* __restrict__ out) {
+  amax_slot_body(x, n, out, blockIdx.x);
+}
+
+// ------------------------------------------------------- batched weight prep
+// Every slab of a trained network re-prepped in two launches per step (the ITN: 31
+// slabs of 14 weights would otherwise be ~35 launches, each a few microseconds of
+// launch-bound tail): (1) the max|w| groups of the distinct split-slab weights, 32
+// blocks each; (2) all conversions, a fixed block range per job.
+struct WprepAmax {
+  const float* w[STX_WPREP_MAX];
+  float* out[STX_WPREP_MAX];
+  long long n[STX_WPREP_MAX];
+};
+
+__global__ void __launch_bounds__(1024) amax_batch_kernel(WprepAmax a) {
+  const int j = blockIdx.x / STX_AMAX_SLOTS;
+  amax_slot_body(a.w[j], a.n[j], a.out[j], blockIdx.x % STX_AMAX_SLOTS);
+}
+
+struct WprepJobs {
+  stx_wprep_job job[STX_WPREP_MAX];
+  int blk0[STX_WPREP_MAX + 1];  // first block of each job (prefix sums)
+  int gin[STX_WPREP_MAX], gout[STX_WPREP_MAX];  // padded GEMM dims of the slab
+  int njobs;
+};
+
+__global__ void __launch_bounds__(256) weight_prep_batch_kernel(WprepJobs b) {
+  int j = 0;
+  while (j + 1 < b.njobs && (int)blockIdx.x >= b.blk0[j + 1]) ++j;
+  const stx_wprep_job& t = b.job[j];
+  const int nb = b.blk0[j + 1] - b.blk0[j];
+  const long long i0 = (long long)(blockIdx.x - b.blk0[j]) * 256 + threadIdx.x;
+  const long long step = (long long)nb * 256;
+  if (t.kind == STX_WPREP_F16)
+    weight_prep16_body(t.w, reinterpret_cast<_Float16*>(t.slab), t.w_amax, t.cout, t.cin,
+                       t.transpose, b.gin[j], b.gout[j], i0, step);
+  else
+    weight_prep32_body(t.w, reinterpret_cast<float*>(t.slab), t.cout, t.cin, t.ks, t.transpose,
+                       b.gin[j], b.gout[j], i0, step);
 }
 
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st) {
@@ -781,11 +831,84 @@ extern "C" int stx_conv_weight_prep16_pair(const float* w, void* wt16, void* wtT
   if (rc) return rc;
   const long long total = std::max((long long)rup(cin, 16) * rup(cout, 64),
                                    (long long)rup(cout, 16) * rup(cin, 64)) * 9 * 2;
+  if (total >= (1ll << 31)) {
+    set_error("stx_conv_weight_prep16_pair: slab too large");
+    return STX_E_INVALID;
+  }
   const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(weight_prep16_pair_kernel, dim3(blocks, 2), dim3(256), 0,
                      (hipStream_t)stream, w, reinterpret_cast<_Float16*>(wt16),
                      reinterpret_cast<_Float16*>(wtT16), w_amax, cout, cin);
   return check_launch("stx_conv_weight_prep16_pair");
+}
+
+extern "C" int stx_conv_weight_prep_batch(const stx_wprep_job* jobs, int njobs, void* stream) {
+  if (!jobs || njobs <= 0 || njobs > STX_WPREP_MAX) {
+    set_error("stx_conv_weight_prep_batch: 1 <= njobs <= %d required", STX_WPREP_MAX);
+    return STX_E_INVALID;
+  }
+  WprepAmax a{};
+  WprepJobs b{};
+  int na = 0, blocks = 0;
+  b.njobs = njobs;
+  for (int j = 0; j < njobs; ++j) {
+    const stx_wprep_job& t = jobs[j];
+    if (!t.w || !t.slab || t.cout <= 0 || t.cin <= 0 ||
+        (t.kind != STX_WPREP_F32 && t.kind != STX_WPREP_F16) ||
+        (t.kind == STX_WPREP_F16 && (t.ks != 3 || !t.w_amax))) {
+      set_error("stx_conv_weight_prep_batch: job %d invalid", j);
+      return STX_E_INVALID;
+    }
+    const int gin = t.transpose ? t.cout : t.cin, gout = t.transpose ? t.cin : t.cout;
+    long long total;
+    if (t.kind == STX_WPREP_F16) {
+      if (reinterpret_cast<uintptr_t>(t.w) & 15) {
+        set_error("stx_conv_weight_prep_batch: job %d weight not 16-byte aligned", j);
+        return STX_E_INVALID;
+      }
+      b.gin[j] = rup(gin, 16);
+      b.gout[j] = rup(gout, 64);
+      total = (long long)b.gin[j] * 9 * 2 * b.gout[j];
+      bool seen = false;  // the forward / data-gradient slabs of a weight share one group
+      for (int k = 0; k < na; ++k) {
+        if (a.out[k] == t.w_amax) {
+          if (a.w[k] != t.w) {
+            set_error("stx_conv_weight_prep_batch: w_amax shared by two weights");
+            return STX_E_INVALID;
+          }
+          seen = true;
+        }
+      }
+      if (!seen) {
+        a.w[na] = t.w;
+        a.out[na] = t.w_amax;
+        a.n[na] = (long long)t.cout * t.cin * 9;
+        ++na;
+      }
+    } else {
+      int rp, cp;
+      int rc = stx_conv_weight_dims(gin, gout, t.ks, &rp, &cp);
+      if (rc) return rc;
+      b.gin[j] = rp * t.ks * t.ks;
+      b.gout[j] = cp;
+      total = (long long)b.gin[j] * cp;
+    }
+    if (total >= (1ll << 31)) {
+      set_error("stx_conv_weight_prep_batch: job %d slab too large", j);
+      return STX_E_INVALID;
+    }
+    b.job[j] = t;
+    b.blk0[j] = blocks;
+    // ~16 elements per thread: the per-thread setup (job lookup, the 32-slot max|w|
+    // read) costs as much as a handful of elements
+    blocks += (int)std::min<long long>((total + 4095) / 4096, 256);
+  }
+  b.blk0[njobs] = blocks;
+  hipStream_t st = (hipStream_t)stream;
+  if (na > 0)
+    hipLaunchKernelGGL(amax_batch_kernel, dim3(na * STX_AMAX_SLOTS), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(weight_prep_batch_kernel, dim3(blocks), dim3(256), 0, st, b);
+  return check_launch("stx_conv_weight_prep_batch");
 }
 
 extern "C" int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax, int cout, int cin,
@@ -799,6 +922,10 @@ extern "C" int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax,
   const int gin = transpose ? cout : cin, gout = transpose ? cin : cout;
   const int gin16 = rup(gin, 16), gout64 = rup(gout, 64);
   const long long total = (long long)gin16 * 9 * 2 * gout64;
+  if (total >= (1ll << 31)) {
+    set_error("stx_conv_weight_prep16: slab too large");
+    return STX_E_INVALID;
+  }
   const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(weight_prep16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w,
                      reinterpret_cast<_Float16*>(wt16), w_amax, cout, cin, transpose, gin16,

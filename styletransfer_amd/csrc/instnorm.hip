@@ -161,6 +161,7 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
   const float k = gm * rs / (float)hw;
   float* dup = du + base;
   uint32_t om = 0u;  // max |du| as IEEE bits
+  float sdu = 0.f;   // sum du: the gradient of the producing conv's bias
   if (vec) {
     for (int i = threadIdx.x * 4; i < hw; i += NBT * 4) {
       const f32x4 d4 = ld4(dyp, i);
@@ -174,6 +175,7 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
         const float xh = (x4[e] + r4[e] - mu) * rs;
         o[e] = k * ((float)hw * g - sg - xh * sgx);
         om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
+        sdu += o[e];
       }
       *reinterpret_cast<f32x4*>(dup + i) = o;
     }
@@ -185,11 +187,14 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
       const float o = k * ((float)hw * g - sg - xh * sgx);
       dup[i] = o;
       om = max(om, __float_as_uint(o) & 0x7fffffffu);
+      sdu += o;
     }
   }
+  sdu = block_sum<NBT>(sdu, red);
   if (threadIdx.x == 0) {
-    parts[2 * blockIdx.x] = sgx;
-    parts[2 * blockIdx.x + 1] = sg;
+    parts[3 * blockIdx.x] = sgx;
+    parts[3 * blockIdx.x + 1] = sg;
+    parts[3 * blockIdx.x + 2] = sdu;
   }
   if (out_amax) block_max_to_nt<NBT>(out_amax, om, red);
 }
@@ -331,6 +336,7 @@ instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ 
   const float kk = gm * rs / (float)hw;
   f32x4* dup = reinterpret_cast<f32x4*>(du + base);
   uint32_t om = 0u;
+  float sdu = 0.f;  // sum du: the gradient of the producing conv's bias
 #pragma unroll
   for (int k = 0; k < R4; ++k) {
     const int i = threadIdx.x + k * NT;
@@ -342,11 +348,14 @@ instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ 
         om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
       }
       dup[i] = o;
+      sdu += (o[0] + o[1]) + (o[2] + o[3]);
     }
   }
+  sdu = block_sum_nt<NT>(sdu, red);
   if (threadIdx.x == 0) {
-    parts[2 * blockIdx.x] = sgx;
-    parts[2 * blockIdx.x + 1] = sg;
+    parts[3 * blockIdx.x] = sgx;
+    parts[3 * blockIdx.x + 1] = sg;
+    parts[3 * blockIdx.x + 2] = sdu;
   }
   if (out_amax) {
     uint32_t m = om;
@@ -364,18 +373,22 @@ instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ 
   }
 }
 
+// dgamma, dbeta and the producing conv's bias gradient: fixed-order sums over n
 __global__ void instnorm_param_grad_kernel(const float* __restrict__ parts, int n, int c,
                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                           int accumulate) {
+                                           float* __restrict__ dbias, int accumulate) {
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= c) return;
-  float a = 0.f, b = 0.f;
+  float a = 0.f, b = 0.f, d = 0.f;
   for (int k = 0; k < n; ++k) {
-    a += parts[2 * ((size_t)k * c + ch)];
-    b += parts[2 * ((size_t)k * c + ch) + 1];
+    const float* p = parts + 3 * ((size_t)k * c + ch);
+    a += p[0];
+    b += p[1];
+    d += p[2];
   }
   if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + a : a;
   if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + b : b;
+  if (dbias) dbias[ch] = accumulate ? dbias[ch] + d : d;
 }
 
 }  // namespace stx
@@ -411,14 +424,14 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
 }
 
 extern "C" size_t stx_instnorm_bwd_ws(int n, int c) {
-  return (size_t)2 * n * c * sizeof(float) + 64;
+  return (size_t)3 * n * c * sizeof(float) + 64;
 }
 
 extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
                                 const float* gamma, const float* mean, const float* rstd,
-                                float* du, float* dgamma, float* dbeta, int n, int c, int hw,
-                                int relu, int accumulate_params, float* out_amax, void* ws,
-                                size_t ws_bytes, void* stream) {
+                                float* du, float* dgamma, float* dbeta, float* dbias_in, int n,
+                                int c, int hw, int relu, int accumulate_params, float* out_amax,
+                                void* ws, size_t ws_bytes, void* stream) {
   if (n <= 0 || c <= 0 || hw <= 0 || !dy || !x || !du || !mean || !rstd || (relu && !y)) {
     set_error("stx_instnorm_bwd: invalid args");
     return STX_E_INVALID;
@@ -443,8 +456,8 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
   else
     hipLaunchKernelGGL(instnorm_bwd_kernel<NB>, dim3(n * c), dim3(NB), 0, st, dy, y, x, res, gamma,
                        mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
-  if (dgamma || dbeta)
+  if (dgamma || dbeta || dbias_in)
     hipLaunchKernelGGL(instnorm_param_grad_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st,
-                       (const float*)ws, n, c, dgamma, dbeta, accumulate_params);
+                       (const float*)ws, n, c, dgamma, dbeta, dbias_in, accumulate_params);
   return check_launch("stx_instnorm_bwd");
 }

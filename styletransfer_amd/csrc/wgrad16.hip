@@ -40,6 +40,7 @@ struct Wg16 {
   int ncot, ncit, nsplit, steps, steps_per_split;
   int cout32, cin32;
   int ci2;  // cout <= 32: a wave takes 32 couts x 64 cins (two cin tiles), not 64 x 32
+  int lds;  // wgrad16_lds_kernel geometry (cout 64/128, 64-cin tiles, 1 block per CU)
 };
 
 constexpr int WG16_S2 = 16;  // private mode: stride 2, pad 1, raw input (h = 2 hv, w = 2 wv)
@@ -416,6 +417,201 @@ wgrad16_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg1
   }
 }
 
+// LDS-staged variant for the ITN's stride-1 layers with cout in {64, 128} and
+// cin % 64 == 0 (the residual convs 128 -> 128, the up convs 128 -> 64): a block
+// owns (all couts, 64 cins, kh) over a K split and steps through 16-pixel rows.
+// The V row segment (64 cins x 18 pixels incl. the kw halo) is split ONCE per block
+// into fp16 hi/lo and written to LDS as the three kw-shifted copies the B fragments
+// need ([kw][plane][h][ci][8 fp16]: every fragment one conflict-free ds_read_b128);
+// each wave keeps its own 32 couts of dY register-direct (A fragments, split in
+// registers).  Double-buffered V images, one barrier per step, the next steps'
+// global loads in flight.  Against wgrad16_kernel this removes the 4x redundant
+// V conversion of its four waves and halves the number of K splits (1 block per CU
+// instead of 8 waves), so the split-K slab the reduce kernel reads is half as big.
+template <int WCO, bool UP, int PF>  // WCO = couts / 32; UP: nearest x2 upsampled input;
+__global__ void __launch_bounds__(256, 1)  // PF + 1 steps of loads in flight (PF odd)
+wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                   float* __restrict__ ws, const float* __restrict__ x_amax,
+                   const float* __restrict__ dy_amax, Wg16 g) {
+  constexpr int NPAIR = WCO * 2 / 4;       // (co tile, ci tile) pairs per wave
+  __shared__ __attribute__((aligned(16))) char vimg[2][3 * 2 * 2 * 64 * 16];  // 2 x 12 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  int unit = blockIdx.x;
+  const int cit = unit % g.ncit;           // 64-cin tile
+  unit /= g.ncit;
+  const int kh = unit % 3;
+  const int split = unit / 3;
+  const int ex = wg_amax_exp(read_amax(x_amax)), ed = wg_amax_exp(read_amax(dy_amax));
+  const float sv = __builtin_ldexpf(1.f, 15 - ex), sd = __builtin_ldexpf(1.f, 15 - ed);
+  const float descale = __builtin_ldexpf(1.f, ex + ed - 30);
+  const int H = g.hv, W = g.wv, wsteps = W / 16;
+  const bool relu = g.mode == STX_IN_RELU;
+  // this wave's (co tile, ci tile) pairs: WCO = 4 -> co tile = wave, ci tiles 0, 1;
+  // WCO = 2 -> co tile = wave & 1, ci tile = wave >> 1
+  const int cot = WCO == 4 ? wave : (wave & 1);
+  const int co = cot * 32 + l32;
+  // V staging: thread -> (ci = tid / 4, quad q = tid % 4): pixels x0 + 4q - 1 .. x0 + 4q + 4
+  const int sci = tid >> 2, q = tid & 3;
+  const int ci_g = cit * 64 + sci;
+  const auto rdy = make_srd(dy, (uint32_t)((size_t)g.n * g.cout * H * W * 4u));
+  const auto rx = make_srd(x, (uint32_t)((size_t)g.n * g.cin * g.h * g.w * 4u));
+  struct Ld {
+    f32x4 a0, a1;        // dY[co][y][x0 + 8h .. +7]
+    f32x4 v;             // V[ci][vy][x0 + 4q .. +3] (upsample: x[.][vy/2][(x0+4q)/2 .. +1] in v.xy)
+    float vl, vr;        // V at x0 + 4q - 1 and x0 + 4q + 4
+  };
+  // Every load is issued unconditionally (steps past the split's end read zeros
+  // through out-of-range offsets) so the wait counts stay exact: no branch around a
+  // load, no vmcnt(0) before the LDS staging.
+  int ln, ly, lxs, lleft;  // running (image, row, 16-px column step) of the next load, steps left
+  auto load = [&](Ld& t) {
+    const int n = ln, y = ly, x0 = lxs * 16;
+    const bool live = lleft-- > 0;
+    if (++lxs == wsteps) {
+      lxs = 0;
+      if (++ly == H) {
+        ly = 0;
+        ++ln;
+      }
+    }
+    const uint32_t oa = (uint32_t)((((size_t)n * g.cout + co) * H + y) * W + x0 + 8 * h) * 4u;
+    t.a0 = buf_ld4(rdy, live ? oa : BUF_OOB);
+    t.a1 = buf_ld4(rdy, live ? oa + 16u : BUF_OOB);
+    const int vy = y + kh - 1, px = x0 + 4 * q;
+    const bool rok = live && vy >= 0 && vy < H;
+    if constexpr (!UP) {
+      const uint32_t ob = (uint32_t)((((size_t)n * g.cin + ci_g) * g.h + vy) * g.w + px) * 4u;
+      t.v = buf_ld4(rx, rok ? ob : BUF_OOB);
+      t.vl = buf_ld(rx, (rok && px > 0) ? ob - 4u : BUF_OOB);
+      t.vr = buf_ld(rx, (rok && px + 4 < W) ? ob + 16u : BUF_OOB);
+    } else {  // V[vy][vx] = x[vy/2][vx/2]; px is a multiple of 4
+      const uint32_t ob =
+          (uint32_t)((((size_t)n * g.cin + ci_g) * g.h + (vy >> 1)) * g.w + (px >> 1)) * 4u;
+      t.v.x = buf_ld(rx, rok ? ob : BUF_OOB);
+      t.v.y = buf_ld(rx, rok ? ob + 4u : BUF_OOB);
+      t.vl = buf_ld(rx, (rok && px > 0) ? ob - 4u : BUF_OOB);
+      t.vr = buf_ld(rx, (rok && px + 4 < W) ? ob + 8u : BUF_OOB);
+    }
+  };
+  // V -> the three kw-shifted fp16 hi/lo copies in LDS (thread: 4 pixels of one ci)
+  auto stage = [&](const Ld& t, char* img) {
+    float v6[6];
+    v6[0] = t.vl;
+    v6[5] = t.vr;
+    if constexpr (!UP) {
+      v6[1] = t.v.x; v6[2] = t.v.y; v6[3] = t.v.z; v6[4] = t.v.w;
+    } else {
+      v6[1] = v6[2] = t.v.x;
+      v6[3] = v6[4] = t.v.y;
+    }
+    _Float16 hi[6], lo[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      float v = v6[e];
+      if (relu) v = fmaxf(v, 0.f);
+      v *= sv;
+      hi[e] = (_Float16)v;
+      lo[e] = (_Float16)(v - (float)hi[e]);
+    }
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      // copy kw, element e = 4q + j holds V[x0 + e + kw - 1] = v6[j + kw]
+      const h4 ph = {hi[kw], hi[kw + 1], hi[kw + 2], hi[kw + 3]};
+      const h4 pl = {lo[kw], lo[kw + 1], lo[kw + 2], lo[kw + 3]};
+      const int base = (((kw * 2 + 0) * 2 + (q >> 1)) * 64 + sci) * 16 + (q & 1) * 8;
+      const int base_l = (((kw * 2 + 1) * 2 + (q >> 1)) * 64 + sci) * 16 + (q & 1) * 8;
+      *reinterpret_cast<h4*>(img + base) = ph;
+      *reinterpret_cast<h4*>(img + base_l) = pl;
+    }
+  };
+  f32x16 acc[NPAIR][3];
+#pragma unroll
+  for (int i = 0; i < NPAIR; ++i)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
+  auto compute = [&](const Ld& t, const char* img) {
+    h8 ah, al;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (e < 4 ? t.a0[e] : t.a1[e - 4]) * sd;
+      ah[e] = (_Float16)v;
+      al[e] = (_Float16)(v - (float)ah[e]);
+    }
+#pragma unroll
+    for (int pi = 0; pi < NPAIR; ++pi) {
+      const int ct = WCO == 4 ? pi : (wave >> 1);   // ci tile (32 cins) within the 64
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const h8 bh = *reinterpret_cast<const h8*>(img + (((kw * 2 + 0) * 2 + h) * 64 + ct * 32 + l32) * 16);
+        const h8 bl = *reinterpret_cast<const h8*>(img + (((kw * 2 + 1) * 2 + h) * 64 + ct * 32 + l32) * 16);
+        acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[pi][kw], 0, 0, 0);
+        acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[pi][kw], 0, 0, 0);
+        acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[pi][kw], 0, 0, 0);
+      }
+    }
+  };
+  const int s0 = split * g.steps_per_split;
+  const int nst = min(g.steps, s0 + g.steps_per_split) - s0;  // >= 1
+  {
+    const int r0 = s0 / wsteps;
+    lxs = s0 - r0 * wsteps;
+    ln = r0 / H;
+    ly = r0 - ln * H;
+    lleft = nst;
+  }
+  // steps run in groups of PF + 1 (a ring slot per step); a ragged last group computes
+  // on zeros
+  Ld ring[PF + 1];
+#pragma unroll
+  for (int k = 0; k <= PF; ++k) load(ring[k]);
+  stage(ring[0], vimg[0]);
+  __syncthreads();
+  for (int s = 0; s < nst; s += PF + 1) {
+#pragma unroll
+    for (int k = 0; k <= PF; ++k) {
+      stage(ring[(k + 1) % (PF + 1)], vimg[(k + 1) & 1]);  // the next step's V image
+      compute(ring[k], vimg[k & 1]);
+      load(ring[k]);  // step s + k + PF + 1
+      __syncthreads();  // lgkmcnt(0) + s_barrier: the global loads stay in flight
+    }
+  }
+  // partial [split][kh*3+kw][co (cout32)][ci (cin32)], descaled (exact)
+#pragma unroll
+  for (int pi = 0; pi < NPAIR; ++pi) {
+    const int ct = WCO == 4 ? pi : (wave >> 1);
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      float* out = ws + (((size_t)split * 9 + kh * 3 + kw) * g.cout32 + cot * 32) * g.cin32 +
+                   cit * 64 + ct * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[(size_t)row * g.cin32] = acc[pi][kw][r] * descale;
+      }
+    }
+  }
+}
+
+static bool wg16_lds_on() {
+  static const bool on = [] {
+    const char* e = getenv("STX_WG16_LDS");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+static bool lds_on_64() {  // cout 64 on the LDS kernel: 1.6x slower (A/B), off by default
+  static const bool on = [] {
+    const char* e = getenv("STX_WG16_LDS64");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg16& g) {
   if (wv % 16 != 0 || cin < 16 || cout < 16 || n <= 0 || hv <= 0) return false;
   // 32-bit buffer offsets over the whole dy / x tensors
@@ -446,6 +642,24 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
     g.cin32 = g.ncit * 32;
   }
   g.steps = n * hv * (wv / 16);
+  g.lds = wg16_lds_on() && (cout == 128 || (cout == 64 && lds_on_64())) && cin % 64 == 0 &&
+          (in_mode == STX_IN_RAW || in_mode == STX_IN_RELU || in_mode == STX_IN_UPSAMPLE2);
+  if (g.lds) {  // blocks of (all couts x 64 cins x kh) x K split: ~512 blocks
+    g.ncot = 1;
+    g.ncit = cin / 64;
+    g.cout32 = cout;
+    g.cin32 = cin;
+    g.ci2 = 0;
+    static const int lblocks = [] {
+      const char* e = getenv("STX_WG16_LBLOCKS");  // 512 measured 10 % faster than 256 / 128
+      return e ? atoi(e) : 512;
+    }();
+    int ns = cdiv(lblocks, 3 * g.ncit);
+    ns = std::max(1, std::min(ns, cdiv(g.steps, 8)));
+    g.steps_per_split = cdiv(g.steps, ns);
+    g.nsplit = cdiv(g.steps, g.steps_per_split);
+    return true;
+  }
   const int units = 3 * g.ncot * g.ncit;
   static const int target = [] {
     const char* e = getenv("STX_WG16_WAVES");
@@ -502,7 +716,22 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
     const char* e = getenv("STX_WG16_PF");
     return e ? atoi(e) : 4;
   }();
-  if (g.ci2)
+  if (g.lds) {
+    const int blocks = g.nsplit * 3 * g.ncit;
+    const bool up = in_mode == STX_IN_UPSAMPLE2;
+    static const int lpf = [] {
+      const char* e = getenv("STX_WG16_LPF");
+      return e ? atoi(e) : 3;
+    }();
+    auto kern = cout == 128
+        ? (up ? wgrad16_lds_kernel<4, true, 3>
+              : (lpf >= 7 ? wgrad16_lds_kernel<4, false, 7>
+                          : (lpf >= 5 ? wgrad16_lds_kernel<4, false, 5>
+                                      : wgrad16_lds_kernel<4, false, 3>)))
+        : (up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, x, dy, (float*)ws, x_amax, dy_amax,
+                       g);
+  } else if (g.ci2)
     hipLaunchKernelGGL((wgrad16_kernel<4, false, true>), dim3(cdiv(units, 4)), dim3(256), 0, st,
                        x, dy, (float*)ws, x_amax, dy_amax, g);
   else if (g.mode == WG16_S2)

@@ -29,6 +29,7 @@ class Conv2d(nn.Conv2d):
         if self.kernel_size[0] != self.kernel_size[1] or self.kernel_size[0] not in (1, 3, 9):
             raise NotImplementedError(f"kernel_size {self.kernel_size}")
         self._wt_cache = None
+        self._train_slabs = None  # set by ops.TrainedSlabs.prep() (fast_st trainers)
 
     def prepped(self):
         """Cached GEMM slabs (fp32, and the fp16 hi/lo split slab where the shape
@@ -45,12 +46,18 @@ class Conv2d(nn.Conv2d):
             self._wt_cache = (key, ops.conv_weight_prep(wd), w16)
         return self._wt_cache[1], self._wt_cache[2]
 
-    def forward(self, x, in_mode=N.STX_IN_RAW):
-        wt = wt16 = None
-        if not self.weight.requires_grad or not torch.is_grad_enabled():
+    def forward(self, x, in_mode=N.STX_IN_RAW, bias_grad=True):
+        """bias_grad=False: the bias enters detached -- for a conv feeding an
+        InstanceNorm2d that is handed the bias (`conv_bias=`) and produces its gradient."""
+        wt = wt16 = wtT = wtT16 = None
+        ts = self._train_slabs
+        w = self.weight
+        if ts is not None and ts[0] == (w.data_ptr(), w._version, w.device):
+            _, wt, wt16, wtT, wtT16 = ts  # the trainer's batched prep of this version
+        elif not w.requires_grad or not torch.is_grad_enabled():
             wt, wt16 = self.prepped()  # frozen or inference: slabs cached per weight version
-        return A.conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], in_mode, wt,
-                        wt16)
+        b = self.bias if bias_grad or self.bias is None else self.bias.detach()
+        return A.conv2d(x, w, b, self.stride[0], self.padding[0], in_mode, wt, wt16, wtT, wtT16)
 
 
 class ReLU(nn.ReLU):
@@ -71,10 +78,11 @@ class MaxPool2d(nn.MaxPool2d):
 
 
 class InstanceNorm2d(nn.InstanceNorm2d):
-    def forward(self, x, relu=False, res=None):
+    def forward(self, x, relu=False, res=None, conv_bias=None):
         if self.track_running_stats:
             raise NotImplementedError("track_running_stats")
-        return A.instance_norm(x, self.weight, self.bias, res=res, eps=self.eps, relu=relu)
+        return A.instance_norm(x, self.weight, self.bias, res=res, eps=self.eps, relu=relu,
+                               conv_bias=conv_bias)
 
 
 class Upsample(nn.Upsample):

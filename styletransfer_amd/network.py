@@ -377,8 +377,10 @@ class ResidualBlock(nn.Module):
         self.insn2 = InstanceNorm2d(out_channels, affine=True)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = self.insn1(self.conv1(x), relu=True)       # IN + ReLU fused
-        return self.insn2(self.conv2(out), res=x)        # (+ residual) + IN fused
+        # IN + ReLU fused; (+ residual) + IN fused; each conv's bias gradient comes out of
+        # the following IN's backward kernel (conv bias passed detached)
+        out = self.insn1(self.conv1(x, bias_grad=False), relu=True, conv_bias=self.conv1.bias)
+        return self.insn2(self.conv2(out, bias_grad=False), res=x, conv_bias=self.conv2.bias)
 
 
 def _itn_layers(in_channels=3):
@@ -424,13 +426,16 @@ class ImageTransformNet(nn.Sequential):
                 i += 1
                 continue
             if isinstance(m, nn.Conv2d):
-                x = m(x, N.STX_IN_UPSAMPLE2 if up else N.STX_IN_RAW)
+                mode = N.STX_IN_UPSAMPLE2 if up else N.STX_IN_RAW
                 up = False
                 if isinstance(nxt, nn.InstanceNorm2d):
+                    # the IN backward produces the conv's bias gradient (sum du)
+                    x = m(x, mode, bias_grad=False)
                     relu = i + 2 < len(mods) and isinstance(mods[i + 2], nn.ReLU)
-                    x = nxt(x, relu=relu)
+                    x = nxt(x, relu=relu, conv_bias=m.bias)
                     i += 3 if relu else 2
                     continue
+                x = m(x, mode)
             else:
                 x = m(x)
             i += 1

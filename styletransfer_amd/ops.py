@@ -184,6 +184,69 @@ def conv_weight_prep16_pair(w: torch.Tensor):
     return (wt16, w_amax), (wtT16, w_amax)
 
 
+class TrainedSlabs:
+    """The GEMM weight slabs of a trained network's conv layers, re-prepped after
+    every parameter update in two launches (stx_conv_weight_prep_batch) instead of
+    ~2 per slab.  For each layer the slabs the forward and the input-gradient kernels
+    of autograd.Conv2dFn will select: the fp16 hi/lo split slab (shapes the split
+    kernel takes) or the fp32 k-major slab, for the forward and the transposed
+    data-gradient GEMM; forward and data-gradient split slabs share one max|w| group.
+
+    `prep()` enqueues the batch and hands each layer `_train_slabs = (key, wt, wt16,
+    wtT, wtT16)` keyed on the weight's (pointer, version): layers.Conv2d uses the
+    slabs only while the key matches, so a weight changed behind the trainer's back
+    falls back to per-call preps."""
+
+    def __init__(self, convs):
+        self.convs = list(convs)
+        self._build()
+
+    def _build(self):
+        split = os.environ.get("STX_CONV_SPLIT", "1") != "0"
+        L = lib()
+        jobs = []
+        self.slabs = []
+        for conv in self.convs:
+            w = conv.weight
+            cout, cin, ks, _ = w.shape
+            stride, pad = conv.stride[0], conv.padding[0]
+            f16 = split and pad == 1 and split_eligible(cin, cout, ks, stride)
+            b16 = split and pad == 1 and split_eligible(cout, cin, ks, 1)
+            dev = w.device
+            am = torch.empty(N.STX_AMAX_SLOTS, device=dev, dtype=torch.float32) \
+                if (f16 or b16) else None
+            out = []
+            for t, is16 in ((0, f16), (1, b16)):
+                if is16:
+                    slab = torch.empty(L.stx_conv_weight16_bytes(cin, cout, ks, t), device=dev,
+                                       dtype=torch.uint8)
+                    jobs.append(N.WprepJob(w.data_ptr(), slab.data_ptr(), am.data_ptr(),
+                                           N.STX_WPREP_F16, cout, cin, ks, t, 0))
+                    out.append((None, (slab, am)))
+                else:
+                    gin, gout = (cout, cin) if t else (cin, cout)
+                    cp, op = conv_weight_dims(gin, gout, ks)
+                    slab = torch.empty((cp * ks * ks, op), device=dev, dtype=torch.float32)
+                    jobs.append(N.WprepJob(w.data_ptr(), slab.data_ptr(), None,
+                                           N.STX_WPREP_F32, cout, cin, ks, t, 0))
+                    out.append((slab, None))
+            self.slabs.append((w.data_ptr(), out[0][0], out[0][1], out[1][0], out[1][1]))
+        if len(jobs) > N.STX_WPREP_MAX:
+            raise N.NativeError(f"{len(jobs)} weight slabs > STX_WPREP_MAX")
+        self._jobs = (N.WprepJob * len(jobs))(*jobs)
+        self._njobs = len(jobs)
+
+    def prep(self):
+        if any(c.weight.data_ptr() != s[0] for c, s in zip(self.convs, self.slabs)):
+            self._build()  # a parameter was re-homed
+        if self._njobs:
+            check(lib().stx_conv_weight_prep_batch(self._jobs, self._njobs, _stream()),
+                  "conv_weight_prep_batch")
+        for c, (_, wt, wt16, wtT, wtT16) in zip(self.convs, self.slabs):
+            w = c.weight
+            c._train_slabs = ((w.data_ptr(), w._version, w.device), wt, wt16, wtT, wtT16)
+
+
 _S2_FWD = os.environ.get("STX_S2_FWD", "1") != "0"
 
 
@@ -561,7 +624,9 @@ def instnorm_fwd(x, gamma, beta, res=None, eps=1e-5, relu=False, out=None, out_a
 
 
 def instnorm_bwd(dy, y, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbeta=None,
-                 accumulate=False, out_amax=None):
+                 accumulate=False, out_amax=None, dbias_in=None):
+    """du of y = [relu](IN(x (+res))*gamma + beta); dgamma / dbeta / dbias_in (the bias
+    gradient of the conv that produced x, sum du) written or accumulated when given."""
     n, c = x.shape[:2]
     hw = x[0, 0].numel()
     du = torch.empty_like(x)
@@ -569,7 +634,8 @@ def instnorm_bwd(dy, y, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbet
     wp, wn = WS.get(L.stx_instnorm_bwd_ws(n, c), x.device)
     check(L.stx_instnorm_bwd(dy.data_ptr(), _p(y), x.data_ptr(), _p(res), _p(gamma),
                              mean.data_ptr(), rstd.data_ptr(), du.data_ptr(), _p(dgamma),
-                             _p(dbeta), n, c, hw, int(relu), int(accumulate), _p(out_amax), wp,
+                             _p(dbeta), _p(dbias_in), n, c, hw, int(relu), int(accumulate),
+                             _p(out_amax), wp,
                              wn, _stream()), "stx_instnorm_bwd")
     return du
 

@@ -70,6 +70,9 @@ class FastStTrainer:
         self.opt = FlatAdam(self.flat, self.flat_grad, lr=lr, params=self.params)
         self.vgg_weights = vgg_weights
         self._graph = None  # (replay, static batch, static loss) of train_step
+        from .layers import Conv2d
+        # every conv slab of the ITN re-prepped in two launches per step
+        self.slabs = ops.TrainedSlabs(m for m in itn.modules() if isinstance(m, Conv2d))
 
     def _src(self):
         """Global rank of the group's rank 0."""
@@ -98,6 +101,7 @@ class FastStTrainer:
     def _fwd_bwd(self, batch: torch.Tensor) -> torch.Tensor:
         """Local loss and gradient (into flat_grad) of one batch."""
         self.flat_grad.zero_()
+        self.slabs.prep()
         ops.ARENA.begin(self.device)  # InstanceNorm outputs carry their max|.| to the convs
         try:
             y = self.itn(batch)
@@ -226,6 +230,7 @@ class VideoTrainer(FastStTrainer):
     def step(self, batch: torch.Tensor) -> torch.Tensor:
         batch, old_c, old_s, x6 = self._inputs(batch)
         self.flat_grad.zero_()
+        self.slabs.prep()
         ops.ARENA.begin(self.device)
         try:
             y = self.itn(x6)

@@ -284,7 +284,12 @@ def test_split_gram_bwd_window_ties(dev, c):
                                   # cout <= 32: 32 x 64 wave tiles (two cin rows per lane)
                                   (2, 64, 32, 8, 16, N.STX_IN_UPSAMPLE2),
                                   (2, 72, 32, 12, 32, N.STX_IN_RAW),
-                                  (1, 64, 16, 16, 32, N.STX_IN_RELU)])
+                                  (1, 64, 16, 16, 32, N.STX_IN_RELU),
+                                  # cout 64/128, cin % 64 == 0: the LDS-staged kernel
+                                  (2, 64, 64, 12, 32, N.STX_IN_RELU),
+                                  (1, 128, 128, 1, 16, N.STX_IN_RAW),
+                                  (3, 192, 64, 10, 24, N.STX_IN_UPSAMPLE2),
+                                  (1, 64, 128, 3, 16, N.STX_IN_RAW)])
 def test_split_wgrad(dev, case):
     """3x3 weight gradient on the split MFMA vs fp64 (and the fp32 MFMA kernel)."""
     n, cin, cout, h, w, mode = case

@@ -98,24 +98,27 @@ def main():
         print(f"{name:32s} fwd {ms * 1e3:8.1f} us {gf / ms:7.2f} TF | bwd {ms2 * 1e3:8.1f} us "
               f"{gf / ms2:7.2f} TF")
     # wgrad
-    for name, n, cin, cout, h, ks, s in (("wgrad res B8 128 64^2", 8, 128, 128, 64, 3, 1),
-                                         ("wgrad conv0 9x9 B8", 8, 3, 32, 256, 9, 1),
-                                         ("wgrad conv22 9x9 B8", 8, 32, 3, 256, 9, 1),
-                                         ("wgrad down s2 B8 32->64 256", 8, 32, 64, 256, 3, 2),
-                                         ("wgrad down s2 B8 64->128 128", 8, 64, 128, 128, 3, 2)):
+    up = N.STX_IN_UPSAMPLE2
+    for name, n, cin, cout, h, ks, s, mode in (
+            ("wgrad res B8 128 64^2", 8, 128, 128, 64, 3, 1, 0),
+            ("wgrad up B8 128->64 128^2", 8, 128, 64, 64, 3, 1, up),
+            ("wgrad conv0 9x9 B8", 8, 3, 32, 256, 9, 1, 0),
+            ("wgrad conv22 9x9 B8", 8, 32, 3, 256, 9, 1, 0),
+            ("wgrad down s2 B8 32->64 256", 8, 32, 64, 256, 3, 2, 0),
+            ("wgrad down s2 B8 64->128 128", 8, 64, 128, 128, 3, 2, 0)):
         if args.only not in name:
             continue
         x = torch.randn(n, cin, h, h, generator=g).to(dev)
-        ho = (h + 2 * (ks // 2) - ks) // s + 1
+        hv = 2 * h if mode == up else h
+        ho = (hv + 2 * (ks // 2) - ks) // s + 1
         dy = torch.randn(n, cout, ho, ho, generator=g).to(dev)
-        ms = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s, split=False), reps=10)
+        ms = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s, in_mode=mode,
+                                         split=False), reps=10)
         gf = 2.0 * n * cin * cout * ks * ks * ho * ho / 1e9
         line = f"{name:32s} fp32 {ms * 1e3:9.1f} us {gf / ms:7.2f} TF"
-        if s in (1, 2):
-            ms16 = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s), reps=10)
-            line += f" | f16x3 {ms16 * 1e3:9.1f} us {gf / ms16:7.2f} TF (incl. 2 amax passes)"
+        ms16 = ev(lambda: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=s, in_mode=mode), reps=10)
+        line += f" | f16x3 {ms16 * 1e3:9.1f} us {gf / ms16:7.2f} TF (incl. 2 amax passes)"
         print(line, flush=True)
-
 
 if __name__ == "__main__":
     main()
