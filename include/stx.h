@@ -106,6 +106,14 @@ typedef struct stx_conv_params {
    * dz = s*A[n].z, stx_gram_bwd) given in_amax and wt16 = (void*)1 runs as that
    * phase alone on the split kernel (no ReLU mask allowed there). */
   const float* p2_amax;
+  /* optional fused Gram partials of the output (StyleLoss.gram_matrix of a 64-channel
+   * VGG tap, stransfer/network.py:92-108, computed where the tile is produced instead
+   * of re-reading y): split path, stride 1, cout == 64, wo > 32, and the plain
+   * epilogue (no mask / aux / accumulate / acc_scale / up_dp / p2_z / relu_out).
+   * Block t of image n writes sum over its output pixels of y y^T (64 x 64 fp32, fp16
+   * hi/lo MFMA with a block-local power-of-two scale) to gram_part + (n * T + t) * 4096,
+   * T = stx_conv_gram_tiles(p); stx_style_loss_from_parts reduces them. */
+  float* gram_part;
 } stx_conv_params;
 
 int stx_version(void);
@@ -155,6 +163,10 @@ typedef struct stx_wprep_job {
 int stx_conv_weight_prep_batch(const stx_wprep_job* jobs, int njobs, void* stream);
 /* *out = max |x[i]| over n floats (device scalar; NaN propagates). */
 int stx_amax(const float* x, long long n, float* out, void* stream);
+
+/* Gram partials per image a stx_conv2d call with these params writes through
+ * gram_part (its 256-pixel output tiles), or 0 when the fused Gram does not apply. */
+int stx_conv_gram_tiles(const stx_conv_params* p);
 
 /* Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32), fused input
  * transform (in_mode) and epilogue (bias, mask, aux, accumulate, relu). */
@@ -257,6 +269,13 @@ int stx_mse(const float* a, const float* b, long long n, int relu_inputs, int mo
 int stx_diff_scale(const float* a, const float* b, float* grad, long long n, float s0,
                    const float* s1_dev, const float* s2_dev, int relu, int accumulate,
                    void* stream);
+/* stx_style_loss from precomputed Gram partials (stx_conv_params.gram_part; c <= 64):
+ * parts [b][nparts][64][64] summed in a fixed order, then the same G, coef, loss and
+ * deferred loss partials (ws >= stx_gram_ws(b, c, hw); stx_style_loss_parts). */
+int stx_style_loss_from_parts(const float* parts, int nparts, const float* target,
+                              float* g_out, float* coef, float* loss, int b, int c, int hw,
+                              int target_batched, float weight, float diag_alpha, void* ws,
+                              size_t ws_bytes, void* stream);
 /* *out = sum_i w_host[i] * s[i]   (k <= 16 device scalars, fixed order) */
 int stx_loss_combine(const float* s, int k, const float* w_host, float* out, void* stream);
 

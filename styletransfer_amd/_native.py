@@ -36,7 +36,7 @@ class ConvParams(C.Structure):
         ("p2_z", vp), ("p2_wt", vp), ("p2_scale", vp), ("p2_c", i32), ("p2_wt_batch_stride", i64),
         ("up_dp", vp), ("up_z", vp),
         ("wt16", vp), ("w_amax", vp), ("in_amax", vp), ("out_amax", vp),
-        ("pool_out", vp), ("p2_amax", vp),
+        ("pool_out", vp), ("p2_amax", vp), ("gram_part", vp),
     ]
 
 
@@ -68,6 +68,7 @@ SIGNATURES = {
     "stx_conv_weight_dims": (i32, [i32, i32, i32, C.POINTER(i32), C.POINTER(i32)]),
     "stx_conv_weight_prep": (i32, [vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv2d": (i32, [C.POINTER(ConvParams), vp]),
+    "stx_conv_gram_tiles": (i32, [C.POINTER(ConvParams)]),
     "stx_conv_weight16_bytes": (sz, [i32, i32, i32, i32]),
     "stx_conv_weight_prep16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv_weight_prep16_pair": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
@@ -96,6 +97,8 @@ SIGNATURES = {
     "stx_gram_coef_pitch": (i32, [i32]),
     "stx_style_loss": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, vp, sz,
                              vp]),
+    "stx_style_loss_from_parts": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32,
+                                        vp, sz, vp]),
     "stx_gram_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, f32, i32, vp]),
     "stx_mse_ws": (sz, [i64]),
     "stx_mse": (i32, [vp, vp, i64, i32, i32, vp, vp, f32, vp, sz, vp]),

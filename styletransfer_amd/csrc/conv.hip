@@ -541,6 +541,7 @@ static int dispatch_tw(const stx_conv_params& p, hipStream_t st) {
 
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st);  // conv16.hip
 int conv2d_fewin(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
+int fewin_gram_tiles(const stx_conv_params& p);              // convfew.hip
 int conv2d_fewout(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
 
 }  // namespace stx
@@ -574,6 +575,18 @@ extern "C" int stx_conv_weight_prep(const float* w, float* wt, int cout, int cin
   hipLaunchKernelGGL(weight_prep_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, wt,
                      cout, cin, ks, transpose, rp * ks * ks, cp);
   return check_launch("stx_conv_weight_prep");
+}
+
+extern "C" int stx_conv_gram_tiles(const stx_conv_params* pp) {
+  if (!pp) return 0;
+  const stx_conv_params& p = *pp;
+  // conv16's 256-pixel (64 x 4) tiles through the plain epilogue
+  const bool ok = p.wt16 && p.wt16 != (const void*)1 && p.ks == 3 && p.pad == 1 &&
+                  p.stride == 1 && p.cin >= 16 && p.cout == 64 && p.wo > 32 &&
+                  p.wt_batch_stride == 0 && !p.mask && !p.aux && !p.accumulate &&
+                  !p.acc_scale && !p.up_dp && !p.p2_z && !p.relu_out;
+  if (ok) return cdiv(p.wo, 64) * cdiv(p.ho, 4);
+  return fewin_gram_tiles(p);  // 3 input channels (VGG conv1_1): 64 x 8 tiles
 }
 
 extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
@@ -626,6 +639,11 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   }
   if (p.up_dp && (!p.up_z || p.ho < 2 || p.wo < 2)) {
     set_error("stx_conv2d: unpool epilogue needs up_z");
+    return STX_E_INVALID;
+  }
+  if (p.gram_part && !stx_conv_gram_tiles(&p)) {
+    set_error("stx_conv2d: fused Gram partials need the split path, stride 1, cout 64, "
+              "wo > 32 and the plain epilogue");
     return STX_E_INVALID;
   }
   // fp16 hi/lo split MFMA path (conv16.hip) for the 3x3 stride-1 layers it covers;

@@ -249,6 +249,8 @@ struct C16 {
   static constexpr int LDS_BYTES = (2 * NITP + WT_U) * 16;
   static_assert(WT_U % 256 == 0, "weight units per thread");
   static_assert(16 * NPIX * 4 + 16 * BM * 4 <= LDS_BYTES, "phase-2 staging fits");
+  static_assert(TW != 64 || NI != 2 || S != 1 || 64 * 260 * 4 + 16 <= LDS_BYTES,
+                "fused Gram tile fits");
 };
 
 // DBG (profiling experiments only, tools/bench_conv.py --dbg): bit 0 skips the
@@ -524,7 +526,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
                                            reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
     return;
   }
-  if (conv_epilogue_plain<TW, NI, RP>(acc, p, et, descale)) return;
+  if (conv_epilogue_plain<TW, NI, RP, (DBG >> 3) & 3>(acc, p, et, descale, smem)) return;
   conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, false>(acc, p, et, descale, reinterpret_cast<float*>(smem),
                                          reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
 }
@@ -556,6 +558,8 @@ static int launch16(const stx_conv_params& p, hipStream_t st) {
       case 1: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 1>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
       case 2: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 2>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
       case 3: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 3>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
+      case 8: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 8>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
+      case 16: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 16>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
       default: break;
     }
   }
@@ -596,7 +600,7 @@ template <int TW, int LM>
 static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
   const long long blocks2 = (long long)cdiv(p.wo, TW) * cdiv(p.ho, 256 / TW) *
                             cdiv(p.cout, 64) * p.n;
-  if (blocks2 < 512 && !p.pool_out && !p.p2_z) return launch16<TW, LM, 1>(p, st);
+  if (blocks2 < 512 && !p.pool_out && !p.p2_z && !p.gram_part) return launch16<TW, LM, 1>(p, st);
   return launch16<TW, LM, 2>(p, st);
 }
 

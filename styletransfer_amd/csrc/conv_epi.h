@@ -77,10 +77,99 @@ __device__ __forceinline__ void block_max_to(float* group, float m) {
 // All stores go through buffer descriptors: a per-lane pixel offset plus a per-
 // register row constant, rows past cout / pixels past the image dropped by the
 // hardware range check.
-template <int TW, int NI, bool ROWPAIR, bool RELU>
+// Fused Gram partial of a 64-channel, 256-pixel output tile (stx_conv_params.gram_part):
+// the tile (invalid pixels zeroed) goes to LDS as fp32 [channel][pixel slot] (pitch
+// 260 floats: the 16-B operand reads of 16 lanes hit distinct banks), then waves
+// 0..2 each take one 32 x 32 block of the upper triangle of G = Z Z^T over the 256
+// pixels: 16 K steps x 3 fp16 hi/lo MFMAs (s = 2^(15 - e), max|y| of the block
+// < 2^e), de-scaled by 2^(2e - 30) (exact).  The lower 32 x 32 block is the mirror
+// of the upper one.  acc holds y; lane_ok[j] marks pixels inside the image.
+template <int NI, int GDBG = 0>  // GDBG (profiling): 1 skips the MFMAs, 2 the stores
+__device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
+                                               const stx_conv_params& p, const EpiTile& t,
+                                               const bool (&lane_ok)[NI], uint32_t vmax_u,
+                                               char* smem) {
+  static_assert(NI == 2, "256-pixel tiles");
+  constexpr int PITCH = 260;
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  float* T = reinterpret_cast<float*>(smem);
+  float* red = T + 64 * PITCH;
+  const int tid = threadIdx.x, wave = tid >> 6, h = t.h, l32 = t.l32;
+  uint32_t m = vmax_u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+  if ((tid & 63) == 0) red[wave] = __uint_as_float(m);
+#pragma unroll
+  for (int j = 0; j < NI; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ch = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        T[ch * PITCH + wave * 64 + j * 32 + l32] = lane_ok[j] ? acc[i][j][r] : 0.f;
+      }
+  __syncthreads();
+  uint32_t bm = 0u;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) bm = max(bm, __float_as_uint(red[w]));
+  int e = 0;
+  frexpf(__uint_as_float(bm), &e);
+  e = min(max(e, -60), 60);
+  const float sx = __builtin_ldexpf(1.f, 15 - e), inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
+  if (wave < 3 && !(GDBG & 1)) {
+    const int I = wave == 2 ? 1 : 0, J = wave == 0 ? 0 : 1;
+    const float* ra = T + (I * 32 + l32) * PITCH + 8 * h;
+    const float* rb = T + (J * 32 + l32) * PITCH + 8 * h;
+    f32x16 g;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) g[q] = 0.f;
+    auto split = [&](const float* src, h8& hi, h8& lo) {
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float v = (k < 4 ? x0[k] : x1[k - 4]) * sx;
+        hi[k] = (_Float16)v;
+        lo[k] = (_Float16)(v - (float)hi[k]);
+      }
+    };
+#pragma unroll 4
+    for (int ks = 0; ks < 16; ++ks) {
+      h8 ah, al, bh, bl;
+      split(ra + ks * 16, ah, al);
+      if (I == J) {
+        bh = ah;
+        bl = al;
+      } else {
+        split(rb + ks * 16, bh, bl);
+      }
+      g = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, g, 0, 0, 0);
+      g = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, g, 0, 0, 0);
+      g = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, g, 0, 0, 0);
+    }
+    float* out = p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096;
+    if (GDBG & 2) {
+      float tt = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tt += g[r];
+      if (tt == 12345.f) out[0] = tt;
+      return;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float v = g[r] * inv2;
+      out[(I * 32 + row) * 64 + J * 32 + l32] = v;
+      if (I != J) out[(J * 32 + l32) * 64 + I * 32 + row] = v;
+    }
+  }
+}
+
+template <int TW, int NI, bool ROWPAIR, bool RELU, int GDBG = 0>
 __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
                                                          const stx_conv_params& p,
-                                                         const EpiTile& t, float scale) {
+                                                         const EpiTile& t, float scale,
+                                                         char* smem) {
   const size_t plane = (size_t)p.ho * p.wo;
   const int h = t.h, l32 = t.l32;
   const int co_w = t.co0 + t.wm * 64;
@@ -164,17 +253,21 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
         buf_st(rp, po + (uint32_t)row * ppb, __uint_as_float(m));
       }
   }
+  if constexpr (NI == 2 && TW == 64 && !RELU) if (p.gram_part) {
+    // the max over valid pixels of all 64 rows (cout == 64: rows_full)
+    conv_gram_tile<NI, GDBG>(acc, p, t, lane_ok, vmax_u, smem);
+  }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
-template <int TW, int NI, bool ROWPAIR>
+template <int TW, int NI, bool ROWPAIR, int GDBG = 0>
 __device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const stx_conv_params& p,
-                                                    const EpiTile& t, float scale) {
+                                                    const EpiTile& t, float scale, char* smem) {
   if (p.mask || p.aux || p.accumulate || p.acc_scale || p.up_dp || p.p2_z) return false;
   if (p.relu_out)
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, true>(acc, p, t, scale);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, true, GDBG>(acc, p, t, scale, smem);
   else
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, false>(acc, p, t, scale);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, GDBG>(acc, p, t, scale, smem);
   return true;
 }
 
@@ -304,7 +397,8 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][NI], const stx_co
       !p.pool_out) {
     // data gradient + Gram-backward phase (the Gatys dZ1 / dZ3 launches): bias and
     // out_amax only
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, false>(acc, p, t, 1.f);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false>(acc, p, t, 1.f,
+                                                     reinterpret_cast<char*>(lds_in));
     return;
   }
 

@@ -254,6 +254,19 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
       bias_r[mt][r] = (p.bias && co < p.cout) ? p.bias[co] : 0.f;
     }
   uint32_t vmax_u = 0u;
+  // fused Gram partial (stx_conv_params.gram_part; KS == 3, cout == 64): each N-block's
+  // 4 x 32 pixels go to gT as fp32 [channel][pixel], waves 0..2 add their 32 x 32 block
+  // of the upper triangle (fp16 hi/lo MFMA at the N-block's own power-of-two scale,
+  // de-scaled into g)
+  constexpr bool GRAM = KS == 3 && MT == 2;
+  constexpr int GP = 132;  // pitch: 16 lanes' 16-B operand reads hit distinct banks
+  __shared__ __attribute__((aligned(16))) float gT[GRAM ? 64 * GP : 1];
+  __shared__ float gred[4];
+  const bool gram = GRAM && p.gram_part;
+  const int gI = wave == 2 ? 1 : 0, gJ = wave == 0 ? 0 : 1;
+  f32x16 g;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) g[q] = 0.f;
 #pragma unroll 1
   for (int b = 0; b < 4; ++b) {
     const int row = 2 * wave + (b >> 1), col = 32 * (b & 1) + l32;
@@ -298,7 +311,72 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
         if (p.relu_out) v = fmaxf(v, 0.f);
         buf_st(ry, vo + (uint32_t)row_c * pb, v);
         if (in && row_c + 4 * h < p.cout) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
+        if constexpr (GRAM) acc[mt][r] = in ? v : 0.f;
       }
+    if constexpr (GRAM) if (gram) {
+      uint32_t m = 0u;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          gT[(32 * mt + 8 * (r >> 2) + 4 * h + (r & 3)) * GP + wave * 32 + l32] = acc[mt][r];
+          m = max(m, __float_as_uint(acc[mt][r]) & 0x7fffffffu);
+        }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+      if (lane == 0) gred[wave] = __uint_as_float(m);
+      __syncthreads();
+      uint32_t bm = 0u;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) bm = max(bm, __float_as_uint(gred[w]));
+      int e = 0;
+      frexpf(__uint_as_float(bm), &e);
+      e = min(max(e, -60), 60);
+      const float gs = __builtin_ldexpf(1.f, 15 - e), ginv = __builtin_ldexpf(1.f, 2 * e - 30);
+      if (wave < 3) {
+        const float* ra = gT + (gI * 32 + l32) * GP + 8 * h;
+        const float* rb = gT + (gJ * 32 + l32) * GP + 8 * h;
+        auto split = [&](const float* src, f16x8& hi, f16x8& lo) {
+          const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
+          const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float v = (k < 4 ? x0[k] : x1[k - 4]) * gs;
+            hi[k] = (_Float16)v;
+            lo[k] = (_Float16)(v - (float)hi[k]);
+          }
+        };
+        f32x16 gc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) gc[q] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          f16x8 ah, al, bh, bl;
+          split(ra + ks * 16, ah, al);
+          if (gI == gJ) {
+            bh = ah;
+            bl = al;
+          } else {
+            split(rb + ks * 16, bh, bl);
+          }
+          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, gc, 0, 0, 0);
+          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, gc, 0, 0, 0);
+          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, gc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) g[q] = fmaf(gc[q], ginv, g[q]);
+      }
+      __syncthreads();  // gT / gred reused by the next N-block
+    }
+  }
+  if constexpr (GRAM) if (gram && wave < 3) {
+    float* out = p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+      out[(gI * 32 + rr) * 64 + gJ * 32 + l32] = g[r];
+      if (gI != gJ) out[(gJ * 32 + l32) * 64 + gI * 32 + rr] = g[r];
+    }
   }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
@@ -326,6 +404,16 @@ int launch_fewin(const stx_conv_params& p, hipStream_t st) {
 }
 
 }  // namespace
+
+// Gram partials per image of conv_fewin16_kernel<3, 2> (gram_part), 0 if another kernel
+// would run this conv
+int fewin_gram_tiles(const stx_conv_params& p) {
+  const bool ok = p.cin == CF_CIN && p.ks == 3 && p.stride == 1 && p.pad == 1 &&
+                  p.in_mode == STX_IN_RAW && p.cout == 64 && !p.relu_out && !p.mask && !p.aux &&
+                  !p.accumulate && !p.p2_z && !p.up_dp && !p.pool_out && !p.acc_scale &&
+                  p.wt_batch_stride == 0 && few16_on();
+  return ok ? ((p.wo + CF_TW - 1) / CF_TW) * ((p.ho + CF_TH - 1) / CF_TH) : 0;
+}
 
 // cin == 3, stride 1, pad ks/2, raw input, cout in {32, 64} (9x9: 32); bias / relu_out / out_amax
 // epilogue only.  Returns -1 when the shape is not covered.

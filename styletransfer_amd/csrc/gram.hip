@@ -688,6 +688,39 @@ extern "C" int stx_style_loss(const float* z, const float* target, float* g_out,
                   (float)(1.0 / ((double)b * c * c)), z_amax, ws, ws_bytes, st);
 }
 
+extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const float* target,
+                                         float* g_out, float* coef, float* loss, int b, int c,
+                                         int hw, int target_batched, float weight,
+                                         float diag_alpha, void* ws, size_t ws_bytes,
+                                         void* stream) {
+  if (!gparts || !target || nparts <= 0 || b <= 0 || c <= 0 || c > GT || hw <= 0) {
+    set_error("stx_style_loss_from_parts: invalid arguments (c <= 64)");
+    return STX_E_INVALID;
+  }
+  const size_t need = gram_ws_bytes(b, c, hw);
+  if (!ws || ws_bytes < need) {
+    set_error("stx_style_loss_from_parts: workspace %zu < %zu", ws_bytes, need);
+    return STX_E_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const double n = (double)c * hw;
+  const float cA = (float)(weight * 4.0 / ((double)b * c * c * n));
+  const int cpad = stx_gram_coef_pitch(c);
+  if (coef && cpad != c) {
+    const long long cnt = (long long)b * cpad * cpad;
+    hipLaunchKernelGGL(zero_kernel, dim3((int)std::min<long long>((cnt + 255) / 256, 2048)),
+                       dim3(256), 0, st, coef, cnt);
+  }
+  float* lparts = (float*)((char*)ws + gram_parts_offset(b, c, hw, nullptr));
+  hipLaunchKernelGGL(gram_finalize_kernel, dim3(FSUB, b), dim3(256), 0, st, gparts, c, nparts,
+                     (float)(1.0 / n), g_out, target,
+                     target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts);
+  if (loss)
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, st, lparts, b * FSUB,
+                       (float)(1.0 / ((double)b * c * c)), loss);
+  return check_launch("stx_style_loss_from_parts");
+}
+
 extern "C" int stx_gram_bwd(const float* coef, const float* z, float* dz, int b, int c, int h,
                             int w, const float* acc_scale_dev, const float* mask,
                             const float* aux, float aux_scale, int accumulate, void* stream) {

@@ -295,14 +295,16 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
            out=None, mask=None, aux=None, aux_scale=0.0, acc_scale=None, accumulate=False,
            relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
            p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
-           pool_out=None, p2_amax=None, split_1x1=False):
+           pool_out=None, p2_amax=None, split_1x1=False, gram_part=None):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
     up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
     wt16=(slab, w_amax) from conv_weight_prep16 selects the fp16 hi/lo split MFMA
     kernel for eligible shapes; in_amax (device >= max|x|) is computed when absent;
     out_amax (device scalar, zeroed by the caller) receives max|out|; pool_out
-    [n][cout][ho/2][wo/2] receives maxpool2x2(relu(out)) (split path, wo > 32)."""
+    [n][cout][ho/2][wo/2] receives maxpool2x2(relu(out)) (split path, wo > 32);
+    gram_part [n * conv_gram_tiles(...) * 4096] receives the fused per-tile Gram
+    partials of out (stx_conv_params.gram_part)."""
     _req(x, "x")
     n, c, h, w = x.shape
     assert c == cin, (c, cin)
@@ -350,8 +352,20 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         _req(pool_out, "pool_out")
         assert pool_out.shape == (n, cout, ho // 2, wo // 2), pool_out.shape
         p.pool_out = pool_out.data_ptr()
+    if gram_part is not None:
+        _req(gram_part, "gram_part")
+        nt = lib().stx_conv_gram_tiles(C.byref(p))
+        assert nt > 0 and gram_part.numel() >= n * nt * 4096, (nt, gram_part.numel())
+        p.gram_part = gram_part.data_ptr()
     check(lib().stx_conv2d(C.byref(p), _stream()), "stx_conv2d")
     return out
+
+
+def conv_gram_tiles(cin, cout, ho, wo):
+    """Gram partials per image of a split 3x3 stride-1 conv with a fused Gram
+    (stx_conv_gram_tiles; 0: not fusable)."""
+    p = ConvParams(cin=cin, cout=cout, ks=3, stride=1, pad=1, ho=ho, wo=wo, wt16=2)
+    return lib().stx_conv_gram_tiles(C.byref(p))
 
 
 def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, dw=None,
@@ -483,6 +497,32 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
         off = L.stx_style_loss_parts(b, c, hw, C.byref(npart))
         return (wp + off, npart.value, 1.0 / (b * c * c)), (coef if want_coef else None)
     return loss, (coef if want_coef else None)
+
+
+def style_loss_from_parts(gparts, nparts, b, c, hw, target, weight=1.0, diag_alpha=0.0,
+                          coef=None, defer_ws=None):
+    """style_loss from the fused Gram partials a conv wrote (conv2d(gram_part=...)):
+    gparts [b][nparts][64][64].  Returns (deferred LossPart, coef) as style_loss with
+    defer_ws."""
+    _req(gparts, "gram partials")
+    _req(target, "target")
+    tb = target.numel() == b * c * c and b > 1
+    if not tb and target.numel() != c * c:
+        raise ValueError(f"style target {tuple(target.shape)} cannot expand to ({b},{c},{c})")
+    if coef is None:
+        cp = coef_pitch(c)
+        coef = torch.empty((b, cp, cp), device=gparts.device, dtype=torch.float32)
+    L = lib()
+    need = L.stx_gram_ws(b, c, hw)
+    assert defer_ws is not None and defer_ws.numel() >= need, need
+    wp, wn = defer_ws.data_ptr(), defer_ws.numel()
+    check(L.stx_style_loss_from_parts(gparts.data_ptr(), int(nparts), target.data_ptr(), None,
+                                      coef.data_ptr(), None, b, c, hw, int(tb), float(weight),
+                                      float(diag_alpha), wp, wn, _stream()),
+          "stx_style_loss_from_parts")
+    npart = C.c_int()
+    off = L.stx_style_loss_parts(b, c, hw, C.byref(npart))
+    return (wp + off, npart.value, 1.0 / (b * c * c)), coef
 
 
 def loss_finalize(parts, losses, extra=None, weights=None, total=None):

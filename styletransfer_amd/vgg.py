@@ -111,12 +111,21 @@ class VGGFeatures:
         return (l + 1 < len(IN_MODES) and IN_MODES[l + 1] == N.STX_IN_RELU_POOL2
                 and self.wt16[l] is not None and self.wt16[l + 1] is not None and wo > 32)
 
-    def forward(self, x, upto=5, outs=None, amax=None, pools=None, on_layer=None):
+    def gram_tiles(self, l, ho, wo):
+        """Fused Gram partials per image conv l can emit (0: not fusable)."""
+        cout, cin = VGG_CONV_SHAPES[l]
+        # conv1_1 (3 input channels) runs on convfew.hip's split kernel without a slab
+        if (cin >= 16 and self.wt16[l] is None) or os.environ.get("STX_GRAM_FUSE", "1") == "0":
+            return 0
+        return ops.conv_gram_tiles(cin, cout, ho, wo)
+
+    def forward(self, x, upto=5, outs=None, amax=None, pools=None, on_layer=None, grams=None):
         """[Z1..Z_upto] (pre-ReLU conv outputs).  amax: device [>=5] slots, zeroed by
         the caller; slot l+1 receives max|Z_l| (the next split conv's input scale);
         each slot is an amax group of N.STX_AMAX_SLOTS floats (slot(amax, k)).
         Where fuses_pool holds, conv l also writes P = maxpool(relu(Z_l)) (into
-        pools[l] if given) and conv l+1 reads P directly."""
+        pools[l] if given) and conv l+1 reads P directly.  grams[l] (if given and not
+        None): conv l writes its fused Gram partials there (gram_tiles)."""
         zs, cur, pin = [], x, None
         for l in range(upto):
             cout, cin = VGG_CONV_SHAPES[l]
@@ -135,6 +144,8 @@ class VGGFeatures:
                 if pools is not None:
                     pools[l] = pin
                 kw["pool_out"] = pin
+            if grams is not None and grams[l] is not None:
+                kw["gram_part"] = grams[l]
             cur = ops.conv2d(src, self.wt[l], cin, cout, 3, in_mode=mode, bias=self.b[l],
                              out=None if outs is None else outs[l], wt16=self.wt16[l], **kw)
             zs.append(cur)
@@ -162,6 +173,7 @@ class LossState:
     pools: list = field(default_factory=lambda: [None] * 5)  # fused relu+pool outputs
     lws: list = field(default_factory=lambda: [None] * 5)    # per-layer style-loss scratch
     parts: list = field(default_factory=lambda: [None] * 5)  # deferred loss partials
+    grams: list = field(default_factory=lambda: [None] * 5)  # fused Gram partial slabs
 
 
 def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
@@ -220,6 +232,15 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
             for t in [st.losses, st.amax, c4] + [c for c in st.coef if c is not None]:
                 t.record_stream(side)
 
+    # conv layers whose Gram partials come out of the conv epilogue (no re-read of Z)
+    hs = [H, H, H // 2, H // 2, H // 4]
+    for l in range(5):
+        nt = feat.gram_tiles(l, hs[l], hs[l] * W // H) if split and not overlap else 0
+        if nt == 0:
+            st.grams[l] = None
+        elif st.grams[l] is None or st.grams[l].numel() != B * nt * 4096:
+            st.grams[l] = torch.empty(B * nt * 4096, device=dev, dtype=torch.float32)
+
     def on_layer(l, z):
         # the style loss of layer l (and the content/feature losses at conv2_2) run on
         # the side stream while the next conv runs: memory-bound reductions under
@@ -236,15 +257,21 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
             need = N.lib().stx_gram_ws(b_, c_, z[0, 0].numel())
             if st.lws[i] is None or st.lws[i].numel() < need:
                 st.lws[i] = torch.empty(need, device=dev, dtype=torch.uint8)
-            st.parts[i], st.coef[i] = ops.style_loss(
-                z, targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
-                coef=st.coef[i], z_amax=slot(st.amax, l + 1) if split else None,
-                defer_ws=st.lws[i])
+            if st.grams[l] is not None:
+                st.parts[i], st.coef[i] = ops.style_loss_from_parts(
+                    st.grams[l], st.grams[l].numel() // (b_ * 4096), b_, c_, z[0, 0].numel(),
+                    targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
+                    coef=st.coef[i], defer_ws=st.lws[i])
+            else:
+                st.parts[i], st.coef[i] = ops.style_loss(
+                    z, targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
+                    coef=st.coef[i], z_amax=slot(st.amax, l + 1) if split else None,
+                    defer_ws=st.lws[i])
             if l == CONTENT_CONV:  # content, feature, feature-mse: one pass
                 ops.mse(z, c4, mode=2, out=st.losses[5:8])
 
     st.z = feat.forward(x, 5, st.z if st.z else None, amax=st.amax, pools=st.pools,
-                        on_layer=on_layer)
+                        on_layer=on_layer, grams=st.grams)
     if overlap:
         main.wait_stream(side)
         if not capturing:

@@ -226,6 +226,54 @@ def test_split_gram(dev, shape):
     assert rel(a16, a32) < 1e-5
 
 
+@pytest.mark.parametrize("case", [(1, 64, 64, 64, N.STX_IN_RELU, True),
+                                  (2, 64, 38, 72, N.STX_IN_RELU, False),
+                                  (1, 32, 30, 100, N.STX_IN_RAW, False),
+                                  (1, 64, 256, 256, N.STX_IN_RELU, True),
+                                  # 3 input channels (conv1_1, convfew.hip): 64 x 8 tiles
+                                  (1, 3, 64, 128, N.STX_IN_RAW, False),
+                                  (2, 3, 30, 70, N.STX_IN_RAW, False)])
+def test_fused_gram_partials(dev, case):
+    """Gram partials emitted by the conv epilogue (stx_conv_params.gram_part): their
+    sum is the Gram of the conv output (vs fp64), the conv output and pooled output are
+    unchanged, and style_loss_from_parts equals style_loss on the stored output."""
+    n, cin, h, w, mode, pool = case
+    cout = 64
+    x = rnd(n, cin, h, w, dev=dev, seed=91, scale=2, shift=-1)
+    wgt = rnd(cout, cin, 3, 3, dev=dev, seed=92, scale=0.1, shift=-0.05)
+    bias = rnd(cout, dev=dev, seed=93, scale=0.2, shift=-0.1)
+    wt = ops.conv_weight_prep(wgt)
+    w16 = ops.conv_weight_prep16(wgt)
+    nt = ops.conv_gram_tiles(cin, cout, h, w)
+    assert nt == -(-w // 64) * -(-h // (8 if cin == 3 else 4))
+    parts = torch.full((n * nt * 4096,), float("nan"), device=dev)
+    kw = {}
+    if pool:
+        kw["pool_out"] = torch.empty(n, cout, h // 2, w // 2, device=dev)
+    y = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=bias, wt16=w16, gram_part=parts,
+                   **kw)
+    kw2 = {}
+    if pool:
+        kw2["pool_out"] = torch.empty(n, cout, h // 2, w // 2, device=dev)
+    y2 = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=bias, wt16=w16, **kw2)
+    assert torch.equal(y, y2)
+    if pool:
+        assert torch.equal(kw["pool_out"], kw2["pool_out"])
+    assert torch.isfinite(parts).all()
+    g = parts.view(n, nt, 64, 64).double().sum(1).cpu() / (cout * h * w)
+    f = y.double().cpu().reshape(n, cout, h * w)
+    ref = torch.bmm(f, f.transpose(1, 2)) / (cout * h * w)
+    assert rel(g, ref) < TOL64, rel(g, ref)
+    t = rnd(cout, cout, dev=dev, seed=94, scale=0.02)
+    ws = torch.empty(N.lib().stx_gram_ws(n, cout, h * w), device=dev, dtype=torch.uint8)
+    lp, a_f = ops.style_loss_from_parts(parts, nt, n, cout, h * w, t, weight=3.0, defer_ws=ws)
+    lf = torch.zeros(1, device=dev)
+    ops.loss_finalize([lp], lf)
+    l32, a32 = ops.style_loss(y, t, weight=3.0)
+    assert rel(lf[0], l32) < 1e-5
+    assert rel(a_f, a32) < 1e-5
+
+
 @pytest.mark.parametrize("shape", [(2, 64, 20, 70), (1, 128, 34, 64), (1, 256, 16, 16),
                                    (1, 64, 9, 13), (1, 64, 128, 256), (3, 128, 32, 96),
                                    (2, 64, 2, 32), (2, 256, 32, 48)])

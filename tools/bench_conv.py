@@ -75,6 +75,19 @@ def main():
             ms16 = ev(lambda: ops.conv2d(x, wt, cin, cout, ks, stride=s, in_mode=mode, out=out,
                                          wt16=w16, in_amax=am, **kw))
             line += f" | f16x3 {ms16 * 1e3:9.1f} us {gf / ms16:7.2f} TF"
+        nt = ops.conv_gram_tiles(cin, cout, ho, wo) if s == 1 and mode in (
+            N.STX_IN_RAW, N.STX_IN_RELU) else 0
+        if nt and not args.no_split and (cin == 3 or ops.split_eligible(cin, cout, ks, s)):
+            gp = torch.empty(n * nt * 4096, device=dev)
+            kw16 = {}
+            if cin != 3:
+                kw16 = dict(wt16=ops.conv_weight_prep16(wraw), in_amax=ops.amax(x))
+                if "conv1_2" in name:
+                    kw16.update(pool_out=torch.empty(n, cout, ho // 2, wo // 2, device=dev),
+                                out_amax=torch.zeros(N.STX_AMAX_SLOTS, device=dev))
+            msg = ev(lambda: ops.conv2d(x, wt, cin, cout, ks, stride=s, in_mode=mode, out=out,
+                                        gram_part=gp, **kw16))
+            line += f" | +gram {msg * 1e3:9.1f} us"
         print(line, flush=True)
     for name, n, c, h in (("gram C64 512^2", 1, 64, 512), ("gram C128 256^2", 1, 128, 256),
                           ("gram C256 128^2", 1, 256, 128), ("gram C64 B8 256^2", 8, 64, 256)):
