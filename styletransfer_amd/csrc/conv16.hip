@@ -249,8 +249,8 @@ struct C16 {
   static constexpr int LDS_BYTES = (2 * NITP + WT_U) * 16;
   static_assert(WT_U % 256 == 0, "weight units per thread");
   static_assert(16 * NPIX * 4 + 16 * BM * 4 <= LDS_BYTES, "phase-2 staging fits");
-  static_assert(TW != 64 || NI != 2 || S != 1 || 64 * 260 * 4 + 16 <= LDS_BYTES,
-                "fused Gram tile fits");
+  static_assert(TW != 64 || NI != 2 || S != 1 || GramPlanes<256>::BYTES <= LDS_BYTES,
+                "fused Gram planes fit");
 };
 
 // DBG (profiling experiments only, tools/bench_conv.py --dbg): bit 0 skips the

@@ -77,28 +77,89 @@ __device__ __forceinline__ void block_max_to(float* group, float m) {
 // All stores go through buffer descriptors: a per-lane pixel offset plus a per-
 // register row constant, rows past cout / pixels past the image dropped by the
 // hardware range check.
-// Fused Gram partial of a 64-channel, 256-pixel output tile (stx_conv_params.gram_part):
-// the tile (invalid pixels zeroed) goes to LDS as fp32 [channel][pixel slot] (pitch
-// 260 floats: the 16-B operand reads of 16 lanes hit distinct banks), then waves
-// 0..2 each take one 32 x 32 block of the upper triangle of G = Z Z^T over the 256
-// pixels: 16 K steps x 3 fp16 hi/lo MFMAs (s = 2^(15 - e), max|y| of the block
-// < 2^e), de-scaled by 2^(2e - 30) (exact).  The lower 32 x 32 block is the mirror
-// of the upper one.  acc holds y; lane_ok[j] marks pixels inside the image.
+// ---- fused Gram partials (stx_conv_params.gram_part) --------------------------------
+// A producing conv's 64-channel output tile is split ONCE into fp16 hi/lo planes in LDS,
+// [plane][channel][pixel] with a pitch of NPX + 8 halves (the 16-B operand reads of 16
+// lanes land on distinct banks; a store's two lane halves on disjoint banks), at the
+// tile's own power-of-two scale s = 2^(15 - e), max|y| < 2^e.  Waves 0..2 then each
+// take one 32 x 32 block of the upper triangle of G = Z Z^T (3 MFMAs per 16 pixels),
+// de-scaled by 2^(2e - 30) (exact); the lower block is the mirror of the upper one.
+template <int NPX>
+struct GramPlanes {
+  static constexpr int HP = NPX + 8;                 // pitch (halves)
+  static constexpr int BYTES = 2 * 64 * HP * 2 + 16;  // hi + lo planes, 4 floats of max
+};
+
+// block max over 4 waves (IEEE bits of |y|) -> the scale exponent e (barrier inside)
+__device__ __forceinline__ int gram_block_exp(uint32_t m, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = __uint_as_float(m);
+  __syncthreads();
+  uint32_t bm = 0u;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) bm = max(bm, __float_as_uint(red[w]));
+  int e = 0;
+  frexpf(__uint_as_float(bm), &e);
+  return min(max(e, -60), 60);
+}
+
+// scaled value v of (channel, pixel) -> the hi and lo planes
+__device__ __forceinline__ void gram_put(_Float16* H, int hp, int ch, int px, float v) {
+  const _Float16 hi = (_Float16)v;
+  H[ch * hp + px] = hi;
+  H[(64 + ch) * hp + px] = (_Float16)(v - (float)hi);
+}
+
+// g += this wave's upper-triangle block over KS x 16 pixels (waves 0..2)
+template <int KS>
+__device__ __forceinline__ void gram_mma(const _Float16* H, int hp, int wave, int h, int l32,
+                                         f32x16& g) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  const int I = wave == 2 ? 1 : 0, J = wave == 0 ? 0 : 1;
+  const _Float16* ra = H + (I * 32 + l32) * hp + 8 * h;
+  const _Float16* rb = H + (J * 32 + l32) * hp + 8 * h;
+  const int lo = 64 * hp;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const h8 ah = *reinterpret_cast<const h8*>(ra + ks * 16);
+    const h8 al = *reinterpret_cast<const h8*>(ra + lo + ks * 16);
+    h8 bh = ah, bl = al;
+    if (I != J) {
+      bh = *reinterpret_cast<const h8*>(rb + ks * 16);
+      bl = *reinterpret_cast<const h8*>(rb + lo + ks * 16);
+    }
+    g = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, g, 0, 0, 0);
+    g = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, g, 0, 0, 0);
+  }
+}
+
+// the 64 x 64 partial of this block (waves 0..2 hold the three upper blocks)
+__device__ __forceinline__ void gram_store(float* out, const f32x16& g, int wave, int h,
+                                           int l32) {
+  const int I = wave == 2 ? 1 : 0, J = wave == 0 ? 0 : 1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+    out[(I * 32 + row) * 64 + J * 32 + l32] = g[r];
+    if (I != J) out[(J * 32 + l32) * 64 + I * 32 + row] = g[r];
+  }
+}
+
+// conv16's 64 x 256 tile: acc holds y; lane_ok[j] marks pixels inside the image
 template <int NI, int GDBG = 0>  // GDBG (profiling): 1 skips the MFMAs, 2 the stores
 __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
                                                const stx_conv_params& p, const EpiTile& t,
                                                const bool (&lane_ok)[NI], uint32_t vmax_u,
                                                char* smem) {
   static_assert(NI == 2, "256-pixel tiles");
-  constexpr int PITCH = 260;
-  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-  float* T = reinterpret_cast<float*>(smem);
-  float* red = T + 64 * PITCH;
-  const int tid = threadIdx.x, wave = tid >> 6, h = t.h, l32 = t.l32;
-  uint32_t m = vmax_u;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
-  if ((tid & 63) == 0) red[wave] = __uint_as_float(m);
+  using GP = GramPlanes<256>;
+  _Float16* H = reinterpret_cast<_Float16*>(smem);
+  float* red = reinterpret_cast<float*>(smem + GP::BYTES - 16);
+  const int wave = threadIdx.x >> 6, h = t.h, l32 = t.l32;
+  const int e = gram_block_exp(vmax_u, red);
+  const float sx = __builtin_ldexpf(1.f, 15 - e);
 #pragma unroll
   for (int j = 0; j < NI; ++j)
 #pragma unroll
@@ -106,47 +167,17 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ch = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        T[ch * PITCH + wave * 64 + j * 32 + l32] = lane_ok[j] ? acc[i][j][r] : 0.f;
+        gram_put(H, GP::HP, ch, wave * 64 + j * 32 + l32, lane_ok[j] ? acc[i][j][r] * sx : 0.f);
       }
   __syncthreads();
-  uint32_t bm = 0u;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) bm = max(bm, __float_as_uint(red[w]));
-  int e = 0;
-  frexpf(__uint_as_float(bm), &e);
-  e = min(max(e, -60), 60);
-  const float sx = __builtin_ldexpf(1.f, 15 - e), inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
   if (wave < 3 && !(GDBG & 1)) {
-    const int I = wave == 2 ? 1 : 0, J = wave == 0 ? 0 : 1;
-    const float* ra = T + (I * 32 + l32) * PITCH + 8 * h;
-    const float* rb = T + (J * 32 + l32) * PITCH + 8 * h;
     f32x16 g;
 #pragma unroll
     for (int q = 0; q < 16; ++q) g[q] = 0.f;
-    auto split = [&](const float* src, h8& hi, h8& lo) {
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
+    gram_mma<16>(H, GP::HP, wave, h, l32, g);
+    const float inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float v = (k < 4 ? x0[k] : x1[k - 4]) * sx;
-        hi[k] = (_Float16)v;
-        lo[k] = (_Float16)(v - (float)hi[k]);
-      }
-    };
-#pragma unroll 4
-    for (int ks = 0; ks < 16; ++ks) {
-      h8 ah, al, bh, bl;
-      split(ra + ks * 16, ah, al);
-      if (I == J) {
-        bh = ah;
-        bl = al;
-      } else {
-        split(rb + ks * 16, bh, bl);
-      }
-      g = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, g, 0, 0, 0);
-      g = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, g, 0, 0, 0);
-      g = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, g, 0, 0, 0);
-    }
+    for (int q = 0; q < 16; ++q) g[q] *= inv2;
     float* out = p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096;
     if (GDBG & 2) {
       float tt = 0.f;
@@ -155,13 +186,7 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
       if (tt == 12345.f) out[0] = tt;
       return;
     }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float v = g[r] * inv2;
-      out[(I * 32 + row) * 64 + J * 32 + l32] = v;
-      if (I != J) out[(J * 32 + l32) * 64 + I * 32 + row] = v;
-    }
+    gram_store(out, g, wave, h, l32);
   }
 }
 

@@ -259,11 +259,11 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
   // of the upper triangle (fp16 hi/lo MFMA at the N-block's own power-of-two scale,
   // de-scaled into g)
   constexpr bool GRAM = KS == 3 && MT == 2;
-  constexpr int GP = 132;  // pitch: 16 lanes' 16-B operand reads hit distinct banks
-  __shared__ __attribute__((aligned(16))) float gT[GRAM ? 64 * GP : 1];
-  __shared__ float gred[4];
+  using GPL = GramPlanes<128>;
+  __shared__ __attribute__((aligned(16))) char gsm[GRAM ? GPL::BYTES : 16];
+  _Float16* gH = reinterpret_cast<_Float16*>(gsm);
+  float* gred = reinterpret_cast<float*>(gsm + (GRAM ? GPL::BYTES - 16 : 0));
   const bool gram = GRAM && p.gram_part;
-  const int gI = wave == 2 ? 1 : 0, gJ = wave == 0 ? 0 : 1;
   f32x16 g;
 #pragma unroll
   for (int q = 0; q < 16; ++q) g[q] = 0.f;
@@ -314,70 +314,36 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
         if constexpr (GRAM) acc[mt][r] = in ? v : 0.f;
       }
     if constexpr (GRAM) if (gram) {
+      // this N-block's 4 x 32 pixels at their own scale: max, split into the planes, then
+      // waves 0..2 add their upper-triangle block (de-scaled into g)
       uint32_t m = 0u;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          gT[(32 * mt + 8 * (r >> 2) + 4 * h + (r & 3)) * GP + wave * 32 + l32] = acc[mt][r];
-          m = max(m, __float_as_uint(acc[mt][r]) & 0x7fffffffu);
-        }
+        for (int r = 0; r < 16; ++r) m = max(m, __float_as_uint(acc[mt][r]) & 0x7fffffffu);
+      const int e = gram_block_exp(m, gred);  // (its barrier also retires the last block's reads)
+      const float gs = __builtin_ldexpf(1.f, 15 - e);
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
-      if (lane == 0) gred[wave] = __uint_as_float(m);
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          gram_put(gH, GPL::HP, 32 * mt + 8 * (r >> 2) + 4 * h + (r & 3), wave * 32 + l32,
+                   acc[mt][r] * gs);
       __syncthreads();
-      uint32_t bm = 0u;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) bm = max(bm, __float_as_uint(gred[w]));
-      int e = 0;
-      frexpf(__uint_as_float(bm), &e);
-      e = min(max(e, -60), 60);
-      const float gs = __builtin_ldexpf(1.f, 15 - e), ginv = __builtin_ldexpf(1.f, 2 * e - 30);
       if (wave < 3) {
-        const float* ra = gT + (gI * 32 + l32) * GP + 8 * h;
-        const float* rb = gT + (gJ * 32 + l32) * GP + 8 * h;
-        auto split = [&](const float* src, f16x8& hi, f16x8& lo) {
-          const f32x4 x0 = *reinterpret_cast<const f32x4*>(src);
-          const f32x4 x1 = *reinterpret_cast<const f32x4*>(src + 4);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const float v = (k < 4 ? x0[k] : x1[k - 4]) * gs;
-            hi[k] = (_Float16)v;
-            lo[k] = (_Float16)(v - (float)hi[k]);
-          }
-        };
         f32x16 gc;
 #pragma unroll
         for (int q = 0; q < 16; ++q) gc[q] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          f16x8 ah, al, bh, bl;
-          split(ra + ks * 16, ah, al);
-          if (gI == gJ) {
-            bh = ah;
-            bl = al;
-          } else {
-            split(rb + ks * 16, bh, bl);
-          }
-          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, gc, 0, 0, 0);
-          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, gc, 0, 0, 0);
-          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, gc, 0, 0, 0);
-        }
+        gram_mma<8>(gH, GPL::HP, wave, h, l32, gc);
+        const float ginv = __builtin_ldexpf(1.f, 2 * e - 30);
 #pragma unroll
         for (int q = 0; q < 16; ++q) g[q] = fmaf(gc[q], ginv, g[q]);
       }
-      __syncthreads();  // gT / gred reused by the next N-block
     }
   }
-  if constexpr (GRAM) if (gram && wave < 3) {
-    float* out = p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-      out[(gI * 32 + rr) * 64 + gJ * 32 + l32] = g[r];
-      if (gI != gJ) out[(gJ * 32 + l32) * 64 + gI * 32 + rr] = g[r];
-    }
-  }
+  if constexpr (GRAM) if (gram && wave < 3)
+    gram_store(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, g, wave, h,
+               l32);
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
