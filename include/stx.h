@@ -331,6 +331,21 @@ int stx_instnorm_fwd(const float* x, const float* res, const float* gamma, const
  * conv needs no separate bias-gradient pass.  out_amax (amax group or NULL) receives
  * max|du| -- the split dgrad/wgrad scale of du. */
 size_t stx_instnorm_bwd_ws(int n, int c);
+/* The parameter reductions of many stx_instnorm_bwd calls in one launch: each such
+ * call ran with dgamma = dbeta = dbias_in = NULL into its own workspace `parts`
+ * (>= stx_instnorm_bwd_ws(n, c) bytes, kept until this call); each job then writes /
+ * accumulates its dgamma, dbeta, dbias_in (any may be NULL) with the same fixed-order
+ * sums over n -- one launch per training step instead of one per InstanceNorm2d
+ * layer (stransfer/network.py:474-600, 15 layers in ImageTransformNet). */
+#define STX_PGRAD_MAX 32
+typedef struct stx_in_pgrad_job {
+  const float* parts;
+  float* dgamma;
+  float* dbeta;
+  float* dbias_in;
+  int n, c, accumulate, pad_;
+} stx_in_pgrad_job;
+int stx_instnorm_param_grads(const stx_in_pgrad_job* jobs, int njobs, void* stream);
 int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
                      const float* gamma, const float* mean, const float* rstd, float* du,
                      float* dgamma, float* dbeta, float* dbias_in, int n, int c, int hw, int relu,

@@ -56,6 +56,15 @@ class WprepJob(C.Structure):
 STX_WPREP_MAX, STX_WPREP_F32, STX_WPREP_F16 = 48, 0, 1
 
 
+class PGradJob(C.Structure):
+    """Mirror of `stx_in_pgrad_job` (include/stx.h)."""
+    _fields_ = [("parts", vp), ("dgamma", vp), ("dbeta", vp), ("dbias_in", vp), ("n", i32),
+                ("c", i32), ("accumulate", i32), ("pad_", i32)]
+
+
+STX_PGRAD_MAX = 32
+
+
 class LossParts(C.Structure):
     """Mirror of `stx_loss_parts` (include/stx.h)."""
     _fields_ = [("parts", vp * 8), ("nparts", i32 * 8), ("inv", f32 * 8), ("k", i32)]
@@ -115,6 +124,7 @@ SIGNATURES = {
     "stx_adam_step": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp, vp]),
     "stx_instnorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp, vp]),
     "stx_instnorm_bwd_ws": (sz, [i32, i32]),
+    "stx_instnorm_param_grads": (i32, [C.POINTER(PGradJob), i32, vp]),
     "stx_instnorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32,
                                i32, i32, vp, vp, sz, vp]),
     "stx_upsample2x_fwd": (i32, [vp, vp, i32, i32, i32, vp]),

@@ -340,6 +340,40 @@ class TemporalLossFn(torch.autograd.Function):
         return dy, None, None, None, None
 
 
+class FastStLossFn(torch.autograd.Function):
+    """The fast_st closure's scalar (stransfer/network.py:690-731):
+        total = sw * sum(style) + cw * content + TV(y, tv_factor)
+    in one pass: the loss weights are folded into the backward operators (vgg.py
+    folded mode: no per-loss scale vector, the content term rides on A_4), the TV loss
+    and its gradient come from one kernel in the forward, and the weighted total is
+    summed in the same launch as the five style losses.  The backward assumes a unit
+    upstream gradient, i.e. `total.backward()` or a plain sum with other terms (as the
+    trainers use it; checking the value would cost a host sync).  Other callers use
+    VGGLossFn + TVLossFn."""
+
+    @staticmethod
+    def forward(ctx, y, c4, feat, targets, sw, cw, tv_factor):
+        y = _c(y)
+        dev = y.device
+        st = V.LossState()
+        st.losses = torch.empty(V.N_LOSSES + 2, device=dev, dtype=torch.float32)
+        st.fmean = st.losses[6:8]
+        tvg = torch.empty_like(y)
+        ops.tv_loss(y, tv_factor, grad=tvg, out=st.losses[8])
+        total = torch.empty((), device=dev, dtype=torch.float32)
+        V.loss_forward(feat, targets, y, _c(c4), st=st, folded_weights=(sw, cw), total=total,
+                       extra_slot=True)
+        ctx.st, ctx.feat, ctx.tvg = st, feat, tvg
+        return total
+
+    @staticmethod
+    def backward(ctx, g):
+        dx = V.loss_backward(ctx.feat, ctx.st, feature_grad=False)
+        dx.add_(ctx.tvg)
+        ctx.st = ctx.tvg = None
+        return dx, None, None, None, None, None, None
+
+
 class VGGLossFn(torch.autograd.Function):
     """All 7 StyleNetwork losses of a batch in one fused forward/backward:
     returns [style1..5, content, feature] for input x given the style targets and

@@ -391,9 +391,60 @@ __global__ void instnorm_param_grad_kernel(const float* __restrict__ parts, int 
   if (dbias) dbias[ch] = accumulate ? dbias[ch] + d : d;
 }
 
+// many layers' parameter reductions in one launch (stx_instnorm_param_grads): thread ->
+// (job, channel) in job order; the same fixed-order sums as instnorm_param_grad_kernel
+struct PGradJobs {
+  stx_in_pgrad_job job[STX_PGRAD_MAX];
+  int ch0[STX_PGRAD_MAX + 1];  // first channel of each job (prefix sums)
+  int njobs;
+};
+
+__global__ void __launch_bounds__(256) instnorm_param_grads_kernel(PGradJobs b) {
+  const int gc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gc >= b.ch0[b.njobs]) return;
+  int j = 0;
+  while (j + 1 < b.njobs && gc >= b.ch0[j + 1]) ++j;
+  const stx_in_pgrad_job& t = b.job[j];
+  const int ch = gc - b.ch0[j];
+  float a = 0.f, bb = 0.f, d = 0.f;
+  for (int k = 0; k < t.n; ++k) {
+    const float* p = t.parts + 3 * ((size_t)k * t.c + ch);
+    a += p[0];
+    bb += p[1];
+    d += p[2];
+  }
+  const bool acc = t.accumulate != 0;
+  if (t.dgamma) t.dgamma[ch] = acc ? t.dgamma[ch] + a : a;
+  if (t.dbeta) t.dbeta[ch] = acc ? t.dbeta[ch] + bb : bb;
+  if (t.dbias_in) t.dbias_in[ch] = acc ? t.dbias_in[ch] + d : d;
+}
+
 }  // namespace stx
 
 using namespace stx;
+
+extern "C" int stx_instnorm_param_grads(const stx_in_pgrad_job* jobs, int njobs, void* stream) {
+  if (!jobs || njobs <= 0 || njobs > STX_PGRAD_MAX) {
+    set_error("stx_instnorm_param_grads: 1 <= njobs <= %d required", STX_PGRAD_MAX);
+    return STX_E_INVALID;
+  }
+  PGradJobs b{};
+  int ch = 0;
+  for (int j = 0; j < njobs; ++j) {
+    if (!jobs[j].parts || jobs[j].n <= 0 || jobs[j].c <= 0) {
+      set_error("stx_instnorm_param_grads: job %d invalid", j);
+      return STX_E_INVALID;
+    }
+    b.job[j] = jobs[j];
+    b.ch0[j] = ch;
+    ch += jobs[j].c;
+  }
+  b.ch0[njobs] = ch;
+  b.njobs = njobs;
+  hipLaunchKernelGGL(instnorm_param_grads_kernel, dim3(cdiv(ch, 256)), dim3(256), 0,
+                     (hipStream_t)stream, b);
+  return check_launch("stx_instnorm_param_grads");
+}
 
 extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* gamma,
                                 const float* beta, float* y, float* mean, float* rstd, int n,

@@ -133,6 +133,43 @@ class AmaxArena:
 ARENA = AmaxArena()
 
 
+class ParamGradBatch:
+    """Deferred InstanceNorm parameter reductions of one training step: between
+    begin() and flush() each instnorm_bwd given dgamma/dbeta/dbias_in keeps its
+    per-plane partials in a buffer of its own and records a job; flush() reduces all
+    of them in one launch (stx_instnorm_param_grads).  Outside a step the reductions
+    run per call."""
+
+    def __init__(self):
+        self.active = False
+        self.jobs, self.keep = [], []
+
+    def begin(self):
+        self.active = True
+        self.jobs, self.keep = [], []
+
+    def add(self, parts, n, c, dgamma, dbeta, dbias, accumulate):
+        self.keep.append(parts)
+        self.jobs.append(N.PGradJob(parts.data_ptr(), _p(dgamma), _p(dbeta), _p(dbias), n, c,
+                                    int(accumulate), 0))
+        if len(self.jobs) == N.STX_PGRAD_MAX:
+            self._launch()
+
+    def _launch(self):
+        if self.jobs:
+            arr = (N.PGradJob * len(self.jobs))(*self.jobs)
+            check(lib().stx_instnorm_param_grads(arr, len(self.jobs), _stream()),
+                  "stx_instnorm_param_grads")
+        self.jobs, self.keep = [], []
+
+    def flush(self):
+        self._launch()
+        self.active = False
+
+
+PGRADS = ParamGradBatch()
+
+
 # ----------------------------------------------------------------------- conv
 def conv_weight_dims(cin, cout, ks):
     a, b = C.c_int(), C.c_int()
@@ -671,12 +708,26 @@ def instnorm_bwd(dy, y, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbet
     hw = x[0, 0].numel()
     du = torch.empty_like(x)
     L = lib()
-    wp, wn = WS.get(L.stx_instnorm_bwd_ws(n, c), x.device)
+    need = L.stx_instnorm_bwd_ws(n, c)
+    # deferred only when accumulating into persistent buffers (.grad views): a fresh
+    # gradient tensor handed back to autograd must be complete on return
+    defer = PGRADS.active and accumulate and (
+        dgamma is not None or dbeta is not None or dbias_in is not None)
+    job = None
+    if defer:  # partials kept for the step's single parameter-reduction launch
+        parts = torch.empty(need, device=x.device, dtype=torch.uint8)
+        job = (parts, n, c, dgamma, dbeta, dbias_in, accumulate)
+        wp, wn = parts.data_ptr(), need
+        dgamma = dbeta = dbias_in = None
+    else:
+        wp, wn = WS.get(need, x.device)
     check(L.stx_instnorm_bwd(dy.data_ptr(), _p(y), x.data_ptr(), _p(res), _p(gamma),
                              mean.data_ptr(), rstd.data_ptr(), du.data_ptr(), _p(dgamma),
                              _p(dbeta), _p(dbias_in), n, c, hw, int(relu), int(accumulate),
                              _p(out_amax), wp,
                              wn, _stream()), "stx_instnorm_bwd")
+    if job is not None:
+        PGRADS.add(*job)  # after the kernel that writes its partials
     return du
 
 

@@ -93,9 +93,13 @@ class FastStTrainer:
     def _total(self, batch, y):
         with torch.no_grad():
             c4 = V.content_target(self.feat, batch, amax=ops.ARENA.take_span(5, batch.device))
+        w = self.world
+        if torch.is_grad_enabled() and y.requires_grad:
+            # one fused scalar: folded loss weights, TV value + gradient in one pass
+            return A.FastStLossFn.apply(y, c4, self.feat, self.targets, self.sw / w,
+                                        self.cw / w, self.tv)
         losses = A.VGGLossFn.apply(y, c4, self.feat, self.targets, False)  # feature loss unused
         tv = A.TVLossFn.apply(y, self.tv)
-        w = self.world
         return (self.sw / w) * losses[:5].sum() + (self.cw / w) * losses[5] + tv
 
     def _fwd_bwd(self, batch: torch.Tensor) -> torch.Tensor:
@@ -103,11 +107,14 @@ class FastStTrainer:
         self.flat_grad.zero_()
         self.slabs.prep()
         ops.ARENA.begin(self.device)  # InstanceNorm outputs carry their max|.| to the convs
+        ops.PGRADS.begin()            # one launch for all InstanceNorm parameter gradients
         try:
             y = self.itn(batch)
             total = self._total(batch, y)
             total.backward()
+            ops.PGRADS.flush()
         finally:
+            ops.PGRADS.active = False
             ops.ARENA.end()
         return total.detach()
 
@@ -232,11 +239,14 @@ class VideoTrainer(FastStTrainer):
         self.flat_grad.zero_()
         self.slabs.prep()
         ops.ARENA.begin(self.device)
+        ops.PGRADS.begin()
         try:
             y = self.itn(x6)
             total = self._video_total(batch, y, old_c, old_s)
             total.backward()
+            ops.PGRADS.flush()
         finally:
+            ops.PGRADS.active = False
             ops.ARENA.end()
         self.old = (batch, y.detach())
         self.opt_head.step()

@@ -177,7 +177,7 @@ class LossState:
 
 
 def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
-                 folded_weights=None, total=None):
+                 folded_weights=None, total=None, extra_slot=False):
     """Forward of all 7 losses for input batch x [B,3,H,W] given style targets and
     the content target c4 (= Z4 of the content image, pre-ReLU).
 
@@ -279,11 +279,15 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                 c.record_stream(main)
     # the 5 style losses (+ the weighted total) in one launch
     w = None
+    extra = None
     if total is not None:
         fw = folded_weights if folded_weights is not None else (1.0, 1.0)
         w = [float(fw[0])] * 5 + [float(fw[1])]
-    ops.loss_finalize(st.parts, st.losses[0:5], extra=st.losses[5:6] if w else None, weights=w,
-                      total=total)
+        extra = st.losses[5:6]
+        if extra_slot:  # st.losses[8] (written by the caller, e.g. TV) joins the total
+            w += [0.0, 0.0, 1.0]
+            extra = st.losses[5:9]
+    ops.loss_finalize(st.parts, st.losses[0:5], extra=extra, weights=w, total=total)
     return st
 
 
