@@ -61,10 +61,13 @@ PEAK_HBM_GBS = 8000.0
 # the dominant kernel instance and its per-launch HBM traffic (rocprofv3 PMC passes
 # of tools/gpu_round.sh, summarised by tools/pmc_summary.py)
 ROOFLINE_KERNEL = "conv3x3_f16x3_kernel<64, 1, 0, 0, 2>"
-PMC_FILE = os.path.join(REPO, "profiles", "r1_pmc_conv1_2_fwd.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r2_pmc_conv1_2_fwd.json")
 # algorithmic bytes of conv1_2 fwd @512^2: read Z1 + write Z2 (64 MiB each) + the fused
 # relu+pool output P2 (16 MiB) + weights (fp16 hi/lo slab) + bias
-CONV1_2_BYTES = 2 * 64 * 512 * 512 * 4 + 64 * 256 * 256 * 4 + 64 * 64 * 9 * 4 + 64 * 4
+# conv1_2 forward at 512^2 as the iteration launches it: Z1 in, Z2 + relu/pool(Z2) out,
+# weights + bias, and the fused Gram partials (1024 tiles x 64 x 64 fp32)
+CONV1_2_BYTES = (2 * 64 * 512 * 512 * 4 + 64 * 256 * 256 * 4 + 64 * 64 * 9 * 4 + 64 * 4
+                 + 1024 * 64 * 64 * 4)
 
 
 def pmc_traffic():
@@ -168,21 +171,42 @@ def gatys_leg(args, world, rank, dev):
     am = V.slot(eng.st.amax, 1).clone()
     am_out = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
     pool = torch.empty_like(eng.st.pools[1])
-    fwd_ms = event_avg_ms(lambda: ops.conv2d(z1, feat.wt[1], 64, 64, 3, in_mode=N.STX_IN_RELU,
-                                             bias=feat.b[1], out=out, wt16=feat.wt16[1],
-                                             in_amax=am, out_amax=am_out, pool_out=pool),
-                          reps=20)
-    gf = conv_gflop(64, 64, H, H)
+    gparts = eng.st.grams[1]
+    gp = torch.empty_like(gparts) if gparts is not None else None
+
+    def conv12(gram_part):
+        return ops.conv2d(z1, feat.wt[1], 64, 64, 3, in_mode=N.STX_IN_RELU, bias=feat.b[1],
+                          out=out, wt16=feat.wt16[1], in_amax=am, out_amax=am_out,
+                          pool_out=pool, gram_part=gram_part)
+
+    fwd_ms = event_avg_ms(lambda: conv12(gp), reps=20)
+    gf_conv = conv_gflop(64, 64, H, H)
+    gf_gram = 2.0 * 64 * 64 * H * H / 1e9
+    gf = gf_conv + (gf_gram if gp is not None else 0.0)
     achieved = gf / (fwd_ms * 1e-3) / 1e3  # TFLOP/s
-    # the style-loss Gram of conv1_2's output (C=64, HW=H^2): split partials + finalize
+    # the style-loss Gram of conv1_2's output (C=64, HW=H^2): fused into the conv's
+    # epilogue (cost = the launch with gram_part minus the launch without, plus the
+    # finalize from the partials), or split partials + finalize when not fusable
     z2 = eng.st.z[1]
-    zam = V.slot(eng.st.amax, 2).clone()
-    gram_ms = event_avg_ms(lambda: ops.gram(z2, z_amax=zam), reps=20)
+    if gp is not None:
+        plain_ms = event_avg_ms(lambda: conv12(None), reps=20)
+        conv12(gp)
+        nt = gp.numel() // 4096
+        wsb = torch.empty(N.lib().stx_gram_ws(1, 64, H * H), device=dev, dtype=torch.uint8)
+        tgt = eng.targets[1]
+        fin_ms = event_avg_ms(lambda: ops.style_loss_from_parts(gp, nt, 1, 64, H * H, tgt,
+                                                                defer_ws=wsb), reps=20)
+        gram = dict(ms=max(fwd_ms - plain_ms, 0.0) + fin_ms, fused=True, epi_ms=fwd_ms - plain_ms,
+                    finalize_ms=fin_ms, conv_ms=plain_ms)
+    else:
+        zam = V.slot(eng.st.amax, 2).clone()
+        gram = dict(ms=event_avg_ms(lambda: ops.gram(z2, z_amax=zam), reps=20), fused=False)
+    gram.update(gflop=gf_gram, bytes=64 * H * H * 4)
     loss = float(eng.total)
     return dict(rate=rate, dt=dt, loss=loss, run=run, kernel=dict(fwd_ms=fwd_ms, gflop=gf,
-                                                         tflops=achieved),
-                gram=dict(ms=gram_ms, gflop=2.0 * 64 * 64 * H * H / 1e9,
-                          bytes=64 * H * H * 4))
+                                                         gflop_conv=gf_conv, tflops=achieved,
+                                                         gram_fused=gp is not None),
+                gram=gram)
 
 
 def fast_st_leg(args, world, rank, dev, B=None, steps=None):
@@ -424,8 +448,10 @@ def main():
             "roofline": {
                 "bound": "mfma",
                 "kernel": f"{ROOFLINE_KERNEL} (conv1_2 forward, 64->64 3x3 @ "
-                          f"{args.size}^2, fused ReLU loader + ReLU/MaxPool output, fp16 hi/lo "
-                          "split MFMA; the same launch as in the iteration)",
+                          f"{args.size}^2, fused ReLU loader + ReLU/MaxPool output"
+                          + (" + the style-loss Gram partials of its output" if k["gram_fused"]
+                             else "") + ", fp16 hi/lo split MFMA; the same launch as in the "
+                          "iteration)",
                 "achieved": round(k["tflops"], 3),
                 "peak": round(PEAK_SPLIT_TFLOPS, 1),
                 "unit": "TFLOP/s",
@@ -435,6 +461,8 @@ def main():
                              "(fp32-input MFMA peak is 157.3 TF)",
                 "traffic": traffic_bytes,
                 "per_launch_gflop": round(k["gflop"], 3),
+                "per_launch_gflop_note": "3x3 conv 2*64*64*9*H*W"
+                                         + (" + Gram 2*64*64*H*W" if k["gram_fused"] else ""),
                 "fwd_ms": round(k["fwd_ms"], 4),
                 "traffic_source": traffic_src,
                 "algorithmic_bytes": CONV1_2_BYTES if args.size == 512 else None,
@@ -442,17 +470,24 @@ def main():
                                           / world / 1e3, 3),
             },
             "gram_roofline": {
-                "kernel": "gram_partial_f16_kernel + gram_finalize_kernel (StyleLoss.gram_matrix "
-                          f"of conv1_2's output, C=64, HW={args.size}^2)",
+                "kernel": ("fused into conv1_2's epilogue (launch with gram_part minus launch "
+                           "without) + gram_finalize_kernel from the partials"
+                           if g["gram"]["fused"] else
+                           "gram_partial_f16_kernel + gram_finalize_kernel")
+                          + f" (StyleLoss.gram_matrix of conv1_2's output, C=64, HW={args.size}^2)",
                 "ms": round(g["gram"]["ms"], 4),
+                "parts_ms": {kk: round(v, 4) for kk, v in g["gram"].items()
+                             if kk in ("epi_ms", "finalize_ms", "conv_ms")},
                 "achieved_tflops_fp32eq": round(g["gram"]["gflop"] / g["gram"]["ms"], 2),
                 "mfma_bf16_peak_frac": round(3 * g["gram"]["gflop"] / g["gram"]["ms"]
                                              / PEAK_F16_MFMA_TFLOPS, 4),
                 "hbm_gbs": round(g["gram"]["bytes"] / (g["gram"]["ms"] * 1e-3) / 1e9, 1),
                 "hbm_frac": round(g["gram"]["bytes"] / (g["gram"]["ms"] * 1e-3) / 1e9
                                   / PEAK_HBM_GBS, 4),
-                "note": "HBM-bound: 2*C^2*HW FLOPs over C*HW*4 bytes = 32 FLOP/B; the MFMA "
-                        "fraction counts the 3 fp16 products per fp32 product",
+                "note": "standalone it is HBM-bound (2*C^2*HW FLOPs over C*HW*4 bytes = 32 "
+                        "FLOP/B); fused, Z is not re-read and the cost is the epilogue's extra "
+                        "time + the partial reduction; hbm_* rate Z's bytes over that time; the "
+                        "MFMA fraction counts the 3 fp16 products per fp32 product",
             },
             "cpu_baseline": cpu,
             "gatys_loss": g["loss"],
