@@ -417,6 +417,138 @@ __device__ __forceinline__ void gram_f16_tile(const float* __restrict__ z, float
 }
 #undef MF16
 
+// Whole-triangle split Gram for C = 128 / 256 (the conv2_x / conv3_1 taps): a block
+// takes a pixel range of one image and ALL 32 x 32 blocks of the upper triangle of
+// G (10 / 36 of them), so z is read exactly once (the 64 x 64-tile kernel above reads
+// every row (nt + 1) / 2 times).  Per chunk of 64 pixels the C x 64 slab is split
+// into fp16 hi/lo planes in LDS ([plane][channel][pixel], pitch 72 halves: the 16-B
+// fragment reads of 16 lanes hit distinct banks) -- once per element instead of once
+// per tile that uses it -- with the next chunk's loads in flight; wave w owns blocks
+// w, w + 4, ... (3 MFMAs per block per 16 pixels).  The partials are written in the
+// 64 x 64-tile layout gram_finalize_kernel reads (diagonal tiles with the mirrored
+// lower-left quadrant).
+template <int C>
+__global__ void __launch_bounds__(256, 1)
+gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw, int nsplit,
+                    int split_len, const float* __restrict__ z_amax) {
+  constexpr int NB = C / 32;                 // 32-row blocks per side
+  constexpr int NBLK = NB * (NB + 1) / 2;    // upper-triangle blocks
+  constexpr int PER = (NBLK + 3) / 4;        // per wave
+  constexpr int NPX = 64, HP = NPX + 8;      // pixels per chunk, plane pitch (halves)
+  constexpr int NL = C * NPX / 4 / 256;      // float4 loads per thread per chunk
+  constexpr int NT = C / GT, NTU = NT * (NT + 1) / 2;
+  __shared__ __attribute__((aligned(16))) _Float16 pl[2 * C * HP];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int split = blockIdx.x, b = blockIdx.z;
+  const int p0 = split * split_len, p1 = min(hw, p0 + split_len);
+  const float* zb = z + (size_t)b * C * hw;
+  const auto rz = make_srd(zb, (uint32_t)C * (uint32_t)hw * 4u);
+  const int e = gram_amax_exp(read_amax(z_amax));
+  const float sx = __builtin_ldexpf(1.f, 15 - e), inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
+  // this wave's blocks (bi <= bj), row-major over the upper triangle
+  int bi[PER], bj[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    int t = wave + 4 * q, i = 0;
+    if (t >= NBLK) t = 0;  // padding slot (its result is not stored)
+    while (t >= NB - i) {
+      t -= NB - i;
+      ++i;
+    }
+    bi[q] = i;
+    bj[q] = i + t;
+  }
+  f32x16 acc[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+  // loads: float4 f = tid + 256 r -> (channel f / 16, pixels 4 (f % 16) ..)
+  f32x4 ld[NL];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int r = 0; r < NL; ++r) {
+      const int f = tid + 256 * r, ch = f >> 4, px = c0 + 4 * (f & 15);
+      ld[r] = buf_ld4(rz, px < p1 ? (uint32_t)(ch * hw + px) * 4u : BUF_OOB);
+    }
+  };
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  auto stage = [&]() {
+#pragma unroll
+    for (int r = 0; r < NL; ++r) {
+      const int f = tid + 256 * r, ch = f >> 4, px = 4 * (f & 15);
+      f16x4 hi, lo;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float v = ld[r][k] * sx;
+        hi[k] = (_Float16)v;
+        lo[k] = (_Float16)(v - (float)hi[k]);
+      }
+      *reinterpret_cast<f16x4*>(pl + ch * HP + px) = hi;
+      *reinterpret_cast<f16x4*>(pl + (C + ch) * HP + px) = lo;
+    }
+  };
+  if (p0 < p1) fetch(p0);
+  for (int c0 = p0; c0 < p1; c0 += NPX) {
+    __syncthreads();  // the previous chunk's fragment reads are done
+    stage();
+    __syncthreads();
+    if (c0 + NPX < p1) fetch(c0 + NPX);  // in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < NPX / 16; ++ks) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        if (wave + 4 * q >= NBLK) continue;
+        const _Float16* ra = pl + (bi[q] * 32 + l32) * HP + ks * 16 + 8 * h;
+        const _Float16* rb = pl + (bj[q] * 32 + l32) * HP + ks * 16 + 8 * h;
+        const f16x8_t ah = *reinterpret_cast<const f16x8_t*>(ra);
+        const f16x8_t al = *reinterpret_cast<const f16x8_t*>(ra + C * HP);
+        const f16x8_t bh = *reinterpret_cast<const f16x8_t*>(rb);
+        const f16x8_t bl = *reinterpret_cast<const f16x8_t*>(rb + C * HP);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[q], 0, 0, 0);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[q], 0, 0, 0);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[q], 0, 0, 0);
+      }
+    }
+  }
+  // partials in the 64 x 64-tile layout [b][tile][split][64][64]
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (wave + 4 * q >= NBLK) continue;
+    const int I = bi[q] >> 1, J = bj[q] >> 1, qi = bi[q] & 1, qj = bj[q] & 1;
+    float* out = ws + (((size_t)b * NTU + tile_index(I, J, NT)) * nsplit + split) * (GT * GT);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float v = acc[q][r] * inv2;
+      out[(qi * 32 + row) * GT + qj * 32 + l32] = v;
+      if (I == J && qi != qj) out[(qj * 32 + l32) * GT + qi * 32 + row] = v;  // mirror
+    }
+  }
+}
+
+static int gram_tri_splits(int c, int hw) {
+  static const int target = [] {
+    const char* e = getenv("STX_GRAM_TRI_BLOCKS");
+    return e ? std::max(8, atoi(e)) : 256;  // C = 128 @ 256^2: 256 > 128 > 64 blocks (A/B)
+  }();
+  return std::max(1, std::min(target, hw / 64));
+}
+
+static bool gram_tri_on(int c, int hw) {
+  static const bool on = [] {
+    const char* e = getenv("STX_GRAM_TRI");
+    return !(e && atoi(e) == 0);
+  }();
+  // C = 256 @ 128^2 measured slower than the 64 x 64-tile kernel (36 vs 10 blocks of
+  // accumulators per block: 33-37 us vs 32 us with the finalize); STX_GRAM_TRI=2 forces it
+  static const bool all = [] {
+    const char* e = getenv("STX_GRAM_TRI");
+    return e && atoi(e) == 2;
+  }();
+  return on && (c == 128 || (all && c == 256)) && hw % 64 == 0;
+}
+
 // grid (ntu * 16, B); one thread per tile element (256 elements per block).  The
 // split partials are summed in a fixed order (bit-reproducible); loads are
 // independent and unrolled so a block streams its slab column at full rate.
@@ -551,6 +683,7 @@ static size_t gram_parts_offset(int b, int c, int hw, int* nparts) {
   gram_geometry(c, hw, b, nsplit, split_len, ntu);
   gram_geometry16(c, hw, b, ns16, sl16, ntu);
   nsplit = std::max(nsplit, ns16);
+  if (gram_tri_on(c, hw)) nsplit = std::max(nsplit, gram_tri_splits(c, hw));
   if (nparts) *nparts = b * ntu * FSUB;
   return (size_t)b * ntu * nsplit * GT * GT * sizeof(float);
 }
@@ -582,7 +715,17 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
   }
   float* slabs = (float*)ws;
   float* parts = (float*)((char*)ws + gram_parts_offset(b, c, hw, nullptr));
-  if (f16) {
+  if (f16 && gram_tri_on(c, hw)) {
+    nsplit = gram_tri_splits(c, hw);
+    split_len = rup(cdiv(hw, nsplit), 64);
+    nsplit = cdiv(hw, split_len);
+    if (c == 128)
+      hipLaunchKernelGGL(gram_tri_f16_kernel<128>, dim3(nsplit, 1, b), dim3(256), 0, st, z, slabs,
+                         hw, nsplit, split_len, z_amax);
+    else
+      hipLaunchKernelGGL(gram_tri_f16_kernel<256>, dim3(nsplit, 1, b), dim3(256), 0, st, z, slabs,
+                         hw, nsplit, split_len, z_amax);
+  } else if (f16) {
     hipLaunchKernelGGL(gram_partial_f16_kernel, dim3(nsplit * ntu, 1, b), dim3(256), 0, st, z,
                        slabs, c, hw, nsplit, split_len, z_amax);
   } else if (hw % 4 == 0) {

@@ -108,7 +108,10 @@ def main():
             print(f"{'gram bwd split+unpool C%d' % c:32s} {ms3 * 1e3:9.1f} us "
                   f"{mb / (ms3 * 1e3):6.2f} TB/s ({mb:.0f} MB)", flush=True)
         gf = 2.0 * n * c * c * h * h / 1e9
-        print(f"{name:32s} fwd {ms * 1e3:8.1f} us {gf / ms:7.2f} TF | bwd {ms2 * 1e3:8.1f} us "
+        zam2 = ops.amax(z)
+        ms16 = ev(lambda: ops.style_loss(z, t, z_amax=zam2))
+        print(f"{name:32s} fwd {ms * 1e3:8.1f} us {gf / ms:7.2f} TF | split {ms16 * 1e3:8.1f} us "
+              f"{c * h * h * n * 4 / (ms16 * 1e3) / 1e6:5.2f} TB/s | bwd {ms2 * 1e3:8.1f} us "
               f"{gf / ms2:7.2f} TF")
     # wgrad
     up = N.STX_IN_UPSAMPLE2
