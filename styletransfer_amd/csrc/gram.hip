@@ -527,12 +527,13 @@ gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw,
   }
 }
 
-static int gram_tri_splits(int c, int hw) {
+static int gram_tri_splits(int c, int hw, int b) {
   static const int target = [] {
     const char* e = getenv("STX_GRAM_TRI_BLOCKS");
     return e ? std::max(8, atoi(e)) : 256;  // C = 128 @ 256^2: 256 > 128 > 64 blocks (A/B)
   }();
-  return std::max(1, std::min(target, hw / 64));
+  // ~target blocks over the whole batch (the partial slab grows with b * splits)
+  return std::max(1, std::min(std::max(1, target / std::max(1, b)), hw / 64));
 }
 
 static bool gram_tri_on(int c, int hw) {
@@ -616,13 +617,26 @@ gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scal
   }
 }
 
-// single block: sum parts (fixed order) -> loss = sum * inv
+// one wave: the fixed-order sum of n loss partials (4 lane-strided accumulators, then a
+// wave tree) -- shared by sum_parts_kernel and loss_finalize_kernel so the deferred and
+// direct style losses are the same bits
+__device__ __forceinline__ float wave_sum_parts(const float* __restrict__ parts, int n, int lane) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int i = lane;
+  for (; i + 192 < n; i += 256) {
+    s0 += parts[i];
+    s1 += parts[i + 64];
+    s2 += parts[i + 128];
+    s3 += parts[i + 192];
+  }
+  for (; i < n; i += 64) s0 += parts[i];
+  return wave_sum((s0 + s1) + (s2 + s3));
+}
+
+// single wave: loss = inv * sum(parts)
 __global__ void sum_parts_kernel(const float* __restrict__ parts, int n, float inv,
                                  float* __restrict__ out) {
-  __shared__ float red[4];
-  float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) s += parts[i];
-  s = block_sum<256>(s, red);
+  const float s = wave_sum_parts(parts, n, threadIdx.x);
   if (threadIdx.x == 0) *out = s * inv;
 }
 
@@ -683,7 +697,7 @@ static size_t gram_parts_offset(int b, int c, int hw, int* nparts) {
   gram_geometry(c, hw, b, nsplit, split_len, ntu);
   gram_geometry16(c, hw, b, ns16, sl16, ntu);
   nsplit = std::max(nsplit, ns16);
-  if (gram_tri_on(c, hw)) nsplit = std::max(nsplit, gram_tri_splits(c, hw));
+  if (gram_tri_on(c, hw)) nsplit = std::max(nsplit, gram_tri_splits(c, hw, b));
   if (nparts) *nparts = b * ntu * FSUB;
   return (size_t)b * ntu * nsplit * GT * GT * sizeof(float);
 }
@@ -716,7 +730,7 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
   float* slabs = (float*)ws;
   float* parts = (float*)((char*)ws + gram_parts_offset(b, c, hw, nullptr));
   if (f16 && gram_tri_on(c, hw)) {
-    nsplit = gram_tri_splits(c, hw);
+    nsplit = gram_tri_splits(c, hw, b);
     split_len = rup(cdiv(hw, nsplit), 64);
     nsplit = cdiv(hw, split_len);
     if (c == 128)
@@ -742,7 +756,7 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
   hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(256), 0, st, slabs, c,
                      nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts);
   if (target && loss)
-    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, st, parts, b * ntu * FSUB,
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, parts, b * ntu * FSUB,
                        loss_inv, loss);
   return check_launch("gram");
 }
@@ -758,22 +772,21 @@ extern "C" size_t stx_style_loss_parts(int b, int c, int hw, int* nparts) {
 }
 
 namespace stx {
-// one block: losses[i] = inv_i * sum(parts_i) (the per-thread strided order of
-// sum_parts_kernel, so the values are identical), then the weighted total
-__global__ void loss_finalize_kernel(stx_loss_parts lp, float* __restrict__ losses,
-                                     const float* __restrict__ extra, int m, LossWF w,
-                                     float* __restrict__ total) {
-  __shared__ float red[4];
-  float lv[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    lv[i] = 0.f;
-    if (i < lp.k) {
-      float s = 0.f;
-      for (int j = threadIdx.x; j < lp.nparts[i]; j += 256) s += lp.parts[i][j];
-      lv[i] = block_sum<256>(s, red) * lp.inv[i];
-    }
+// one block: losses[i] = inv_i * sum(parts_i) (wave i, the order of sum_parts_kernel, so
+// the values are identical), then the weighted total
+__global__ void __launch_bounds__(512) loss_finalize_kernel(stx_loss_parts lp,
+                                                           float* __restrict__ losses,
+                                                           const float* __restrict__ extra,
+                                                           int m, LossWF w,
+                                                           float* __restrict__ total) {
+  // wave i reduces loss i (the sum_parts_kernel order), all losses in parallel
+  __shared__ float lv[8];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave < lp.k) {
+    const float s = wave_sum_parts(lp.parts[wave], lp.nparts[wave], lane);
+    if (lane == 0) lv[wave] = s * lp.inv[wave];
   }
+  __syncthreads();
   if (threadIdx.x == 0) {
     float t = 0.f;
     for (int i = 0; i < lp.k; ++i) {
@@ -795,7 +808,7 @@ extern "C" int stx_loss_finalize(const stx_loss_parts* lp, float* losses, const 
   }
   LossWF w{};
   for (int i = 0; i < lp->k + m && w_host; ++i) w.w[i] = w_host[i];
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *lp,
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, *lp,
                      losses, extra, m, w, total);
   return check_launch("stx_loss_finalize");
 }
@@ -859,7 +872,7 @@ extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const 
                      (float)(1.0 / n), g_out, target,
                      target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts);
   if (loss)
-    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(256), 0, st, lparts, b * FSUB,
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, lparts, b * FSUB,
                        (float)(1.0 / ((double)b * c * c)), loss);
   return check_launch("stx_style_loss_from_parts");
 }
