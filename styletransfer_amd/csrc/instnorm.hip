@@ -373,6 +373,87 @@ instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ 
   }
 }
 
+// Large planes (the ITN's 256^2 layers: 64 K floats, 1024 threads x 16 float4): only g
+// stays in registers (64 VGPRs -- g and x-hat together would not fit 16 waves per CU);
+// the second pass re-reads u = x (+ res) instead of dy, y and u, one plane-read fewer
+// of dy and y than the two-pass loop kernel.  Same arithmetic as instnorm_bwd_reg_kernel.
+template <int NT, int R4, bool RELU, bool RES>
+__global__ void __launch_bounds__(NT)
+instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                         const float* __restrict__ x, const float* __restrict__ res,
+                         const float* __restrict__ gamma, const float* __restrict__ mean,
+                         const float* __restrict__ rstd, float* __restrict__ du,
+                         float* __restrict__ parts, int c, int hw, int relu,
+                         float* __restrict__ out_amax) {
+  __shared__ float red[NT / 64];
+  const size_t base = (size_t)blockIdx.x * hw;
+  const int ch = blockIdx.x % c;
+  const float mu = mean[blockIdx.x], rs = rstd[blockIdx.x];
+  // per-plane buffer descriptors: one lane offset, the per-k step in the scalar offset
+  // (64-bit addresses per k would take 2 VGPRs each and spill); elements past the
+  // plane read 0 and their stores are dropped by the range check
+  const uint32_t pbytes = (uint32_t)hw * 4u;
+  const auto rdy = make_srd(dy + base, pbytes);
+  const auto ry = make_srd(RELU ? y + base : dy + base, pbytes);
+  const auto rx = make_srd(x + base, pbytes);
+  const auto rr = make_srd(RES ? res + base : x + base, pbytes);
+  const auto rdu = make_srd(du + base, pbytes);
+  const uint32_t lo = threadIdx.x * 16u;
+  constexpr uint32_t KSTEP = NT * 16u;
+  const int n4 = hw >> 2;
+  f32x4 g[R4];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int k = 0; k < R4; ++k) {
+    const f32x4 d4 = __builtin_bit_cast(
+        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rdy, lo, k * KSTEP, 0));
+    f32x4 u4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, lo, k * KSTEP, 0));
+    if (RES) u4 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, lo, k * KSTEP, 0));
+    f32x4 y4 = {1.f, 1.f, 1.f, 1.f};
+    if (RELU) y4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, lo, k * KSTEP, 0));
+    const bool in = (int)threadIdx.x + k * NT < n4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      g[k][e] = (RELU && !(y4[e] > 0.f)) ? 0.f : d4[e];
+      const float xh = in ? (u4[e] - mu) * rs : 0.f;
+      sg += g[k][e];
+      sgx += g[k][e] * xh;
+    }
+    // at most 4 steps of loads in flight (the scheduler would hoist all 16 and spill)
+    if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+  sg = block_sum_nt<NT>(sg, red);
+  sgx = block_sum_nt<NT>(sgx, red);
+  const float gm = gamma ? gamma[ch] : 1.f;
+  const float kk = gm * rs / (float)hw;
+  uint32_t om = 0u;
+  float sdu = 0.f;
+#pragma unroll
+  for (int k = 0; k < R4; ++k) {
+    if ((k & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+    f32x4 u4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, lo, k * KSTEP, 0));
+    if (RES) u4 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, lo, k * KSTEP, 0));
+    const bool in = (int)threadIdx.x + k * NT < n4;
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xh = (u4[e] - mu) * rs;
+      o[e] = in ? kk * ((float)hw * g[k][e] - sg - xh * sgx) : 0.f;
+      om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
+    }
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rdu, lo, k * KSTEP, 0);
+    sdu += (o[0] + o[1]) + (o[2] + o[3]);
+  }
+  sdu = block_sum_nt<NT>(sdu, red);
+  if (threadIdx.x == 0) {
+    parts[3 * blockIdx.x] = sgx;
+    parts[3 * blockIdx.x + 1] = sg;
+    parts[3 * blockIdx.x + 2] = sdu;
+  }
+  if (out_amax) block_max_to_nt<NT>(out_amax, om, red);
+}
+
 // dgamma, dbeta and the producing conv's bias gradient: fixed-order sums over n
 __global__ void instnorm_param_grad_kernel(const float* __restrict__ parts, int n, int c,
                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
@@ -474,6 +555,14 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
   return check_launch("stx_instnorm_fwd");
 }
 
+static bool greg_on() {
+  static const bool on = [] {
+    const char* e = getenv("STX_IN_GREG");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 extern "C" size_t stx_instnorm_bwd_ws(int n, int c) {
   return (size_t)3 * n * c * sizeof(float) + 64;
 }
@@ -501,6 +590,10 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
   else if (al && hw <= 4 * 256 * 16)
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 16>), dim3(n * c), dim3(256), 0, st, dy, y,
                        x, res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
+  else if (al && hw <= 4 * 1024 * 16 && relu && !res && greg_on())  // 256^2 IN + ReLU
+    hipLaunchKernelGGL((instnorm_bwd_greg_kernel<1024, 16, true, false>), dim3(n * c),
+                       dim3(1024), 0, st, dy, y, x, res, gamma, mean, rstd, du, (float*)ws, c,
+                       hw, relu, out_amax);
   else if (hw >= 4 * 1024 * 4)  // big planes (256^2): 16 waves per plane
     hipLaunchKernelGGL(instnorm_bwd_kernel<1024>, dim3(n * c), dim3(1024), 0, st, dy, y, x, res,
                        gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
