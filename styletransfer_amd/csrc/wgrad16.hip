@@ -428,17 +428,20 @@ wgrad16_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg1
 // global loads in flight.  Against wgrad16_kernel this removes the 4x redundant
 // V conversion of its four waves and halves the number of K splits (1 block per CU
 // instead of 8 waves), so the split-K slab the reduce kernel reads is half as big.
-template <int WCO, bool UP, int PF>  // WCO = couts / 32; UP: nearest x2 upsampled input;
-__global__ void __launch_bounds__(256, 1)  // PF + 1 steps of loads in flight (PF odd)
+// CIB = cins per block (64; 128 for cout = 64, so each wave still owns two 32 x 32
+// (co, ci) tiles: 18 MFMAs per barrier instead of 9)
+template <int WCO, bool UP, int PF, int CIB = 64>  // WCO = couts / 32; UP: nearest x2
+__global__ void __launch_bounds__(256, 1)  // upsampled input; PF + 1 steps of loads in flight
 wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                    float* __restrict__ ws, const float* __restrict__ x_amax,
                    const float* __restrict__ dy_amax, Wg16 g) {
-  constexpr int NPAIR = WCO * 2 / 4;       // (co tile, ci tile) pairs per wave
-  __shared__ __attribute__((aligned(16))) char vimg[2][3 * 2 * 2 * 64 * 16];  // 2 x 12 KB
+  constexpr int NCI = CIB / 64;            // staged cin rows per thread
+  constexpr int NPAIR = WCO * 2 * NCI / 4;  // (co tile, ci tile) pairs per wave
+  __shared__ __attribute__((aligned(16))) char vimg[2][3 * 2 * 2 * CIB * 16];  // 2 x 12|24 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
   int unit = blockIdx.x;
-  const int cit = unit % g.ncit;           // 64-cin tile
+  const int cit = unit % g.ncit;           // CIB-cin tile
   unit /= g.ncit;
   const int kh = unit % 3;
   const int split = unit / 3;
@@ -448,18 +451,18 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   const int H = g.hv, W = g.wv, wsteps = W / 16;
   const bool relu = g.mode == STX_IN_RELU;
   // this wave's (co tile, ci tile) pairs: WCO = 4 -> co tile = wave, ci tiles 0, 1;
-  // WCO = 2 -> co tile = wave & 1, ci tile = wave >> 1
+  // WCO = 2 -> co tile = wave & 1, ci tile(s) (wave >> 1) * NCI + 0 .. NCI - 1
   const int cot = WCO == 4 ? wave : (wave & 1);
   const int co = cot * 32 + l32;
   // V staging: thread -> (ci = tid / 4, quad q = tid % 4): pixels x0 + 4q - 1 .. x0 + 4q + 4
   const int sci = tid >> 2, q = tid & 3;
-  const int ci_g = cit * 64 + sci;
+  const int ci_g = cit * CIB + sci;        // (+ 64 r for row r < NCI)
   const auto rdy = make_srd(dy, (uint32_t)((size_t)g.n * g.cout * H * W * 4u));
   const auto rx = make_srd(x, (uint32_t)((size_t)g.n * g.cin * g.h * g.w * 4u));
   struct Ld {
     f32x4 a0, a1;        // dY[co][y][x0 + 8h .. +7]
-    f32x4 v;             // V[ci][vy][x0 + 4q .. +3] (upsample: x[.][vy/2][(x0+4q)/2 .. +1] in v.xy)
-    float vl, vr;        // V at x0 + 4q - 1 and x0 + 4q + 4
+    f32x4 v[NCI];        // V[ci][vy][x0 + 4q .. +3] (upsample: x[.][vy/2][(x0+4q)/2 .. +1] in v.xy)
+    float vl[NCI], vr[NCI];  // V at x0 + 4q - 1 and x0 + 4q + 4
   };
   // Every load is issued unconditionally (steps past the split's end read zeros
   // through out-of-range offsets) so the wait counts stay exact: no branch around a
@@ -480,50 +483,58 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
     t.a1 = buf_ld4(rdy, live ? oa + 16u : BUF_OOB);
     const int vy = y + kh - 1, px = x0 + 4 * q;
     const bool rok = live && vy >= 0 && vy < H;
-    if constexpr (!UP) {
-      const uint32_t ob = (uint32_t)((((size_t)n * g.cin + ci_g) * g.h + vy) * g.w + px) * 4u;
-      t.v = buf_ld4(rx, rok ? ob : BUF_OOB);
-      t.vl = buf_ld(rx, (rok && px > 0) ? ob - 4u : BUF_OOB);
-      t.vr = buf_ld(rx, (rok && px + 4 < W) ? ob + 16u : BUF_OOB);
-    } else {  // V[vy][vx] = x[vy/2][vx/2]; px is a multiple of 4
-      const uint32_t ob =
-          (uint32_t)((((size_t)n * g.cin + ci_g) * g.h + (vy >> 1)) * g.w + (px >> 1)) * 4u;
-      t.v.x = buf_ld(rx, rok ? ob : BUF_OOB);
-      t.v.y = buf_ld(rx, rok ? ob + 4u : BUF_OOB);
-      t.vl = buf_ld(rx, (rok && px > 0) ? ob - 4u : BUF_OOB);
-      t.vr = buf_ld(rx, (rok && px + 4 < W) ? ob + 8u : BUF_OOB);
+#pragma unroll
+    for (int r = 0; r < NCI; ++r) {
+      const size_t cig = (size_t)ci_g + 64 * r;
+      if constexpr (!UP) {
+        const uint32_t ob = (uint32_t)((((size_t)n * g.cin + cig) * g.h + vy) * g.w + px) * 4u;
+        t.v[r] = buf_ld4(rx, rok ? ob : BUF_OOB);
+        t.vl[r] = buf_ld(rx, (rok && px > 0) ? ob - 4u : BUF_OOB);
+        t.vr[r] = buf_ld(rx, (rok && px + 4 < W) ? ob + 16u : BUF_OOB);
+      } else {  // V[vy][vx] = x[vy/2][vx/2]; px is a multiple of 4
+        const uint32_t ob =
+            (uint32_t)((((size_t)n * g.cin + cig) * g.h + (vy >> 1)) * g.w + (px >> 1)) * 4u;
+        t.v[r].x = buf_ld(rx, rok ? ob : BUF_OOB);
+        t.v[r].y = buf_ld(rx, rok ? ob + 4u : BUF_OOB);
+        t.vl[r] = buf_ld(rx, (rok && px > 0) ? ob - 4u : BUF_OOB);
+        t.vr[r] = buf_ld(rx, (rok && px + 4 < W) ? ob + 8u : BUF_OOB);
+      }
     }
   };
-  // V -> the three kw-shifted fp16 hi/lo copies in LDS (thread: 4 pixels of one ci)
+  // V -> the three kw-shifted fp16 hi/lo copies in LDS (thread: 4 pixels of NCI cins)
   auto stage = [&](const Ld& t, char* img) {
-    float v6[6];
-    v6[0] = t.vl;
-    v6[5] = t.vr;
-    if constexpr (!UP) {
-      v6[1] = t.v.x; v6[2] = t.v.y; v6[3] = t.v.z; v6[4] = t.v.w;
-    } else {
-      v6[1] = v6[2] = t.v.x;
-      v6[3] = v6[4] = t.v.y;
-    }
-    _Float16 hi[6], lo[6];
 #pragma unroll
-    for (int e = 0; e < 6; ++e) {
-      float v = v6[e];
-      if (relu) v = fmaxf(v, 0.f);
-      v *= sv;
-      hi[e] = (_Float16)v;
-      lo[e] = (_Float16)(v - (float)hi[e]);
-    }
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    for (int r = 0; r < NCI; ++r) {
+      float v6[6];
+      v6[0] = t.vl[r];
+      v6[5] = t.vr[r];
+      if constexpr (!UP) {
+        v6[1] = t.v[r].x; v6[2] = t.v[r].y; v6[3] = t.v[r].z; v6[4] = t.v[r].w;
+      } else {
+        v6[1] = v6[2] = t.v[r].x;
+        v6[3] = v6[4] = t.v[r].y;
+      }
+      _Float16 hi[6], lo[6];
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      // copy kw, element e = 4q + j holds V[x0 + e + kw - 1] = v6[j + kw]
-      const h4 ph = {hi[kw], hi[kw + 1], hi[kw + 2], hi[kw + 3]};
-      const h4 pl = {lo[kw], lo[kw + 1], lo[kw + 2], lo[kw + 3]};
-      const int base = (((kw * 2 + 0) * 2 + (q >> 1)) * 64 + sci) * 16 + (q & 1) * 8;
-      const int base_l = (((kw * 2 + 1) * 2 + (q >> 1)) * 64 + sci) * 16 + (q & 1) * 8;
-      *reinterpret_cast<h4*>(img + base) = ph;
-      *reinterpret_cast<h4*>(img + base_l) = pl;
+      for (int e = 0; e < 6; ++e) {
+        float v = v6[e];
+        if (relu) v = fmaxf(v, 0.f);
+        v *= sv;
+        hi[e] = (_Float16)v;
+        lo[e] = (_Float16)(v - (float)hi[e]);
+      }
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      const int ci_l = sci + 64 * r;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        // copy kw, element e = 4q + j holds V[x0 + e + kw - 1] = v6[j + kw]
+        const h4 ph = {hi[kw], hi[kw + 1], hi[kw + 2], hi[kw + 3]};
+        const h4 pl = {lo[kw], lo[kw + 1], lo[kw + 2], lo[kw + 3]};
+        const int base = (((kw * 2 + 0) * 2 + (q >> 1)) * CIB + ci_l) * 16 + (q & 1) * 8;
+        const int base_l = (((kw * 2 + 1) * 2 + (q >> 1)) * CIB + ci_l) * 16 + (q & 1) * 8;
+        *reinterpret_cast<h4*>(img + base) = ph;
+        *reinterpret_cast<h4*>(img + base_l) = pl;
+      }
     }
   };
   f32x16 acc[NPAIR][3];
@@ -543,11 +554,12 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
     }
 #pragma unroll
     for (int pi = 0; pi < NPAIR; ++pi) {
-      const int ct = WCO == 4 ? pi : (wave >> 1);   // ci tile (32 cins) within the 64
+      // ci tile (32 cins) within the block's CIB
+      const int ct = WCO == 4 ? pi : (wave >> 1) * NCI + (NPAIR > 1 ? pi : 0);
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const h8 bh = *reinterpret_cast<const h8*>(img + (((kw * 2 + 0) * 2 + h) * 64 + ct * 32 + l32) * 16);
-        const h8 bl = *reinterpret_cast<const h8*>(img + (((kw * 2 + 1) * 2 + h) * 64 + ct * 32 + l32) * 16);
+        const h8 bh = *reinterpret_cast<const h8*>(img + (((kw * 2 + 0) * 2 + h) * CIB + ct * 32 + l32) * 16);
+        const h8 bl = *reinterpret_cast<const h8*>(img + (((kw * 2 + 1) * 2 + h) * CIB + ct * 32 + l32) * 16);
         acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[pi][kw], 0, 0, 0);
         acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[pi][kw], 0, 0, 0);
         acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[pi][kw], 0, 0, 0);
@@ -582,11 +594,11 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   // partial [split][kh*3+kw][co (cout32)][ci (cin32)], descaled (exact)
 #pragma unroll
   for (int pi = 0; pi < NPAIR; ++pi) {
-    const int ct = WCO == 4 ? pi : (wave >> 1);
+    const int ct = WCO == 4 ? pi : (wave >> 1) * NCI + (NPAIR > 1 ? pi : 0);
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       float* out = ws + (((size_t)split * 9 + kh * 3 + kw) * g.cout32 + cot * 32) * g.cin32 +
-                   cit * 64 + ct * 32 + l32;
+                   cit * CIB + ct * 32 + l32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -604,7 +616,10 @@ static bool wg16_lds_on() {
   return on;
 }
 
-static bool lds_on_64() {  // cout 64 on the LDS kernel: 1.6x slower (A/B), off by default
+// cout 64 on the LDS kernel (STX_WG16_LDS64=1): 64 cins per block measured 1.6x slower
+// than the register-direct kernel, 128 cins per block (cin % 128 == 0) 5 % slower on the
+// ITN up conv (188 vs 179 us, same box): off by default
+static bool lds_on_64() {
   static const bool on = [] {
     const char* e = getenv("STX_WG16_LDS64");
     return e && atoi(e) != 0;
@@ -646,7 +661,7 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
           (in_mode == STX_IN_RAW || in_mode == STX_IN_RELU || in_mode == STX_IN_UPSAMPLE2);
   if (g.lds) {  // blocks of (all couts x 64 cins x kh) x K split: ~512 blocks
     g.ncot = 1;
-    g.ncit = cin / 64;
+    g.ncit = cout == 64 && cin % 128 == 0 ? cin / 128 : cin / 64;  // CIB
     g.cout32 = cout;
     g.cin32 = cin;
     g.ci2 = 0;
@@ -728,7 +743,9 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
               : (lpf >= 7 ? wgrad16_lds_kernel<4, false, 7>
                           : (lpf >= 5 ? wgrad16_lds_kernel<4, false, 5>
                                       : wgrad16_lds_kernel<4, false, 3>)))
-        : (up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>);
+        : (cin % 128 == 0
+               ? (up ? wgrad16_lds_kernel<2, true, 3, 128> : wgrad16_lds_kernel<2, false, 3, 128>)
+               : (up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>));
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, x, dy, (float*)ws, x_amax, dy_amax,
                        g);
   } else if (g.ci2)

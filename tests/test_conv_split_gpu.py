@@ -337,7 +337,10 @@ def test_split_gram_bwd_window_ties(dev, c):
                                   (2, 64, 64, 12, 32, N.STX_IN_RELU),
                                   (1, 128, 128, 1, 16, N.STX_IN_RAW),
                                   (3, 192, 64, 10, 24, N.STX_IN_UPSAMPLE2),
-                                  (1, 64, 128, 3, 16, N.STX_IN_RAW)])
+                                  (1, 64, 128, 3, 16, N.STX_IN_RAW),
+                                  # cout 64, cin % 128 == 0: 128 cins per block
+                                  (2, 256, 64, 6, 16, N.STX_IN_RAW),
+                                  (1, 128, 64, 5, 32, N.STX_IN_RELU)])
 def test_split_wgrad(dev, case):
     """3x3 weight gradient on the split MFMA vs fp64 (and the fp32 MFMA kernel)."""
     n, cin, cout, h, w, mode = case
