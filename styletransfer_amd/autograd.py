@@ -33,13 +33,30 @@ def _grad_into(param, g, accumulate_fn):
 
 
 # ----------------------------------------------------------------------- conv
+class ResLink:
+    """Hand-off of a residual block's skip gradient (stransfer/network.py:502 `out +=
+    residual`): the InstanceNorm that adds the residual stores its du here instead of
+    returning it for the block input, and the block's first conv (which reads the same
+    input) adds it in its data-gradient epilogue -- autograd's separate sum of the two
+    gradient contributions (one elementwise pass per block) disappears.  The IN's
+    backward always runs first: the first conv's output gradient depends on it."""
+
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
+
+
 class Conv2dFn(torch.autograd.Function):
     """y = conv2d(V(x), w) + b with V = identity / relu / nearest-upsample-x2.
     (nn.Conv2d of VGG-19 and ImageTransformNet; zero padding.)"""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, in_mode, wt=None, wt16=None, wtT=None, wtT16=None):
+    def forward(ctx, x, w, b, stride, pad, in_mode, wt=None, wt16=None, wtT=None, wtT16=None,
+                link=None):
         x = _c(x)
+        # link (ResLink): a skip gradient to add into dx (raw-input stride-1 convs only)
+        ctx.link = link if (stride == 1 and in_mode == N.STX_IN_RAW) else None
         cout, cin, ks, _ = w.shape
         # 3x3 stride-1 layers with cin >= 16 run on the fp16 hi/lo split MFMA kernel
         # (no fp32 slab needed); max|x| is computed once and kept for the wgrad.
@@ -97,8 +114,13 @@ class Conv2dFn(torch.autograd.Function):
                 else:
                     wtT = ctx.wtT if ctx.wtT is not None else ops.conv_weight_prep(
                         w.detach().contiguous(), transpose=True)
+                link = ctx.link
+                skip = link.g if link is not None else None
+                if link is not None:
+                    link.g = None
                 dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16,
-                                in_amax=dy_amax)
+                                in_amax=dy_amax, aux=skip, aux_scale=1.0 if skip is not None
+                                else 0.0)
             elif stride == 2:
                 # stride-1 conv over the zero-dilated dy; the split kernel takes it too
                 if _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1):
@@ -134,14 +156,14 @@ class Conv2dFn(torch.autograd.Function):
             b = ctx.b_ref
             db = _grad_into(b, lambda: ops.bias_grad(dy),
                             lambda dst: ops.bias_grad(dy, db=dst, accumulate=True))
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, w, b=None, stride=1, pad=None, in_mode=N.STX_IN_RAW, wt=None, wt16=None,
-           wtT=None, wtT16=None):
+           wtT=None, wtT16=None, link=None):
     ks = w.shape[-1]
     return Conv2dFn.apply(x, w, b, stride, ks // 2 if pad is None else pad, in_mode, wt, wt16,
-                          wtT, wtT16)
+                          wtT, wtT16, link)
 
 
 # ----------------------------------------------------------------------- relu / pool
@@ -189,7 +211,7 @@ class InstanceNormFn(torch.autograd.Function):
     """y = [relu](IN(x (+ res)) * gamma + beta), per-instance stats (eps 1e-5)."""
 
     @staticmethod
-    def forward(ctx, x, res, gamma, beta, eps, relu, conv_bias=None):
+    def forward(ctx, x, res, gamma, beta, eps, relu, conv_bias=None, res_link=None):
         # conv_bias: the bias of the conv that produced x, given when that conv ran with a
         # detached bias -- its gradient sum(du) comes out of this backward's kernel
         x, res = _c(x), _c(res)
@@ -203,6 +225,7 @@ class InstanceNormFn(torch.autograd.Function):
         ctx.cb_ref = conv_bias
         ctx.relu = relu
         ctx.has_res = res is not None
+        ctx.res_link = res_link if res is not None else None
         return y
 
     @staticmethod
@@ -222,11 +245,18 @@ class InstanceNormFn(torch.autograd.Function):
                               dbias_in=bufs[2], accumulate=acc, out_amax=ga)
         ops.ARENA.annotate(du, ga)
         dg, db, dcb = (None, None, None) if acc else bufs
-        return du, (du if ctx.has_res else None), dg, db, None, None, dcb
+        dres = None
+        if ctx.has_res:
+            if ctx.res_link is not None and ctx.needs_input_grad[1]:
+                ctx.res_link.g = du  # added by the block's first conv (ResLink)
+            else:
+                dres = du
+        return du, dres, dg, db, None, None, dcb, None
 
 
-def instance_norm(x, gamma, beta, res=None, eps=1e-5, relu=False, conv_bias=None):
-    return InstanceNormFn.apply(x, res, gamma, beta, eps, relu, conv_bias)
+def instance_norm(x, gamma, beta, res=None, eps=1e-5, relu=False, conv_bias=None,
+                  res_link=None):
+    return InstanceNormFn.apply(x, res, gamma, beta, eps, relu, conv_bias, res_link)
 
 
 # ----------------------------------------------------------------------- losses

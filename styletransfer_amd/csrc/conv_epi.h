@@ -190,7 +190,9 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
   }
 }
 
-template <int TW, int NI, bool ROWPAIR, bool RELU, int GDBG = 0>
+// AUX: value += aux_scale * aux (a residual block's skip gradient, ResLink), loaded
+// through a descriptor at the store offsets
+template <int TW, int NI, bool ROWPAIR, bool RELU, int GDBG = 0, bool AUX = false>
 __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
                                                          const stx_conv_params& p,
                                                          const EpiTile& t, float scale,
@@ -201,6 +203,8 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
   const int rows = max(0, p.cout - co_w);
   const uint32_t pb = (uint32_t)plane * 4u;
   const auto ry = make_srd(p.y + ((size_t)t.n * p.cout + co_w) * plane, (uint32_t)rows * pb);
+  const auto raux = make_srd(AUX ? p.aux + ((size_t)t.n * p.cout + co_w) * plane : p.y,
+                             AUX ? (uint32_t)rows * pb : 0u);
   uint32_t vo[NI];
   bool lane_ok[NI];
 #pragma unroll
@@ -237,6 +241,7 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
       for (int r = 0; r < 16; ++r) {
         const int row = i * 32 + (r & 3) + 8 * (r >> 2);
         float v = fmaf(acc[i][j][r], scale, bias_r[i][r]);
+        if (AUX) v += p.aux_scale * buf_ld(raux, vo[j] + (uint32_t)row * pb);
         if (RELU) v = fmaxf(v, 0.f);
         buf_st(ry, vo[j] + (uint32_t)row * pb, v);
         acc[i][j][r] = v;  // kept for the fused pooled output
@@ -288,11 +293,15 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
 template <int TW, int NI, bool ROWPAIR, int GDBG = 0>
 __device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const stx_conv_params& p,
                                                     const EpiTile& t, float scale, char* smem) {
-  if (p.mask || p.aux || p.accumulate || p.acc_scale || p.up_dp || p.p2_z) return false;
-  if (p.relu_out)
+  if (p.mask || p.accumulate || p.acc_scale || p.up_dp || p.p2_z) return false;
+  if (p.aux) {
+    if (p.relu_out || p.pool_out || p.gram_part) return false;
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, 0, true>(acc, p, t, scale, smem);
+  } else if (p.relu_out) {
     conv_epilogue_plain_body<TW, NI, ROWPAIR, true, GDBG>(acc, p, t, scale, smem);
-  else
+  } else {
     conv_epilogue_plain_body<TW, NI, ROWPAIR, false, GDBG>(acc, p, t, scale, smem);
+  }
   return true;
 }
 

@@ -46,7 +46,7 @@ class Conv2d(nn.Conv2d):
             self._wt_cache = (key, ops.conv_weight_prep(wd), w16)
         return self._wt_cache[1], self._wt_cache[2]
 
-    def forward(self, x, in_mode=N.STX_IN_RAW, bias_grad=True):
+    def forward(self, x, in_mode=N.STX_IN_RAW, bias_grad=True, link=None):
         """bias_grad=False: the bias enters detached -- for a conv feeding an
         InstanceNorm2d that is handed the bias (`conv_bias=`) and produces its gradient."""
         wt = wt16 = wtT = wtT16 = None
@@ -57,7 +57,8 @@ class Conv2d(nn.Conv2d):
         elif not w.requires_grad or not torch.is_grad_enabled():
             wt, wt16 = self.prepped()  # frozen or inference: slabs cached per weight version
         b = self.bias if bias_grad or self.bias is None else self.bias.detach()
-        return A.conv2d(x, w, b, self.stride[0], self.padding[0], in_mode, wt, wt16, wtT, wtT16)
+        return A.conv2d(x, w, b, self.stride[0], self.padding[0], in_mode, wt, wt16, wtT, wtT16,
+                        link)
 
 
 class ReLU(nn.ReLU):
@@ -78,11 +79,11 @@ class MaxPool2d(nn.MaxPool2d):
 
 
 class InstanceNorm2d(nn.InstanceNorm2d):
-    def forward(self, x, relu=False, res=None, conv_bias=None):
+    def forward(self, x, relu=False, res=None, conv_bias=None, res_link=None):
         if self.track_running_stats:
             raise NotImplementedError("track_running_stats")
         return A.instance_norm(x, self.weight, self.bias, res=res, eps=self.eps, relu=relu,
-                               conv_bias=conv_bias)
+                               conv_bias=conv_bias, res_link=res_link)
 
 
 class Upsample(nn.Upsample):

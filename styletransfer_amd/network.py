@@ -379,8 +379,12 @@ class ResidualBlock(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # IN + ReLU fused; (+ residual) + IN fused; each conv's bias gradient comes out of
         # the following IN's backward kernel (conv bias passed detached)
-        out = self.insn1(self.conv1(x, bias_grad=False), relu=True, conv_bias=self.conv1.bias)
-        return self.insn2(self.conv2(out, bias_grad=False), res=x, conv_bias=self.conv2.bias)
+        # the skip gradient (insn2's du for x) is added inside conv1's data-gradient epilogue
+        link = A.ResLink() if torch.is_grad_enabled() and x.requires_grad else None
+        out = self.insn1(self.conv1(x, bias_grad=False, link=link), relu=True,
+                         conv_bias=self.conv1.bias)
+        return self.insn2(self.conv2(out, bias_grad=False), res=x, conv_bias=self.conv2.bias,
+                          res_link=link)
 
 
 def _itn_layers(in_channels=3):
