@@ -330,7 +330,6 @@ __device__ __forceinline__ void gram_f16_tile(const float* __restrict__ z, float
   struct Grp {
     f32x4 x[4][2][2];  // [row a0, a1, b0, b1][step][lo/hi float4]
   };
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
   auto load = [&](int p0, Grp& g) {
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
