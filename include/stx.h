@@ -269,6 +269,17 @@ int stx_mse(const float* a, const float* b, long long n, int relu_inputs, int mo
 int stx_diff_scale(const float* a, const float* b, float* grad, long long n, float s0,
                    const float* s1_dev, const float* s2_dev, int relu, int accumulate,
                    void* stream);
+/* stx_style_loss(z, ...) and stx_mse(z, content, b*c*hw, 0, 2, mse_out, ...) (the content,
+ * feature and feature-mse values of ContentLoss / FeatureReconstructionLoss at the
+ * content tap, stransfer/network.py:155-164, 186-201) in one pass over z where the
+ * Gram kernel allows it (c = 128 on the split path), else as the two calls.
+ * ws >= stx_style_content_ws(b, c, hw); the deferred style-loss partials sit where
+ * stx_style_loss_parts says, as for stx_style_loss. */
+size_t stx_style_content_ws(int b, int c, int hw);
+int stx_style_content_loss(const float* z, const float* target, float* coef, float* loss,
+                           int b, int c, int hw, int target_batched, float weight,
+                           float diag_alpha, const float* z_amax, const float* content,
+                           float* mse_out, void* ws, size_t ws_bytes, void* stream);
 /* stx_style_loss from precomputed Gram partials (stx_conv_params.gram_part; c <= 64):
  * parts [b][nparts][64][64] summed in a fixed order, then the same G, coef, loss and
  * deferred loss partials (ws >= stx_gram_ws(b, c, hw); stx_style_loss_parts). */

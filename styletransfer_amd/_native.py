@@ -108,6 +108,9 @@ SIGNATURES = {
                              vp]),
     "stx_style_loss_from_parts": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32,
                                         vp, sz, vp]),
+    "stx_style_content_ws": (sz, [i32, i32, i32]),
+    "stx_style_content_loss": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, vp, vp,
+                                     vp, sz, vp]),
     "stx_gram_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, f32, i32, vp]),
     "stx_mse_ws": (sz, [i64]),
     "stx_mse": (i32, [vp, vp, i64, i32, i32, vp, vp, f32, vp, sz, vp]),

@@ -426,10 +426,13 @@ __device__ __forceinline__ void gram_f16_tile(const float* __restrict__ z, float
 // w, w + 4, ... (3 MFMAs per block per 16 pixels).  The partials are written in the
 // 64 x 64-tile layout gram_finalize_kernel reads (diagonal tiles with the mirrored
 // lower-left quadrant).
-template <int C>
+// MSE: also the content/feature sums of (z - cz)^2 and (relu z - relu cz)^2 over the
+// block's pixels (the pass over z the content loss needs anyway): mparts[2 blk + 0/1]
+template <int C, bool MSE = false>
 __global__ void __launch_bounds__(256, 1)
 gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw, int nsplit,
-                    int split_len, const float* __restrict__ z_amax) {
+                    int split_len, const float* __restrict__ z_amax,
+                    const float* __restrict__ cz = nullptr, float* __restrict__ mparts = nullptr) {
   constexpr int NB = C / 32;                 // 32-row blocks per side
   constexpr int NBLK = NB * (NB + 1) / 2;    // upper-triangle blocks
   constexpr int PER = (NBLK + 3) / 4;        // per wave
@@ -442,6 +445,8 @@ gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw,
   const int p0 = split * split_len, p1 = min(hw, p0 + split_len);
   const float* zb = z + (size_t)b * C * hw;
   const auto rz = make_srd(zb, (uint32_t)C * (uint32_t)hw * 4u);
+  const auto rc = make_srd(MSE ? cz + (size_t)b * C * hw : zb, (uint32_t)C * (uint32_t)hw * 4u);
+  float ms = 0.f, msr = 0.f;  // MSE sums
   const int e = gram_amax_exp(read_amax(z_amax));
   const float sx = __builtin_ldexpf(1.f, 15 - e), inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
   // this wave's blocks (bi <= bj), row-major over the upper triangle
@@ -464,11 +469,14 @@ gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw,
     for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
   // loads: float4 f = tid + 256 r -> (channel f / 16, pixels 4 (f % 16) ..)
   f32x4 ld[NL];
+  f32x4 lc[MSE ? NL : 1];
   auto fetch = [&](int c0) {
 #pragma unroll
     for (int r = 0; r < NL; ++r) {
       const int f = tid + 256 * r, ch = f >> 4, px = c0 + 4 * (f & 15);
-      ld[r] = buf_ld4(rz, px < p1 ? (uint32_t)(ch * hw + px) * 4u : BUF_OOB);
+      const uint32_t o = px < p1 ? (uint32_t)(ch * hw + px) * 4u : BUF_OOB;
+      ld[r] = buf_ld4(rz, o);
+      if constexpr (MSE) lc[r] = buf_ld4(rc, o);
     }
   };
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
@@ -482,6 +490,11 @@ gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw,
         const float v = ld[r][k] * sx;
         hi[k] = (_Float16)v;
         lo[k] = (_Float16)(v - (float)hi[k]);
+        if constexpr (MSE) {  // out-of-range pixels read 0 on both sides: no contribution
+          const float d = ld[r][k] - lc[r][k], dr = fmaxf(ld[r][k], 0.f) - fmaxf(lc[r][k], 0.f);
+          ms += d * d;
+          msr += dr * dr;
+        }
       }
       *reinterpret_cast<f16x4*>(pl + ch * HP + px) = hi;
       *reinterpret_cast<f16x4*>(pl + (C + ch) * HP + px) = lo;
@@ -508,6 +521,16 @@ gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw,
         acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[q], 0, 0, 0);
         acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[q], 0, 0, 0);
       }
+    }
+  }
+  if constexpr (MSE) {
+    __shared__ float mred[4];
+    ms = block_sum<256>(ms, mred);
+    msr = block_sum<256>(msr, mred);
+    if (tid == 0) {
+      const int blk = b * nsplit + split;
+      mparts[2 * blk] = ms;
+      mparts[2 * blk + 1] = msr;
     }
   }
   // partials in the 64 x 64-tile layout [b][tile][split][64][64]
@@ -707,10 +730,20 @@ static size_t gram_ws_bytes(int b, int c, int hw) {
   return off + ((size_t)nparts + 64) * sizeof(float);
 }
 
+// content / feature MSE companion of a style loss (stx_style_content_loss)
+struct MseCompanion {
+  const float* content;  // [b][c][hw], the content target
+  float* out;            // [3]: content mse, feature loss, feature mse (stx_mse mode 2)
+  float* parts;          // 2 floats per block
+  size_t parts_bytes;
+};
+
+int mse2_finalize_launch(const float* parts, int nparts, double n, float* out, hipStream_t st);
+
 static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_out,
                     const float* target, long long t_bstride, float* coef, float cA, float alpha, float* loss,
                     float loss_inv, const float* z_amax, void* ws, size_t ws_bytes,
-                    hipStream_t st) {
+                    hipStream_t st, const MseCompanion* mse = nullptr) {
   if (b <= 0 || c <= 0 || hw <= 0 || !z) {
     set_error("gram: invalid dims");
     return STX_E_INVALID;
@@ -732,7 +765,13 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
     nsplit = gram_tri_splits(c, hw, b);
     split_len = rup(cdiv(hw, nsplit), 64);
     nsplit = cdiv(hw, split_len);
-    if (c == 128)
+    if (c == 128 && mse && (reinterpret_cast<uintptr_t>(mse->content) & 15) == 0 &&
+        mse->parts_bytes >= (size_t)2 * b * nsplit * sizeof(float)) {
+      hipLaunchKernelGGL((gram_tri_f16_kernel<128, true>), dim3(nsplit, 1, b), dim3(256), 0, st,
+                         z, slabs, hw, nsplit, split_len, z_amax, mse->content, mse->parts);
+      mse2_finalize_launch(mse->parts, b * nsplit, (double)b * c * hw, mse->out, st);
+      mse = nullptr;  // done
+    } else if (c == 128)
       hipLaunchKernelGGL(gram_tri_f16_kernel<128>, dim3(nsplit, 1, b), dim3(256), 0, st, z, slabs,
                          hw, nsplit, split_len, z_amax);
     else
@@ -757,6 +796,11 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
   if (target && loss)
     hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, parts, b * ntu * FSUB,
                        loss_inv, loss);
+  if (mse) {  // not fused (another Gram kernel ran): the separate content pass
+    const int rc = stx_mse(z, mse->content, (long long)b * c * hw, 0, 2, mse->out, nullptr, 1.f,
+                           mse->parts, mse->parts_bytes, st);
+    if (rc) return rc;
+  }
   return check_launch("gram");
 }
 
@@ -841,6 +885,45 @@ extern "C" int stx_style_loss(const float* z, const float* target, float* g_out,
   }
   return gram_run(z, b, c, hw, scale, g_out, target, target_batched ? (long long)c * c : 0, coef, cA, diag_alpha, loss,
                   (float)(1.0 / ((double)b * c * c)), z_amax, ws, ws_bytes, st);
+}
+
+static size_t style_content_parts_bytes(int b, int c, int hw) {
+  const size_t fused = (size_t)2 * b * gram_tri_splits(c, hw, b) * sizeof(float);
+  return std::max(fused, stx_mse_ws((long long)b * c * hw));
+}
+
+extern "C" size_t stx_style_content_ws(int b, int c, int hw) {
+  return rup((long long)gram_ws_bytes(b, c, hw), 256) + style_content_parts_bytes(b, c, hw);
+}
+
+extern "C" int stx_style_content_loss(const float* z, const float* target, float* coef,
+                                      float* loss, int b, int c, int hw, int target_batched,
+                                      float weight, float diag_alpha, const float* z_amax,
+                                      const float* content, float* mse_out, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  if (!target || !content || !mse_out) {
+    set_error("stx_style_content_loss: target, content and mse_out are required");
+    return STX_E_INVALID;
+  }
+  if (!ws || ws_bytes < stx_style_content_ws(b, c, hw)) {
+    set_error("stx_style_content_loss: workspace too small");
+    return STX_E_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const double n = (double)c * hw;
+  const float scale = (float)(1.0 / n);
+  const float cA = (float)(weight * 4.0 / ((double)b * c * c * n));
+  const int cpad = stx_gram_coef_pitch(c);
+  if (coef && cpad != c) {
+    const long long cnt = (long long)b * cpad * cpad;
+    hipLaunchKernelGGL(zero_kernel, dim3((int)std::min<long long>((cnt + 255) / 256, 2048)),
+                       dim3(256), 0, st, coef, cnt);
+  }
+  const size_t gb = rup((long long)gram_ws_bytes(b, c, hw), 256);
+  MseCompanion m{content, mse_out, (float*)((char*)ws + gb), ws_bytes - gb};
+  return gram_run(z, b, c, hw, scale, nullptr, target, target_batched ? (long long)c * c : 0,
+                  coef, cA, diag_alpha, loss, (float)(1.0 / ((double)b * c * c)), z_amax, ws, gb,
+                  st, &m);
 }
 
 extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const float* target,

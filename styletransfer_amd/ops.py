@@ -536,6 +536,36 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
     return loss, (coef if want_coef else None)
 
 
+def style_content_loss(z, target, content, mse_out, weight=1.0, diag_alpha=0.0, coef=None,
+                       z_amax=None, defer_ws=None):
+    """style_loss(z, target, ..., defer_ws=...) and mse(z, content, mode=2, out=mse_out) in
+    one pass over z where the Gram kernel allows it.  defer_ws >= stx_style_content_ws.
+    Returns (deferred LossPart, coef)."""
+    _req(z, "z")
+    _req(target, "target")
+    _req(content, "content")
+    assert content.numel() == z.numel() and mse_out.numel() >= 3
+    b, c = z.shape[:2]
+    hw = z[0, 0].numel()
+    tb = target.numel() == b * c * c and b > 1
+    if not tb and target.numel() != c * c:
+        raise ValueError(f"style target {tuple(target.shape)} cannot expand to ({b},{c},{c})")
+    if coef is None:
+        cp = coef_pitch(c)
+        coef = torch.empty((b, cp, cp), device=z.device, dtype=torch.float32)
+    L = lib()
+    need = L.stx_style_content_ws(b, c, hw)
+    assert defer_ws is not None and defer_ws.numel() >= need, need
+    wp, wn = defer_ws.data_ptr(), defer_ws.numel()
+    check(L.stx_style_content_loss(z.data_ptr(), target.data_ptr(), coef.data_ptr(), None, b, c,
+                                   hw, int(tb), float(weight), float(diag_alpha), _p(z_amax),
+                                   content.data_ptr(), mse_out.data_ptr(), wp, wn, _stream()),
+          "stx_style_content_loss")
+    npart = C.c_int()
+    off = L.stx_style_loss_parts(b, c, hw, C.byref(npart))
+    return (wp + off, npart.value, 1.0 / (b * c * c)), coef
+
+
 def style_loss_from_parts(gparts, nparts, b, c, hw, target, weight=1.0, diag_alpha=0.0,
                           coef=None, defer_ws=None):
     """style_loss from the fused Gram partials a conv wrote (conv2d(gram_part=...)):

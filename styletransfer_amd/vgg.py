@@ -241,6 +241,8 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         elif st.grams[l] is None or st.grams[l].numel() != B * nt * 4096:
             st.grams[l] = torch.empty(B * nt * 4096, device=dev, dtype=torch.float32)
 
+    fuse_content = os.environ.get("STX_CONTENT_FUSE", "1") != "0"
+
     def on_layer(l, z):
         # the style loss of layer l (and the content/feature losses at conv2_2) run on
         # the side stream while the next conv runs: memory-bound reductions under
@@ -254,9 +256,17 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         with torch.cuda.stream(side):
             i = STYLE_CONVS.index(l)
             b_, c_ = z.shape[:2]
-            need = N.lib().stx_gram_ws(b_, c_, z[0, 0].numel())
+            fuse_mse = l == CONTENT_CONV and st.grams[l] is None and split and fuse_content
+            L = N.lib()
+            need = (L.stx_style_content_ws if fuse_mse else L.stx_gram_ws)(b_, c_,
+                                                                             z[0, 0].numel())
             if st.lws[i] is None or st.lws[i].numel() < need:
                 st.lws[i] = torch.empty(need, device=dev, dtype=torch.uint8)
+            if fuse_mse:  # style loss + content/feature/feature-mse in one pass over z
+                st.parts[i], st.coef[i] = ops.style_content_loss(
+                    z, targets[i], c4, st.losses[5:8], weight=sw, diag_alpha=alpha,
+                    coef=st.coef[i], z_amax=slot(st.amax, l + 1), defer_ws=st.lws[i])
+                return
             if st.grams[l] is not None:
                 st.parts[i], st.coef[i] = ops.style_loss_from_parts(
                     st.grams[l], st.grams[l].numel() // (b_ * 4096), b_, c_, z[0, 0].numel(),

@@ -274,6 +274,37 @@ def test_fused_gram_partials(dev, case):
     assert rel(a_f, a32) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(1, 128, 256, 256), (2, 128, 24, 40), (1, 64, 32, 32),
+                                   (1, 256, 16, 16), (3, 128, 8, 12)])
+def test_style_content_loss(dev, shape):
+    """stx_style_content_loss (the content tap: the style loss with the content, feature
+    and feature-mse sums in the same pass over z where the Gram kernel allows it)
+    equals style_loss + mse(mode=2) run separately."""
+    b, c, h, w = shape
+    z = rnd(b, c, h, w, dev=dev, seed=51, scale=2, shift=-1)
+    cz = rnd(b, c, h, w, dev=dev, seed=52, scale=2, shift=-1)
+    t = rnd(c, c, dev=dev, seed=53, scale=0.02)
+    am = ops.amax(z)
+    ws = torch.empty(N.lib().stx_style_content_ws(b, c, h * w), device=dev, dtype=torch.uint8)
+    m = torch.full((3,), float("nan"), device=dev)
+    lp, a_f = ops.style_content_loss(z, t, cz, m, weight=3.0, diag_alpha=0.5, z_amax=am,
+                                     defer_ws=ws)
+    lf = torch.zeros(1, device=dev)
+    ops.loss_finalize([lp], lf)
+    ws2 = torch.empty(N.lib().stx_gram_ws(b, c, h * w), device=dev, dtype=torch.uint8)
+    lp2, a2 = ops.style_loss(z, t, weight=3.0, diag_alpha=0.5, z_amax=am, defer_ws=ws2)
+    l2 = torch.zeros(1, device=dev)
+    ops.loss_finalize([lp2], l2)
+    m2 = ops.mse(z, cz, mode=2)
+    assert torch.equal(lf, l2) and torch.equal(a_f, a2)
+    assert rel(m, m2) < 1e-6, (m, m2)
+    zd, cd = z.double().cpu(), cz.double().cpu()
+    ref0 = ((zd - cd) ** 2).mean()
+    mr = ((zd.clamp(min=0) - cd.clamp(min=0)) ** 2).mean()
+    ref = torch.stack([ref0, mr * mr / z.numel(), mr])
+    assert rel(m, ref) < 1e-5, (m, ref)
+
+
 @pytest.mark.parametrize("shape", [(2, 64, 20, 70), (1, 128, 34, 64), (1, 256, 16, 16),
                                    (1, 64, 9, 13), (1, 64, 128, 256), (3, 128, 32, 96),
                                    (2, 64, 2, 32), (2, 256, 32, 48)])
