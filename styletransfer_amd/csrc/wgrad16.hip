@@ -23,6 +23,9 @@
 // input pixels 2*x0 .. 2*x0+15 (four float4) plus 2*x0-1 and takes the even ones
 // (kw = 1) and the odd ones shifted by zero / one (kw = 0 / 2) as packed pairs.
 #include "common.h"
+
+#include <mutex>
+#include <unordered_map>
 #include "../../include/stx.h"
 
 namespace stx {
@@ -43,6 +46,14 @@ struct Wg16 {
   int lds;  // wgrad16_lds_kernel geometry (cout 64/128, 64-cin tiles, 1 block per CU)
 };
 
+// Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one L2): renumber
+// them so that consecutive logical blocks -- the units of one K split, which read the
+// same dY rows -- sit on one XCD.  A bijection on [0, nb).
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  const int per = nb >> 3, rem = nb & 7, x = b & 7, k = b >> 3;
+  return x * per + min(x, rem) + k;
+}
+
 constexpr int WG16_S2 = 16;  // private mode: stride 2, pad 1, raw input (h = 2 hv, w = 2 wv)
 
 template <int PF, bool S2, bool CI2 = false>
@@ -51,7 +62,7 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
                const float* __restrict__ x_amax, const float* __restrict__ dy_amax, Wg16 g) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, l32 = lane & 31;
-  int unit = blockIdx.x * 4 + wave;
+  int unit = xcd_block(blockIdx.x, gridDim.x) * 4 + wave;
   const int cit = unit % g.ncit;
   unit /= g.ncit;
   const int cot = unit % g.ncot;  // pair of 32-cout tiles (64 couts)
@@ -440,7 +451,7 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   __shared__ __attribute__((aligned(16))) char vimg[2][3 * 2 * 2 * CIB * 16];  // 2 x 12|24 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
-  int unit = blockIdx.x;
+  int unit = xcd_block(blockIdx.x, gridDim.x);
   const int cit = unit % g.ncit;           // CIB-cin tile
   unit /= g.ncit;
   const int kh = unit % 3;
@@ -627,6 +638,66 @@ static bool lds_on_64() {
   return on;
 }
 
+typedef void (*Wg16Kernel)(const float*, const float*, float*, const float*, const float*, Wg16);
+
+static int wg16_pf() {
+  static const int pf = [] {
+    const char* e = getenv("STX_WG16_PF");
+    return e ? atoi(e) : 4;
+  }();
+  return pf;
+}
+
+// the kernel a planned geometry launches (g.lds / g.ci2 / mode / cout / cin set)
+static Wg16Kernel wg16_kernel(const Wg16& g) {
+  if (g.lds) {
+    const bool up = g.mode == STX_IN_UPSAMPLE2;
+    static const int lpf = [] {
+      const char* e = getenv("STX_WG16_LPF");
+      return e ? atoi(e) : 3;
+    }();
+    if (g.cout == 128)
+      return up ? wgrad16_lds_kernel<4, true, 3>
+                : (lpf >= 7 ? wgrad16_lds_kernel<4, false, 7>
+                            : (lpf >= 5 ? wgrad16_lds_kernel<4, false, 5>
+                                        : wgrad16_lds_kernel<4, false, 3>));
+    if (g.cin % 128 == 0)
+      return up ? wgrad16_lds_kernel<2, true, 3, 128> : wgrad16_lds_kernel<2, false, 3, 128>;
+    return up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>;
+  }
+  if (g.ci2) return wgrad16_kernel<4, false, true>;
+  if (g.mode == WG16_S2) return wgrad16_kernel<4, true>;
+  const int pf = wg16_pf();
+  return pf >= 12 ? wgrad16_kernel<12, false>
+                  : (pf >= 8 ? wgrad16_kernel<8, false> : wgrad16_kernel<4, false>);
+}
+
+// resident blocks of `k` over the whole device (CUs x blocks per CU at 256 threads);
+// 256 x 1 when no device answers (the CPU-only build host sizing a workspace)
+static int wg16_slots_query(Wg16Kernel k) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k), 256,
+                                                   0) != hipSuccess ||
+      cus <= 0 || per <= 0) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  return cus * per;
+}
+
+static int wg16_slots(Wg16Kernel k) {  // cached per kernel (plans run at every launch)
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(reinterpret_cast<const void*>(k));
+  if (it != cache.end()) return it->second;
+  const int v = wg16_slots_query(k);
+  cache.emplace(reinterpret_cast<const void*>(k), v);
+  return v;
+}
+
 static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg16& g) {
   if (wv % 16 != 0 || cin < 16 || cout < 16 || n <= 0 || hv <= 0) return false;
   // 32-bit buffer offsets over the whole dy / x tensors
@@ -665,25 +736,17 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
     g.cout32 = cout;
     g.cin32 = cin;
     g.ci2 = 0;
-    static const int lblocks = [] {
-      const char* e = getenv("STX_WG16_LBLOCKS");  // 512 measured 10 % faster than 256 / 128
-      return e ? atoi(e) : 512;
-    }();
-    int ns = cdiv(lblocks, 3 * g.ncit);
-    ns = std::max(1, std::min(ns, cdiv(g.steps, 8)));
-    g.steps_per_split = cdiv(g.steps, ns);
-    g.nsplit = cdiv(g.steps, g.steps_per_split);
-    return true;
   }
-  const int units = 3 * g.ncot * g.ncit;
-  static const int target = [] {
-    const char* e = getenv("STX_WG16_WAVES");
-    return e ? atoi(e) : 2048;
+  // K splits: as many as fill whole rounds of resident blocks (a ragged last round of a
+  // few blocks costs a full block duration: 513 blocks at 256 slots ran 3 rounds)
+  static const int rounds = [] {
+    const char* e = getenv("STX_WG16_ROUNDS");
+    return e ? std::max(1, atoi(e)) : 1;
   }();
-  // ~2048 waves (one per SIMD pair at this kernel's 1 wave/SIMD; measured 8 % faster
-  // than 1024 on the ITN residual convs despite the larger split-K slab)
-  int ns = cdiv(target, units);
-  ns = std::max(1, std::min(ns, cdiv(g.steps, 8)));  // >= 8 steps per wave
+  const int slots = rounds * wg16_slots(wg16_kernel(g));
+  // blocks per split: (kh x cin tiles) for the LDS kernel; 4 units (waves) per block
+  int ns = g.lds ? slots / (3 * g.ncit) : slots * 4 / (3 * g.ncot * g.ncit);
+  ns = std::max(1, std::min(ns, cdiv(g.steps, 8)));  // >= 8 steps per split
   g.steps_per_split = cdiv(g.steps, ns);
   g.nsplit = cdiv(g.steps, g.steps_per_split);
   return true;
@@ -727,49 +790,16 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
   }
   hipStream_t st = (hipStream_t)stream;
   const int units = g.nsplit * 3 * g.ncot * g.ncit;
-  static const int pf = [] {
-    const char* e = getenv("STX_WG16_PF");
-    return e ? atoi(e) : 4;
-  }();
-  if (g.lds) {
-    const int blocks = g.nsplit * 3 * g.ncit;
-    const bool up = in_mode == STX_IN_UPSAMPLE2;
-    static const int lpf = [] {
-      const char* e = getenv("STX_WG16_LPF");
-      return e ? atoi(e) : 3;
-    }();
-    auto kern = cout == 128
-        ? (up ? wgrad16_lds_kernel<4, true, 3>
-              : (lpf >= 7 ? wgrad16_lds_kernel<4, false, 7>
-                          : (lpf >= 5 ? wgrad16_lds_kernel<4, false, 5>
-                                      : wgrad16_lds_kernel<4, false, 3>)))
-        : (cin % 128 == 0
-               ? (up ? wgrad16_lds_kernel<2, true, 3, 128> : wgrad16_lds_kernel<2, false, 3, 128>)
-               : (up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>));
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, x, dy, (float*)ws, x_amax, dy_amax,
-                       g);
-  } else if (g.ci2)
-    hipLaunchKernelGGL((wgrad16_kernel<4, false, true>), dim3(cdiv(units, 4)), dim3(256), 0, st,
-                       x, dy, (float*)ws, x_amax, dy_amax, g);
-  else if (g.mode == WG16_S2)
-    hipLaunchKernelGGL((wgrad16_kernel<4, true>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
-                       (float*)ws, x_amax, dy_amax, g);
-  else if (pf >= 12)
-    hipLaunchKernelGGL((wgrad16_kernel<12, false>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
-                       (float*)ws, x_amax, dy_amax, g);
-  else if (pf >= 8)
-    hipLaunchKernelGGL((wgrad16_kernel<8, false>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
-                       (float*)ws, x_amax, dy_amax, g);
-  else
-    hipLaunchKernelGGL((wgrad16_kernel<4, false>), dim3(cdiv(units, 4)), dim3(256), 0, st, x, dy,
-                       (float*)ws, x_amax, dy_amax, g);
+  const int blocks = g.lds ? g.nsplit * 3 * g.ncit : cdiv(units, 4);
+  hipLaunchKernelGGL(wg16_kernel(g), dim3(blocks), dim3(256), 0, st, x, dy, (float*)ws, x_amax,
+                     dy_amax, g);
   const long long total = (long long)cout * cin * 9;
-  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-  if (blocks < 512 && g.nsplit >= 32)
+  const int rblocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  if (rblocks < 512 && g.nsplit >= 32)
     hipLaunchKernelGGL(wgrad16_reduce4_kernel, dim3((int)((total + 63) / 64)), dim3(256), 0, st,
                        (const float*)ws, dw, g, accumulate);
   else
-    hipLaunchKernelGGL(wgrad16_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)ws,
+    hipLaunchKernelGGL(wgrad16_reduce_kernel, dim3(rblocks), dim3(256), 0, st, (const float*)ws,
                        dw, g, accumulate);
   return check_launch("stx_conv2d_wgrad16");
 }
