@@ -552,6 +552,7 @@ int conv2d_f16x3(const stx_conv_params& p, hipStream_t st);  // conv16.hip
 int conv2d_fewin(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
 int fewin_gram_tiles(const stx_conv_params& p);              // convfew.hip
 int conv2d_fewout(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
+int conv2d_conv9(const stx_conv_params& p, hipStream_t st);   // conv9.hip (-1: not covered)
 
 }  // namespace stx
 
@@ -710,7 +711,9 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
       const char* e = getenv("STX_FEWIN");
       return e && atoi(e) == 0;
     }();
-    int rc = few_off ? -1 : conv2d_fewin(p, st);
+    int rc = few_off ? -1 : conv2d_conv9(p, st);  // the ITN's 9x9 layers, split MFMA
+    if (rc >= 0) return rc;
+    rc = few_off ? -1 : conv2d_fewin(p, st);
     if (rc >= 0) return rc;
     rc = few_off ? -1 : conv2d_fewout(p, st);
     if (rc >= 0) return rc;
