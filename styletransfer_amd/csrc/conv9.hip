@@ -21,11 +21,14 @@
 //   halo; the output is the kw-shifted sum y[co][r][x] = sum_kw P[(co, kw)][r][x + kw]
 //   formed from LDS after the MFMAs.  64 input columns give 56 output columns.
 //
-// Scales are block-local (max|x| over the block's input window, max|W| over the
-// weights it stages), so no producer annotates the input and each block's outputs
-// depend only on its window; the de-scale 2^(ex + ew - 30) is exact.  Weights come
-// from the fp32 k-major slab (stx_conv_weight_prep: row (ci, kh, kw), column co; the
-// data-gradient slab is already transposed and flipped).
+// Both run persistent: one 8-wave block per CU stages the split weights once and walks
+// its tiles with the next tile's (or chunk's) input loads in flight during the current
+// MFMAs.  The input scale is per tile for 3 -> 32 (the tile's window max: no producer
+// annotates the image or the loss-network gradient) and the producer's max|x| bound
+// (p.in_amax, an InstanceNorm output) for 32 -> 3; the weight scale is max|W|.  Each
+// tile's outputs depend only on its window, and the de-scale 2^(ex + ew - 30) is exact.
+// Weights come from the fp32 k-major slab (stx_conv_weight_prep: row (ci, kh, kw),
+// column co; the data-gradient slab is already transposed and flipped).
 #include <stdlib.h>
 
 #include "common.h"
@@ -37,6 +40,8 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
+constexpr int NWV = 8, NT = 64 * NWV;  // waves / threads per block
+
 __device__ __forceinline__ void split8(const float (&v)[8], float s, f16x8& hi, f16x8& lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -47,21 +52,25 @@ __device__ __forceinline__ void split8(const float (&v)[8], float s, f16x8& hi, 
   }
 }
 
-// block max of two values (4 waves), returned to every thread
-__device__ __forceinline__ void block_max2(float& a, float& b, float* red) {
+// block max (NWV waves), returned to every thread; red[NWV] is free again once every
+// thread has passed the next barrier
+template <int W = NWV>
+__device__ __forceinline__ float block_max(float a, float* red) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    a = fmaxf(a, __shfl_xor(a, o, 64));
-    b = fmaxf(b, __shfl_xor(b, o, 64));
-  }
-  const int tid = threadIdx.x;
-  if ((tid & 63) == 0) {
-    red[tid >> 6] = a;
-    red[4 + (tid >> 6)] = b;
-  }
+  for (int o = 32; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a;
   __syncthreads();
-  a = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  b = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+  float m = red[0];
+#pragma unroll
+  for (int i = 1; i < W; ++i) m = fmaxf(m, red[i]);
+  return m;
+}
+
+// one atomic per block into slot (block id % STX_AMAX_SLOTS) of an amax group
+template <int W = NWV>
+__device__ __forceinline__ void block_amax_out(float* group, uint32_t m_u, float* red) {
+  const float m = block_max<W>(__uint_as_float(m_u), red);
+  if (threadIdx.x == 0) atomic_max_abs(group + (blockIdx.x & (STX_AMAX_SLOTS - 1)), m);
 }
 
 __device__ __forceinline__ int exp_of(float m) {
@@ -70,306 +79,378 @@ __device__ __forceinline__ int exp_of(float m) {
   return min(max(e, -60), 60);
 }
 
-// ------------------------------------------------------------------ 3 -> 32
-// Block: 4 waves, output tile 4 rows x 64 columns (wave w: row w, two 32-pixel
-// N-blocks), all 32 output channels (one M tile).
-namespace in3 {
-constexpr int TH = 4, TW = 64, RW = TW + 8;           // unit columns per row
-constexpr int NPOS = TH * RW;                          // 288 unit positions
-constexpr int NB_ITEMS = 4 * NPOS;                     // (group, position) items
-constexpr int NB_R = (NB_ITEMS + 255) / 256;           // 5
-constexpr int NA_ITEMS = 9 * 2 * 2 * 32;               // (kw, s, h, co) items
-constexpr int LDS_B = 2 * 4 * NPOS * 16;               // [P][g][pos] units
-constexpr int LDS_A = 9 * 2 * 2 * 2 * 32 * 16;         // [kw][s][P][h][co] units
-}  // namespace in3
-
-__global__ void __launch_bounds__(256, 2) conv9_in3_kernel(stx_conv_params p, int tiles_x) {
-  using namespace in3;
-  __shared__ __attribute__((aligned(16))) char smem[LDS_B + LDS_A];
-  __shared__ float red[8];
-  char* lb = smem;
-  char* la = smem + LDS_B;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
-  const int n = blockIdx.z;
-  const int oy0 = (blockIdx.x / tiles_x) * TH, ox0 = (blockIdx.x % tiles_x) * TW;
-  const int plane_in = p.h * p.w;
-  const auto rx = make_srd(p.x + (size_t)n * 3 * plane_in, (uint32_t)(3 * plane_in) * 4u);
-  const bool relu_in = p.in_mode == STX_IN_RELU;
-
-  // B items i = tid + 256 k: position pos = i % NPOS (r, c), group g = i / NPOS
-  float bv[NB_R][8];
-  float mx = 0.f;
-#pragma unroll
-  for (int k = 0; k < NB_R; ++k) {
-    const int i = tid + 256 * k;
-    const int g = i / NPOS, pos = i - g * NPOS;
-    const int r = pos / RW, c = pos - r * RW;
-    const int x = ox0 - 4 + c;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int q = 8 * g + e;
-      const int ci = q / 9, kh = q - 9 * (q / 9);
-      const int y = oy0 + r + kh - 4;
-      const bool ok = i < NB_ITEMS && q < 27 && y >= 0 && y < p.h && x >= 0 && x < p.w;
-      float v = buf_ld(rx, ok ? (uint32_t)(ci * plane_in + y * p.w + x) * 4u : BUF_OOB);
-      if (relu_in) v = fmaxf(v, 0.f);
-      bv[k][e] = v;
-      mx = fmaxf(mx, fabsf(v));
-    }
-  }
-  // A items u = tid + 256 k: co = u % 32, h = (u / 32) % 2, s = (u / 64) % 2, kw = u / 128;
-  // element e is pair q = 16 s + 8 h + e of W[co][ci][kh][kw] = wt[(ci*81 + kh*9 + kw)][co]
-  constexpr int NAK = (NA_ITEMS + 255) / 256;  // 5 (the last round half idle)
-  float av[NAK][8];
-  float mw = 0.f;
-#pragma unroll
-  for (int k = 0; k < NAK; ++k) {
-    const int u = tid + 256 * k;
-    const int co = u & 31, hh = (u >> 5) & 1, s = (u >> 6) & 1, kw = u >> 7;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int q = 16 * s + 8 * hh + e;
-      const int ci = q / 9, kh = q - 9 * (q / 9);
-      const bool ok = u < NA_ITEMS && q < 27 && co < p.cout;
-      const int row = ok ? ci * 81 + kh * 9 + kw : 0;
-      const float v = p.wt[(size_t)row * p.cout_pad + (ok ? co : 0)];
-      av[k][e] = ok ? v : 0.f;
-      mw = fmaxf(mw, fabsf(av[k][e]));
-    }
-  }
-  block_max2(mx, mw, red);
-  const int ex = exp_of(mx), ew = exp_of(mw);
-  const float sx = __builtin_ldexpf(1.f, 15 - ex), sw = __builtin_ldexpf(1.f, 15 - ew);
-  const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
-#pragma unroll
-  for (int k = 0; k < NB_R; ++k) {
-    const int i = tid + 256 * k;
-    if (i < NB_ITEMS) {
-      f16x8 hi, lo;
-      split8(bv[k], sx, hi, lo);
-      const int g = i / NPOS, pos = i - g * NPOS;
-      *reinterpret_cast<f16x8*>(lb + ((0 * 4 + g) * NPOS + pos) * 16) = hi;
-      *reinterpret_cast<f16x8*>(lb + ((1 * 4 + g) * NPOS + pos) * 16) = lo;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NAK; ++k) {
-    const int u = tid + 256 * k;
-    if (u < NA_ITEMS) {
-      f16x8 hi, lo;
-      split8(av[k], sw, hi, lo);
-      const int co = u & 31, hh = (u >> 5) & 1, s = (u >> 6) & 1, kw = u >> 7;
-      const int base = ((kw * 2 + s) * 2) * 2;  // [kw][s][P][h]
-      *reinterpret_cast<f16x8*>(la + (((base + 0 * 2 + hh) * 32) + co) * 16) = hi;
-      *reinterpret_cast<f16x8*>(la + (((base + 1 * 2 + hh) * 32) + co) * 16) = lo;
-    }
-  }
-  __syncthreads();
-
-  f32x16 acc[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  const char* bb = lb + (wave * RW + l32) * 16;
-#pragma unroll
-  for (int kw = 0; kw < 9; ++kw)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int base = ((kw * 2 + s) * 2) * 2;
-      const f16x8 ah = *reinterpret_cast<const f16x8*>(la + ((base + h) * 32 + l32) * 16);
-      const f16x8 al = *reinterpret_cast<const f16x8*>(la + ((base + 2 + h) * 32 + l32) * 16);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int off = (32 * j + kw) * 16;
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + ((0 * 4 + 2 * s + h) * NPOS) * 16 + off);
-        const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + ((1 * 4 + 2 * s + h) * NPOS) * 16 + off);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
-      }
-    }
-
-  // epilogue: rows co = 8 (r/4) + 4h + r%4, pixel (oy0 + wave, ox0 + 32 j + l32)
-  const size_t plane = (size_t)p.ho * p.wo;
-  const uint32_t pb = (uint32_t)plane * 4u;
-  const auto ry = make_srd(p.y + (size_t)n * p.cout * plane, (uint32_t)p.cout * pb);
-  uint32_t vmax_u = 0u;
-  const int oy = oy0 + wave;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int ox = ox0 + 32 * j + l32;
-    const bool in = oy < p.ho && ox < p.wo;
-    const uint32_t vo = in ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row_c = 8 * (r >> 2) + (r & 3);
-      const int co = row_c + 4 * h;
-      float v = acc[j][r] * descale;
-      if (p.bias) v += p.bias[min(co, p.cout - 1)];
-      if (p.relu_out) v = fmaxf(v, 0.f);
-      if (co < p.cout) {
-        buf_st(ry, vo + (uint32_t)row_c * pb, v);
-        if (in) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
-      }
-    }
-  }
-  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
+// persistent tile walk: XCD x (block b -> x = b % 8) takes a contiguous run of each
+// round's tiles, so neighbouring tiles (which share halo rows) meet in one L2
+__device__ __forceinline__ int first_tile() {
+  const int g = gridDim.x;
+  if (g % 8) return blockIdx.x;
+  return (blockIdx.x % 8) * (g / 8) + blockIdx.x / 8;
 }
 
-// ------------------------------------------------------------------ 32 -> 3
-// Block: 4 waves, 4 output rows x 56 output columns (wave w: row w; its two N-blocks
-// are the 64 input columns ox0 - 4 .. ox0 + 59), input channels in chunks of 16.
-namespace out3 {
-constexpr int TH = 4, TWO = 56, TWI = 64, RH = TH + 8;
-constexpr int NPOS = RH * TWI;                     // 768 halo positions
-constexpr int NB_ITEMS = 2 * NPOS;                 // (channel group, position)
-constexpr int NB_R = NB_ITEMS / 256;               // 6
-constexpr int NA_ITEMS = 9 * 2 * 32;               // (kh, h, m)
-constexpr int LDS_B = 2 * NB_ITEMS * 16;           // [P][cg][row][col]
-constexpr int LDS_A = 9 * 2 * 2 * 32 * 16;         // [kh][P][h][m]
-constexpr int PST = TWI + 1;                       // P row stride (floats)
-static_assert(NB_ITEMS % 256 == 0, "halo items per thread");
-static_assert(4 * 32 * PST * 4 <= LDS_B + LDS_A, "P planes fit");
-}  // namespace out3
+// ------------------------------------------------------------------ 3 -> 32
+// Tile: 8 output rows x 64 columns (wave w: row w, two 32-pixel N-blocks), all
+// output channels <= 32 (one M tile).
+// W waves per block (8: one block per CU; 4: two, so one block's staging overlaps the
+// other's MFMAs)
+template <int W>
+struct In3 {
+  static constexpr int NT = 64 * W;
+  static constexpr int TH = W, TW = 64, RW = TW + 8;    // unit columns per row
+  static constexpr int NPOS = TH * RW;                  // unit positions
+  static constexpr int NB_ITEMS = 4 * NPOS;             // (pair group, position) units
+  static constexpr int NB_R = (NB_ITEMS + NT - 1) / NT; // 5 (the last round partly idle)
+  static constexpr int NA_ITEMS = 9 * 2 * 2 * 32;      // (kw, s, h, co) units
+  static constexpr int NA_R = (NA_ITEMS + NT - 1) / NT;
+  static constexpr int LDS_B = 2 * 4 * NPOS * 16;      // [P][g][pos]
+  static constexpr int LDS_A = 9 * 2 * 2 * 2 * 32 * 16; // [kw][s][P][h][co]
+};
 
-__global__ void __launch_bounds__(256, 2) conv9_out3_kernel(stx_conv_params p, int tiles_x) {
-  using namespace out3;
+// DBG (profiling only, STX_CONV9_DBG): bit 0 skips the epilogue stores, bit 1 the MFMAs,
+// bit 2 the next tile's input loads
+template <int DBG = 0, int W = NWV>
+__global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_params p, int tiles_x,
+                                                                  int tiles_y) {
+  using C = In3<W>;
+  constexpr int NT = C::NT, TH = C::TH, TW = C::TW, RW = C::RW, NPOS = C::NPOS;
+  constexpr int NB_ITEMS = C::NB_ITEMS, NB_R = C::NB_R, NA_ITEMS = C::NA_ITEMS, NA_R = C::NA_R;
+  constexpr int LDS_B = C::LDS_B, LDS_A = C::LDS_A;
   __shared__ __attribute__((aligned(16))) char smem[LDS_B + LDS_A];
-  __shared__ float red[8];
+  __shared__ float red[W];
   char* lb = smem;
   char* la = smem + LDS_B;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
-  const int n = blockIdx.z;
-  const int oy0 = (blockIdx.x / tiles_x) * TH, ox0 = (blockIdx.x % tiles_x) * TWO;
+  const int tiles_img = tiles_x * tiles_y, ntiles = tiles_img * p.n;
   const int plane_in = p.h * p.w;
-  const auto rx = make_srd(p.x + (size_t)n * p.cin * plane_in, (uint32_t)(p.cin * plane_in) * 4u);
   const bool relu_in = p.in_mode == STX_IN_RELU;
-  const int nchunks = cdiv(p.cin, 16);
 
-  // halo item i = tid + 256 k -> channel group cg = i / NPOS, position (row, col)
-  uint32_t hoff[NB_R];
-#pragma unroll
-  for (int k = 0; k < NB_R; ++k) {
-    const int i = tid + 256 * k;
-    const int cg = i / NPOS, pos = i - cg * NPOS;
-    const int rr = pos / TWI, cc = pos - rr * TWI;
-    const int y = oy0 - 4 + rr, x = ox0 - 4 + cc;
-    const bool ok = y >= 0 && y < p.h && x >= 0 && x < p.w;
-    hoff[k] = ok ? (uint32_t)(8 * cg * plane_in + y * p.w + x) * 4u : BUF_OOB;
-  }
-  auto ld_halo = [&](int c0, int k, int e) -> float {
-    const bool ok = c0 + 8 * ((tid + 256 * k) / NPOS) + e < p.cin && hoff[k] != BUF_OOB;
-    float v = buf_ld(rx, ok ? hoff[k] + (uint32_t)((c0 + e) * plane_in) * 4u : BUF_OOB);
-    return relu_in ? fmaxf(v, 0.f) : v;
-  };
-  // weight item u = tid + 256 k -> (kh, h, m): m = co * 9 + kw, element e = channel
-  // c0 + 8 h + e: W[co][ci][kh][kw] = wt[(ci*81 + kh*9 + kw)][co]
-  auto ld_w = [&](int c0, int k, int e) -> float {
-    const int u = tid + 256 * k;
-    const int m = u & 31, hh = (u >> 5) & 1, kh = u >> 6;
-    const int co = m / 9, kw = m - 9 * (m / 9), ci = c0 + 8 * hh + e;
-    const bool ok = u < NA_ITEMS && co < p.cout && ci < p.cin;
-    const float v = p.wt[(size_t)(ok ? ci * 81 + kh * 9 + kw : 0) * p.cout_pad + (ok ? co : 0)];
-    return ok ? v : 0.f;
-  };
-  // block-local maxima over the whole window and all weights (a read-only first pass)
-  float mx = 0.f, mw = 0.f;
-  for (int c = 0; c < nchunks; ++c) {
-#pragma unroll
-    for (int k = 0; k < NB_R; ++k)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) mx = fmaxf(mx, fabsf(ld_halo(16 * c, k, e)));
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) mw = fmaxf(mw, fabsf(ld_w(16 * c, k, e)));
-  }
-  block_max2(mx, mw, red);
-  const int ex = exp_of(mx), ew = exp_of(mw);
-  const float sx = __builtin_ldexpf(1.f, 15 - ex), sw = __builtin_ldexpf(1.f, 15 - ew);
-  const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
-
-  f32x16 acc[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  const char* bb = lb + (wave * TWI + l32) * 16;  // (row wave + kh, column 32 j + l32)
-  for (int c = 0; c < nchunks; ++c) {
-    const int c0 = 16 * c;
-    float hv[NB_R][8], wv[3][8];
-#pragma unroll
-    for (int k = 0; k < NB_R; ++k)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) hv[k][e] = ld_halo(c0, k, e);
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) wv[k][e] = ld_w(c0, k, e);
-    __syncthreads();  // the previous chunk's operand reads are done
+  // B unit i = tid + NT k: position pos = i % NPOS (r, c), pair group g = i / NPOS
+  float bv[NB_R][8];
+  auto load_b = [&](int tile) {
+    const int n = tile / tiles_img, t = tile - n * tiles_img;
+    const int oy0 = (t / tiles_x) * TH, ox0 = (t % tiles_x) * TW;
+    const auto rx = make_srd(p.x + (size_t)n * 3 * plane_in, (uint32_t)(3 * plane_in) * 4u);
 #pragma unroll
     for (int k = 0; k < NB_R; ++k) {
-      f16x8 hi, lo;
-      split8(hv[k], sx, hi, lo);
-      const int i = tid + 256 * k;
-      *reinterpret_cast<f16x8*>(lb + i * 16) = hi;
-      *reinterpret_cast<f16x8*>(lb + (NB_ITEMS + i) * 16) = lo;
-    }
+      const int i = tid + NT * k;
+      const int g = i / NPOS, pos = i - g * NPOS;
+      const int r = pos / RW, c = pos - r * RW;
+      const int x = ox0 - 4 + c;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int u = tid + 256 * k;
+      for (int e = 0; e < 8; ++e) {
+        const int q = 8 * g + e;
+        const int ci = q / 9, kh = q - 9 * (q / 9);
+        const int y = oy0 + r + kh - 4;
+        const bool ok = i < NB_ITEMS && q < 27 && y >= 0 && y < p.h && x >= 0 && x < p.w;
+        bv[k][e] = buf_ld(rx, ok ? (uint32_t)(ci * plane_in + y * p.w + x) * 4u : BUF_OOB);
+      }
+    }
+  };
+  int tile = first_tile();
+  if (!(DBG & 16) && tile < ntiles) load_b(tile);
+
+  // weights, once: unit u = tid + NT k -> co = u % 32, h = (u / 32) % 2, s = (u / 64) % 2,
+  // kw = u / 128; element e is pair q = 16 s + 8 h + e of W[co][ci][kh][kw]
+  int ew;
+  {
+    float av[NA_R][8];
+    float mw = 0.f;
+#pragma unroll
+    for (int k = 0; k < NA_R; ++k) {
+      const int u = tid + NT * k;
+      const int co = u & 31, hh = (u >> 5) & 1, s = (u >> 6) & 1, kw = u >> 7;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int q = 16 * s + 8 * hh + e;
+        const int ci = q / 9, kh = q - 9 * (q / 9);
+        const bool ok = u < NA_ITEMS && q < 27 && co < p.cout;
+        const float v = p.wt[(size_t)(ok ? ci * 81 + kh * 9 + kw : 0) * p.cout_pad + (ok ? co : 0)];
+        av[k][e] = ok ? v : 0.f;
+        mw = fmaxf(mw, fabsf(av[k][e]));
+      }
+    }
+    ew = exp_of(block_max<W>(mw, red));
+    const float sw = __builtin_ldexpf(1.f, 15 - ew);
+#pragma unroll
+    for (int k = 0; k < NA_R; ++k) {
+      const int u = tid + NT * k;
       if (u < NA_ITEMS) {
         f16x8 hi, lo;
-        split8(wv[k], sw, hi, lo);
-        const int m = u & 31, hh = (u >> 5) & 1, kh = u >> 6;
-        *reinterpret_cast<f16x8*>(la + (((kh * 2 + 0) * 2 + hh) * 32 + m) * 16) = hi;
-        *reinterpret_cast<f16x8*>(la + (((kh * 2 + 1) * 2 + hh) * 32 + m) * 16) = lo;
+        split8(av[k], sw, hi, lo);
+        const int co = u & 31, hh = (u >> 5) & 1, s = (u >> 6) & 1, kw = u >> 7;
+        const int base = ((kw * 2 + s) * 2) * 2;  // [kw][s][P][h]
+        *reinterpret_cast<f16x8*>(la + ((base + 0 * 2 + hh) * 32 + co) * 16) = hi;
+        *reinterpret_cast<f16x8*>(la + ((base + 1 * 2 + hh) * 32 + co) * 16) = lo;
+      }
+    }
+    __syncthreads();  // red[] is reused by the first tile's window max
+  }
+  if (DBG & 8) {  // profiling: the prologue alone
+    if (bv[0][0] == 1234.5f && threadIdx.x == 0) p.y[0] = 0.f;
+    return;
+  }
+
+  const size_t plane = (size_t)p.ho * p.wo;
+  const uint32_t pb = (uint32_t)plane * 4u;
+  float bias_r[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int co = 8 * (r >> 2) + 4 * h + (r & 3);
+    bias_r[r] = (p.bias && co < p.cout) ? p.bias[co] : 0.f;
+  }
+  uint32_t vmax_u = 0u;
+  const char* bb = lb + (wave * RW + l32) * 16;
+  for (; tile < ntiles; tile += gridDim.x) {
+    // this tile's window max (the barrier inside also retires the last tile's B reads)
+    float mx = 0.f;
+#pragma unroll
+    for (int k = 0; k < NB_R; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (relu_in) bv[k][e] = fmaxf(bv[k][e], 0.f);
+        mx = fmaxf(mx, fabsf(bv[k][e]));
+      }
+    const int ex = exp_of(block_max<W>(mx, red));
+    const float sx = __builtin_ldexpf(1.f, 15 - ex);
+    const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
+#pragma unroll
+    for (int k = 0; k < NB_R; ++k) {
+      const int i = tid + NT * k;
+      if (i < NB_ITEMS) {
+        f16x8 hi, lo;
+        split8(bv[k], sx, hi, lo);
+        *reinterpret_cast<f16x8*>(lb + i * 16) = hi;  // [P][g][pos]: i = g * NPOS + pos
+        *reinterpret_cast<f16x8*>(lb + (NB_ITEMS + i) * 16) = lo;
       }
     }
     __syncthreads();
+    const int cur = tile;
+    if (!(DBG & 4) && tile + (int)gridDim.x < ntiles) load_b(tile + gridDim.x);  // in flight during the MFMAs
+
+    f32x16 acc[2];
 #pragma unroll
-    for (int kh = 0; kh < 9; ++kh) {
-      const f16x8 ah = *reinterpret_cast<const f16x8*>(la + (((kh * 2 + 0) * 2 + h) * 32 + l32) * 16);
-      const f16x8 al = *reinterpret_cast<const f16x8*>(la + (((kh * 2 + 1) * 2 + h) * 32 + l32) * 16);
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int off = ((h * NPOS) + kh * TWI + 32 * j) * 16;
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + off);
-        const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + NB_ITEMS * 16 + off);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+#pragma unroll
+    for (int kw = 0; kw < ((DBG & 2) ? 1 : 9); ++kw)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int base = ((kw * 2 + s) * 2) * 2;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(la + ((base + h) * 32 + l32) * 16);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(la + ((base + 2 + h) * 32 + l32) * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int off = ((2 * s + h) * NPOS + 32 * j + kw) * 16;
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + off);
+          const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + NB_ITEMS * 16 + off);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
+        }
+      }
+
+    // rows co = 8 (r/4) + 4h + r%4, pixel (oy0 + wave, ox0 + 32 j + l32)
+    const int n = cur / tiles_img, t = cur - n * tiles_img;
+    const int oy = (t / tiles_x) * TH + wave, ox0 = (t % tiles_x) * TW;
+    const auto ry = make_srd(p.y + (size_t)n * p.cout * plane, (uint32_t)p.cout * pb);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ox = ox0 + 32 * j + l32;
+      const bool in = oy < p.ho && ox < p.wo;
+      const uint32_t vo = in ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row_c = 8 * (r >> 2) + (r & 3);
+        float v = fmaf(acc[j][r], descale, bias_r[r]);
+        if (p.relu_out) v = fmaxf(v, 0.f);
+        if (row_c + 4 * h < p.cout && (!(DBG & 1) || v == 1234.5f)) {
+          buf_st(ry, vo + (uint32_t)row_c * pb, v);
+          if (in) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
+        }
       }
     }
   }
-  // P[(co, kw)][column] of this wave's row to LDS, then y[co][x] = sum_kw P[co*9+kw][x+kw]
-  __syncthreads();
-  float* pw = reinterpret_cast<float*>(smem) + wave * 32 * PST;
+  if (p.out_amax) block_amax_out<W>(p.out_amax, vmax_u, red);
+}
+
+// ------------------------------------------------------------------ 32 -> 3
+// Tile: 8 output rows x 56 output columns (wave w: row w; its two N-blocks are the 64
+// input columns ox0 - 4 .. ox0 + 59); input channels in chunks of 16 (cin <= 32: the
+// split weights of every chunk stay in LDS).
+namespace out3 {
+constexpr int TH = NWV, TWO = 56, TWI = 64, RH = TH + 8;
+constexpr int NPOS = RH * TWI;                     // 1024 halo positions
+constexpr int NB_ITEMS = 2 * NPOS;                 // (channel group, position) units
+constexpr int NB_R = NB_ITEMS / NT;                // 4
+constexpr int NA_ITEMS = 9 * 2 * 32;               // (kh, h, m) units per chunk
+constexpr int NA_R = (2 * NA_ITEMS + NT - 1) / NT; // both chunks: 3 rounds
+constexpr int LDS_B = 2 * NB_ITEMS * 16;           // [P][cg][row][col]
+constexpr int LDS_A = 2 * 9 * 2 * 2 * 32 * 16;     // [chunk][kh][P][h][m]
+constexpr int PST = TWI + 1;                       // P row stride (floats)
+static_assert(NB_ITEMS % NT == 0, "halo units per thread");
+static_assert(NWV * 27 * PST * 4 <= LDS_B, "P rows fit in the halo region");
+}  // namespace out3
+
+template <int DBG = 0>
+__global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, int tiles_x,
+                                                           int tiles_y) {
+  using namespace out3;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_B + LDS_A];
+  __shared__ float red[NWV];
+  char* lb = smem;
+  char* la = smem + LDS_B;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int tiles_img = tiles_x * tiles_y, ntiles = tiles_img * p.n;
+  const int plane_in = p.h * p.w;
+  const bool relu_in = p.in_mode == STX_IN_RELU;
+  const int nch = cdiv(p.cin, 16);  // 1 or 2
+
+  // halo unit i = tid + NT k -> channel group cg = i / NPOS, position (row, col)
+  uint32_t hpos[NB_R];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int k = 0; k < NB_R; ++k) {
+    const int i = tid + NT * k;
+    const int cg = i / NPOS, pos = i - cg * NPOS;
+    const int rr = pos / TWI, cc = pos - rr * TWI;
+    hpos[k] = (uint32_t)(cg << 20 | rr << 10 | cc);
+  }
+  float hv[NB_R][8];
+  auto load_h = [&](int tile, int c) {
+    const int n = tile / tiles_img, t = tile - n * tiles_img;
+    const int oy0 = (t / tiles_x) * TH, ox0 = (t % tiles_x) * TWO;
+    const auto rx = make_srd(p.x + (size_t)n * p.cin * plane_in, (uint32_t)(p.cin * plane_in) * 4u);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) pw[(8 * (r >> 2) + 4 * h + (r & 3)) * PST + 32 * j + l32] = acc[j][r] * descale;
-  __syncthreads();
-  const size_t plane = (size_t)p.ho * p.wo;
-  const int oy = oy0 + wave;
-  uint32_t vmax_u = 0u;
-  for (int idx = lane; idx < p.cout * TWO; idx += 64) {
-    const int co = idx / TWO, x = idx - co * TWO;
-    float v = 0.f;
+    for (int k = 0; k < NB_R; ++k) {
+      const int cg = hpos[k] >> 20, rr = (hpos[k] >> 10) & 1023, cc = hpos[k] & 1023;
+      const int y = oy0 - 4 + rr, x = ox0 - 4 + cc, ch = 16 * c + 8 * cg;
+      const bool ok = y >= 0 && y < p.h && x >= 0 && x < p.w;
+      const uint32_t o = (uint32_t)(ch * plane_in + y * p.w + x) * 4u;
 #pragma unroll
-    for (int kw = 0; kw < 9; ++kw) v += pw[(co * 9 + kw) * PST + x + kw];
-    const int ox = ox0 + x;
-    if (oy < p.ho && ox < p.wo) {
-      const size_t o = ((size_t)n * p.cout + co) * plane + (size_t)oy * p.wo + ox;
-      if (p.bias) v += p.bias[co];
-      if (p.accumulate) v += p.y[o];
-      if (p.relu_out) v = fmaxf(v, 0.f);
-      p.y[o] = v;
-      vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
+      for (int e = 0; e < 8; ++e)
+        hv[k][e] = buf_ld(rx, (ok && ch + e < p.cin) ? o + (uint32_t)(e * plane_in) * 4u : BUF_OOB);
+    }
+  };
+  int tile = first_tile();
+  if (!(DBG & 16) && tile < ntiles) load_h(tile, 0);
+
+  // weights of every chunk, once: unit u = tid + NT k -> chunk c = u / NA_ITEMS, (kh, h, m):
+  // m = co * 9 + kw, element e = channel 16 c + 8 h + e: W[co][ci][kh][kw] = wt[(ci*81 + kh*9 + kw)][co]
+  const float sx = __builtin_ldexpf(1.f, 15 - exp_of(read_amax(p.in_amax)));
+  float descale;
+  {
+    float wv[NA_R][8];
+    float mw = 0.f;
+#pragma unroll
+    for (int k = 0; k < NA_R; ++k) {
+      const int u = tid + NT * k;
+      const int c = u / NA_ITEMS, v = u - c * NA_ITEMS;
+      const int m = v & 31, hh = (v >> 5) & 1, kh = v >> 6;
+      const int co = m / 9, kw = m - 9 * (m / 9);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ci = 16 * c + 8 * hh + e;
+        const bool ok = c < nch && co < p.cout && ci < p.cin;
+        const float w = p.wt[(size_t)(ok ? ci * 81 + kh * 9 + kw : 0) * p.cout_pad + (ok ? co : 0)];
+        wv[k][e] = ok ? w : 0.f;
+        mw = fmaxf(mw, fabsf(wv[k][e]));
+      }
+    }
+    const int ew = exp_of(block_max(mw, red));
+    const float sw = __builtin_ldexpf(1.f, 15 - ew);
+    descale = __builtin_ldexpf(1.f, exp_of(read_amax(p.in_amax)) + ew - 30);
+#pragma unroll
+    for (int k = 0; k < NA_R; ++k) {
+      const int u = tid + NT * k;
+      if (u < 2 * NA_ITEMS) {
+        f16x8 hi, lo;
+        split8(wv[k], sw, hi, lo);
+        const int c = u / NA_ITEMS, v = u - c * NA_ITEMS;
+        const int m = v & 31, hh = (v >> 5) & 1, kh = v >> 6;
+        *reinterpret_cast<f16x8*>(la + ((((c * 9 + kh) * 2 + 0) * 2 + hh) * 32 + m) * 16) = hi;
+        *reinterpret_cast<f16x8*>(la + ((((c * 9 + kh) * 2 + 1) * 2 + hh) * 32 + m) * 16) = lo;
+      }
     }
   }
-  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
+
+  if (DBG & 8) {  // profiling: the prologue alone
+    __syncthreads();
+    if (hv[0][0] == 1234.5f && threadIdx.x == 0) p.y[0] = 0.f;
+    return;
+  }
+  const size_t plane = (size_t)p.ho * p.wo;
+  uint32_t vmax_u = 0u;
+  const char* bb = lb + (wave * TWI + l32) * 16;  // (row wave + kh, column 32 j + l32)
+  float* pw = reinterpret_cast<float*>(smem) + wave * 27 * PST;
+  for (; tile < ntiles; tile += gridDim.x) {
+    f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      __syncthreads();  // the previous chunk's operand reads / P reads are done
+#pragma unroll
+      for (int k = 0; k < NB_R; ++k) {
+        if (relu_in)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hv[k][e] = fmaxf(hv[k][e], 0.f);
+        f16x8 hi, lo;
+        split8(hv[k], sx, hi, lo);
+        const int i = tid + NT * k;
+        *reinterpret_cast<f16x8*>(lb + i * 16) = hi;
+        *reinterpret_cast<f16x8*>(lb + (NB_ITEMS + i) * 16) = lo;
+      }
+      __syncthreads();
+      // the next chunk (or the next tile's first) in flight during the MFMAs
+      if (DBG & 4) {
+      } else if (c + 1 < nch) load_h(tile, c + 1);
+      else if (tile + (int)gridDim.x < ntiles) load_h(tile + gridDim.x, 0);
+      const char* ac = la + c * 9 * 2 * 2 * 32 * 16;
+#pragma unroll
+      for (int kh = 0; kh < ((DBG & 2) ? 1 : 9); ++kh) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(ac + (((kh * 2 + 0) * 2 + h) * 32 + l32) * 16);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(ac + (((kh * 2 + 1) * 2 + h) * 32 + l32) * 16);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int off = ((h * NPOS) + kh * TWI + 32 * j) * 16;
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + off);
+          const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + NB_ITEMS * 16 + off);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
+        }
+      }
+    }
+    // P[(co, kw)][column] of this wave's row into LDS (rows < 27), then
+    // y[co][x] = sum_kw P[co*9 + kw][x + kw]
+    __syncthreads();  // every wave's halo reads are done
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = 8 * (r >> 2) + 4 * h + (r & 3);
+        if (m < 27) pw[m * PST + 32 * j + l32] = acc[j][r] * descale;
+      }
+    __syncthreads();
+    const int n = tile / tiles_img, t = tile - n * tiles_img;
+    const int oy = (t / tiles_x) * TH + wave, ox0 = (t % tiles_x) * TWO;
+    for (int idx = lane; idx < p.cout * TWO; idx += 64) {
+      const int co = idx / TWO, x = idx - co * TWO;
+      float v = 0.f;
+#pragma unroll
+      for (int kw = 0; kw < 9; ++kw) v += pw[(co * 9 + kw) * PST + x + kw];
+      const int ox = ox0 + x;
+      if (oy < p.ho && ox < p.wo && (!(DBG & 1) || v == 1234.5f)) {
+        const size_t o = ((size_t)n * p.cout + co) * plane + (size_t)oy * p.wo + ox;
+        if (p.bias) v += p.bias[co];
+        if (p.accumulate) v += p.y[o];
+        if (p.relu_out) v = fmaxf(v, 0.f);
+        p.y[o] = v;
+        vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
+      }
+    }
+  }
+  if (p.out_amax) block_amax_out(p.out_amax, vmax_u, red);
 }
 
 bool conv9_on() {
@@ -380,11 +461,48 @@ bool conv9_on() {
   return on;
 }
 
+int dbg9() {
+  static const int m = [] {
+    const char* e = getenv("STX_CONV9_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
+#define CONV9_LAUNCH(KERN, grid, st, p, tx, ty)                                            \
+  switch (dbg9()) {                                                                        \
+    case 1: hipLaunchKernelGGL(KERN<1>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
+    case 2: hipLaunchKernelGGL(KERN<2>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
+    case 3: hipLaunchKernelGGL(KERN<3>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
+    case 4: hipLaunchKernelGGL(KERN<4>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
+    case 7: hipLaunchKernelGGL(KERN<7>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
+    case 8: hipLaunchKernelGGL(KERN<8>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
+    case 24: hipLaunchKernelGGL(KERN<24>, grid, dim3(NT), 0, st, p, tx, ty); break;        \
+    default: hipLaunchKernelGGL(KERN<0>, grid, dim3(NT), 0, st, p, tx, ty); break;         \
+  }
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+int persistent_grid(int ntiles, int per_cu) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  static const int over = env_int("STX_CONV9_GRID", 0);  // profiling override
+  return std::min(ntiles, over > 0 ? over : per_cu * cus);  // LDS-limited blocks per CU
+}
+
 }  // namespace
 
-// 9x9 stride 1 pad 4, 3 -> 32 or 32 -> 3 (any cin <= 3 / cout <= 3 side of those
-// shapes), raw or ReLU input, fp32 slab (wt); bias / relu_out / out_amax (and
-// accumulate for 32 -> 3) epilogues.  Returns -1 when not covered.
+// 9x9 stride 1 pad 4, 3 -> <= 32 channels, or <= 32 -> <= 3 channels with a max|x|
+// bound (p.in_amax), raw or ReLU input, fp32 slab (wt); bias / relu_out / out_amax
+// (and accumulate for the 3-output shape) epilogues.  Returns -1 when not covered.
 int conv2d_conv9(const stx_conv_params& p, hipStream_t st) {
   const bool base = p.ks == 9 && p.stride == 1 && p.pad == 4 && p.wt &&
                     (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) && !p.mask && !p.aux &&
@@ -392,15 +510,20 @@ int conv2d_conv9(const stx_conv_params& p, hipStream_t st) {
                     p.wt_batch_stride == 0 && p.hv == p.h && p.wv == p.w && conv9_on();
   if (!base) return -1;
   if (p.cin == 3 && p.cout >= 1 && p.cout <= 32 && !p.accumulate) {
-    const int tiles_x = cdiv(p.wo, in3::TW), tiles_y = cdiv(p.ho, in3::TH);
-    hipLaunchKernelGGL(conv9_in3_kernel, dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0, st, p,
-                       tiles_x);
+    static const int w4 = env_int("STX_CONV9_W4", 0);
+    if (w4) {  // 4-wave blocks, two per CU
+      const int tx = cdiv(p.wo, In3<4>::TW), ty = cdiv(p.ho, In3<4>::TH);
+      hipLaunchKernelGGL((conv9_in3_kernel<0, 4>), dim3(persistent_grid(tx * ty * p.n, 2)),
+                         dim3(256), 0, st, p, tx, ty);
+    } else {
+      const int tx = cdiv(p.wo, In3<8>::TW), ty = cdiv(p.ho, In3<8>::TH);
+      CONV9_LAUNCH(conv9_in3_kernel, dim3(persistent_grid(tx * ty * p.n, 1)), st, p, tx, ty);
+    }
     return check_launch("stx_conv2d(conv9 3->32)");
   }
-  if (p.cout >= 1 && p.cout <= 3 && p.cin >= 1 && p.cin <= 64) {
-    const int tiles_x = cdiv(p.wo, out3::TWO), tiles_y = cdiv(p.ho, out3::TH);
-    hipLaunchKernelGGL(conv9_out3_kernel, dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0, st, p,
-                       tiles_x);
+  if (p.cout >= 1 && p.cout <= 3 && p.cin >= 1 && p.cin <= 32 && p.in_amax) {
+    const int tx = cdiv(p.wo, out3::TWO), ty = cdiv(p.ho, out3::TH);
+    CONV9_LAUNCH(conv9_out3_kernel, dim3(persistent_grid(tx * ty * p.n, 1)), st, p, tx, ty);
     return check_launch("stx_conv2d(conv9 32->3)");
   }
   return -1;

@@ -52,8 +52,12 @@ def test_conv9_out3_fwd(dev, case):
     b = rnd(cout, dev=dev, seed=3)
     wt = ops.conv_weight_prep(wgt)
     am = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
-    y = ops.conv2d(x, wt, cin, cout, 9, in_mode=mode, bias=b, out_amax=am)
+    # the split kernel takes the producer's max|x| bound (an exact one, then a loose one)
+    y = ops.conv2d(x, wt, cin, cout, 9, in_mode=mode, bias=b, out_amax=am, in_amax=ops.amax(x))
     ref = ref_conv(x, wgt, b, relu_in)
+    y_loose = ops.conv2d(x, wt, cin, cout, 9, in_mode=mode, bias=b,
+                         in_amax=ops.amax(x) * 37.0)
+    assert rel(y_loose, ref) < TOL64
     torch.cuda.synchronize()
     assert y.shape == ref.shape
     assert rel(y, ref) < TOL64
@@ -61,7 +65,7 @@ def test_conv9_out3_fwd(dev, case):
     old = rnd(n, cout, h, w, dev=dev, seed=4)
     out = old.clone()
     ops.conv2d(x, wt, cin, cout, 9, in_mode=mode, bias=b, out=out, accumulate=True,
-               relu_out=True)
+               relu_out=True, in_amax=ops.amax(x))
     assert rel(out, F.relu(ref + old.double().cpu())) < TOL64
 
 
