@@ -79,10 +79,13 @@ class Conv2dFn(torch.autograd.Function):
             wt = ops.conv_weight_prep(w.detach().contiguous())
             if stride == 2 and _split_on() and w.requires_grad:
                 x_amax = ops.ARENA.lookup(x)  # for the split stride-2 wgrad (None: computed there)
-        if ks == 9 and cout <= 3:
-            # conv22 (32 -> 3): the split 9x9 kernel takes the producer's max|x| bound
-            # (the InstanceNorm output's amax group; without one the VALU kernel runs)
+        if ks == 9 and cout <= 3 and cin <= 32:
+            # conv22 (32 -> 3): the split 9x9 kernel takes a max|x| bound -- the producing
+            # InstanceNorm's amax group inside the trainers (ops.ARENA), else computed here
+            # (the same exact max either way, so both paths give the same bits)
             x_amax = ops.ARENA.lookup(x)
+            if x_amax is None:
+                x_amax = ops.amax(x)
         y = ops.conv2d(x, wt, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
                        bias=None if b is None else b.detach(), wt16=wt16 if split else None,
                        in_amax=x_amax)

@@ -90,8 +90,7 @@ __device__ __forceinline__ int first_tile() {
 // ------------------------------------------------------------------ 3 -> 32
 // Tile: 8 output rows x 64 columns (wave w: row w, two 32-pixel N-blocks), all
 // output channels <= 32 (one M tile).
-// W waves per block (8: one block per CU; 4: two, so one block's staging overlaps the
-// other's MFMAs)
+// W waves per block (8: one block per CU, LDS-limited)
 template <int W>
 struct In3 {
   static constexpr int NT = 64 * W;
@@ -263,10 +262,12 @@ __global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_param
         const int row_c = 8 * (r >> 2) + (r & 3);
         float v = fmaf(acc[j][r], descale, bias_r[r]);
         if (p.relu_out) v = fmaxf(v, 0.f);
-        if (row_c + 4 * h < p.cout && (!(DBG & 1) || v == 1234.5f)) {
-          buf_st(ry, vo + (uint32_t)row_c * pb, v);
-          if (in) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
-        }
+        // branch-free: channels past cout store out of range (a store inside a branch
+        // leaves the compiler unsure how many are pending, so the next tile's wait for
+        // its prefetched loads becomes a wait for every store too)
+        const bool ok = row_c + 4 * h < p.cout;
+        if constexpr (!(DBG & 1)) buf_st(ry, ok ? vo + (uint32_t)row_c * pb : BUF_OOB, v);
+        vmax_u = max(vmax_u, (in && ok) ? (__float_as_uint(v) & 0x7fffffffu) : 0u);
       }
     }
   }
@@ -434,20 +435,24 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
     __syncthreads();
     const int n = tile / tiles_img, t = tile - n * tiles_img;
     const int oy = (t / tiles_x) * TH + wave, ox0 = (t % tiles_x) * TWO;
-    for (int idx = lane; idx < p.cout * TWO; idx += 64) {
-      const int co = idx / TWO, x = idx - co * TWO;
+    // branch-free stores through a descriptor (see conv9_in3's epilogue): 3 x 64 lanes
+    // cover the 3 x 56 outputs, the rest store out of range
+    const auto ry = make_srd(p.y + (size_t)n * p.cout * plane, (uint32_t)(p.cout * plane) * 4u);
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int idx = lane + 64 * it;
+      const int co = idx / TWO, x = idx - co * TWO, coc = min(co, p.cout - 1);
       float v = 0.f;
 #pragma unroll
-      for (int kw = 0; kw < 9; ++kw) v += pw[(co * 9 + kw) * PST + x + kw];
+      for (int kw = 0; kw < 9; ++kw) v += pw[(coc * 9 + kw) * PST + x + kw];
       const int ox = ox0 + x;
-      if (oy < p.ho && ox < p.wo && (!(DBG & 1) || v == 1234.5f)) {
-        const size_t o = ((size_t)n * p.cout + co) * plane + (size_t)oy * p.wo + ox;
-        if (p.bias) v += p.bias[co];
-        if (p.accumulate) v += p.y[o];
-        if (p.relu_out) v = fmaxf(v, 0.f);
-        p.y[o] = v;
-        vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
-      }
+      const bool ok = co < p.cout && oy < p.ho && ox < p.wo;
+      const uint32_t o = ok ? (uint32_t)((size_t)co * plane + (size_t)oy * p.wo + ox) * 4u : BUF_OOB;
+      if (p.bias) v += p.bias[coc];
+      if (p.accumulate) v += buf_ld(ry, o);
+      if (p.relu_out) v = fmaxf(v, 0.f);
+      if constexpr (!(DBG & 1)) buf_st(ry, o, v);
+      vmax_u = max(vmax_u, ok ? (__float_as_uint(v) & 0x7fffffffu) : 0u);
     }
   }
   if (p.out_amax) block_amax_out(p.out_amax, vmax_u, red);
@@ -510,15 +515,9 @@ int conv2d_conv9(const stx_conv_params& p, hipStream_t st) {
                     p.wt_batch_stride == 0 && p.hv == p.h && p.wv == p.w && conv9_on();
   if (!base) return -1;
   if (p.cin == 3 && p.cout >= 1 && p.cout <= 32 && !p.accumulate) {
-    static const int w4 = env_int("STX_CONV9_W4", 0);
-    if (w4) {  // 4-wave blocks, two per CU
-      const int tx = cdiv(p.wo, In3<4>::TW), ty = cdiv(p.ho, In3<4>::TH);
-      hipLaunchKernelGGL((conv9_in3_kernel<0, 4>), dim3(persistent_grid(tx * ty * p.n, 2)),
-                         dim3(256), 0, st, p, tx, ty);
-    } else {
-      const int tx = cdiv(p.wo, In3<8>::TW), ty = cdiv(p.ho, In3<8>::TH);
-      CONV9_LAUNCH(conv9_in3_kernel, dim3(persistent_grid(tx * ty * p.n, 1)), st, p, tx, ty);
-    }
+    // (4-wave blocks, two per CU, measured the same: 58.5 vs 58.2 us at B8 256^2)
+    const int tx = cdiv(p.wo, In3<8>::TW), ty = cdiv(p.ho, In3<8>::TH);
+    CONV9_LAUNCH(conv9_in3_kernel, dim3(persistent_grid(tx * ty * p.n, 1)), st, p, tx, ty);
     return check_launch("stx_conv2d(conv9 3->32)");
   }
   if (p.cout >= 1 && p.cout <= 3 && p.cin >= 1 && p.cin <= 32 && p.in_amax) {
