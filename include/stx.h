@@ -327,6 +327,12 @@ int stx_relu_bwd(const float* dy, const float* y, float* dx, long long n, void* 
 size_t stx_adam_ws(void);
 int stx_adam_step(float* p, const float* g, float* m, float* v, long long n, float lr,
                   float beta1, float beta2, float eps, int* step_dev, void* ws, void* stream);
+/* the same, and zeroes clear[0 .. clear_n) in the step-counter launch (the Gatys
+ * engine's per-iteration amax groups, which are next produced by the following
+ * iteration's forward): one launch fewer per iteration than a separate fill. */
+int stx_adam_step_clear(float* p, const float* g, float* m, float* v, long long n, float lr,
+                        float beta1, float beta2, float eps, int* step_dev, void* ws,
+                        float* clear, int clear_n, void* stream);
 
 /* InstanceNorm2d(affine) forward, per (n,c) plane over hw (biased var, eps):
  *   u = x (+ res);  y = (u-mean)*rstd*gamma + beta;  y = max(y,0) if relu.

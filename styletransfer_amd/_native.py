@@ -125,6 +125,7 @@ SIGNATURES = {
     "stx_relu_bwd": (i32, [vp, vp, vp, i64, vp]),
     "stx_adam_ws": (sz, []),
     "stx_adam_step": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp, vp]),
+    "stx_adam_step_clear": (i32, [vp, vp, vp, vp, i64, f32, f32, f32, f32, vp, vp, vp, i32, vp]),
     "stx_instnorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp, vp]),
     "stx_instnorm_bwd_ws": (sz, [i32, i32]),
     "stx_instnorm_param_grads": (i32, [C.POINTER(PGradJob), i32, vp]),

@@ -595,13 +595,20 @@ __global__ void __launch_bounds__(256, 2) conv_fewout16_kernel(stx_conv_params p
       if (row < 27) dt[(row * FO_RH + r) * FO_RWP + c0 + l32] = acc[q] * descale;
     }
   };
-  float b0[KST][8], b1[KST][8];
-  load_item(wave, b0);
-  for (int it = wave; it < NITEM; it += 8) {
-    if (it + 4 < NITEM) load_item(it + 4, b1);
-    run_item(it, b0);
-    if (it + 8 < NITEM) load_item(it + 8, b0);
-    if (it + 4 < NITEM) run_item(it + 4, b1);
+  // items wave, wave + 4, ... through a ring of three register buffers: two items'
+  // loads stay in flight behind the one being multiplied (12 MFMAs per item hide far
+  // less than one load round trip).  The loads are unconditional (a clamped item past
+  // the end re-reads the last one): a load skipped in a branch would leave the
+  // compiler unsure how many are pending, and every wait would become vmcnt(0).
+  constexpr int NK = (NITEM + 3) / 4;
+  float bf[3][KST][8];
+  load_item(min(wave, NITEM - 1), bf[0]);
+  load_item(min(wave + 4, NITEM - 1), bf[1]);
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int it = wave + 4 * k;
+    if (k + 2 < NK) load_item(min(it + 8, NITEM - 1), bf[(k + 2) % 3]);
+    if (it < NITEM) run_item(it, bf[k % 3]);
   }
   __syncthreads();
   const int ox = ox0 + (tid & 63), g = tid >> 6;

@@ -572,47 +572,52 @@ static bool gram_tri_on(int c, int hw) {
   return on && (c == 128 || (all && c == 256)) && hw % 64 == 0;
 }
 
-// grid (ntu * 16, B); one thread per tile element (256 elements per block).  The
-// split partials are summed in a fixed order (bit-reproducible); loads are
-// independent and unrolled so a block streams its slab column at full rate.
-// 16 tile elements x 16 split-lanes per block: each split-lane sums every 16th
-// partial (4 loads in flight), the 16 lane sums are combined through LDS in a
-// fixed order, so the result is bit-reproducible and a C=64 tile's 512 partials
-// are read by 256 blocks instead of 16.
-constexpr int FEL = 16, FKL = 16;
+// grid (ntu * FSUB, B), 1024 threads: 64 tile elements (16 lanes x float4, one 256-B
+// row segment of every partial) x 64 split-lanes.  Split-lane kl sums partials kl,
+// kl + 64, ... (four float4 accumulators, so each lane keeps several loads in flight);
+// the 64 lane sums of an element are added through LDS in split-lane order, so the
+// result is bit-reproducible.  (16-element x 16-lane blocks reading 64-B segments
+// left the reduction latency-bound: 11.8 us for the 16.8 MB of C=64 @ 512^2 partials.)
+constexpr int FEL = 64, FKL = 64, FNT = FEL / 4 * FKL;  // elements, split-lanes, threads
 constexpr int FSUB = GT * GT / FEL;   // blocks per tile
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(FNT)
 gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scale,
                      float* __restrict__ g_out, const float* __restrict__ target, long long t_bstride,
                      float* __restrict__ coef, int cpad, float cA, float alpha,
                      float* __restrict__ loss_parts) {
   __shared__ float part[FKL][FEL + 1];
-  __shared__ float red[4];
+  __shared__ float red[FNT / 64];
   const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
   const int tile = blockIdx.x / FSUB, sub = blockIdx.x % FSUB;
   int I, J;
   tile_ij(tile, nt, I, J);
   const int b = blockIdx.y;
-  const float* src = ws + ((size_t)b * ntu + tile) * nsplit * (GT * GT);
-  const int el = threadIdx.x % FEL, kl = threadIdx.x / FEL;
-  const int e = sub * FEL + el;
+  const float* src = ws + ((size_t)b * ntu + tile) * nsplit * (GT * GT) + sub * FEL;
+  const int q4 = threadIdx.x % (FEL / 4), kl = threadIdx.x / (FEL / 4);
   {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+    const f32x4* p4 = reinterpret_cast<const f32x4*>(src) + q4;
+    constexpr int ST = GT * GT / 4;  // float4s per partial
     int k = kl;
     for (; k + 3 * FKL < nsplit; k += 4 * FKL) {
-      s0 += src[(size_t)(k + 0 * FKL) * GT * GT + e];
-      s1 += src[(size_t)(k + 1 * FKL) * GT * GT + e];
-      s2 += src[(size_t)(k + 2 * FKL) * GT * GT + e];
-      s3 += src[(size_t)(k + 3 * FKL) * GT * GT + e];
+      const f32x4 a0 = p4[(size_t)(k + 0 * FKL) * ST], a1 = p4[(size_t)(k + 1 * FKL) * ST];
+      const f32x4 a2 = p4[(size_t)(k + 2 * FKL) * ST], a3 = p4[(size_t)(k + 3 * FKL) * ST];
+      s0 += a0;
+      s1 += a1;
+      s2 += a2;
+      s3 += a3;
     }
-    for (; k < nsplit; k += FKL) s0 += src[(size_t)k * GT * GT + e];
-    part[kl][el] = (s0 + s1) + (s2 + s3);
+    for (; k < nsplit; k += FKL) s0 += p4[(size_t)k * ST];
+    const f32x4 t = (s0 + s1) + (s2 + s3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[kl][4 * q4 + i] = t[i];
   }
   __syncthreads();
   float sq = 0.f;
-  if (kl == 0) {
+  if (threadIdx.x < FEL) {
+    const int el = threadIdx.x, e = sub * FEL + el;
     float s = 0.f;
-#pragma unroll
+#pragma unroll 8
     for (int q = 0; q < FKL; ++q) s += part[q][el];
     const int gi = I * GT + e / GT, gj = J * GT + e % GT;
     if (gi < c && gj < c) {
@@ -634,7 +639,7 @@ gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scal
     }
   }
   if (target) {
-    const float t = block_sum<256>(sq, red);
+    const float t = block_sum<FNT>(sq, red);
     if (threadIdx.x == 0) loss_parts[(size_t)b * ntu * FSUB + blockIdx.x] = t;
   }
 }
@@ -791,7 +796,7 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
     hipLaunchKernelGGL(gram_partial_kernel, dim3(nsplit, ntu, b), dim3(256), 0, st, z, slabs, c,
                        hw, nsplit, split_len);
   const int cpad = stx_gram_coef_pitch(c);
-  hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(256), 0, st, slabs, c,
+  hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(FNT), 0, st, slabs, c,
                      nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts);
   if (target && loss)
     hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, parts, b * ntu * FSUB,
@@ -950,7 +955,7 @@ extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const 
                        dim3(256), 0, st, coef, cnt);
   }
   float* lparts = (float*)((char*)ws + gram_parts_offset(b, c, hw, nullptr));
-  hipLaunchKernelGGL(gram_finalize_kernel, dim3(FSUB, b), dim3(256), 0, st, gparts, c, nparts,
+  hipLaunchKernelGGL(gram_finalize_kernel, dim3(FSUB, b), dim3(FNT), 0, st, gparts, c, nparts,
                      (float)(1.0 / n), g_out, target,
                      target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts);
   if (loss)

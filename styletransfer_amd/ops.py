@@ -709,7 +709,18 @@ def relu_bwd(dy, y):
 
 
 # ----------------------------------------------------------------------- adam
-def adam_step(p, g, m, v, step_dev, ws, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8):
+def adam_step(p, g, m, v, step_dev, ws, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,
+              clear=None):
+    """Adam update (stx_adam_step); clear: a float32 device tensor (<= 2^31 elements)
+    zeroed in the same launch sequence (stx_adam_step_clear)."""
+    if clear is not None:
+        _req(clear, "clear")
+        check(lib().stx_adam_step_clear(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                        p.numel(), float(lr), float(beta1), float(beta2),
+                                        float(eps), step_dev.data_ptr(), ws.data_ptr(),
+                                        clear.data_ptr(), clear.numel(), _stream()),
+              "stx_adam_step_clear")
+        return
     check(lib().stx_adam_step(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(),
                               float(lr), float(beta1), float(beta2), float(eps),
                               step_dev.data_ptr(), ws.data_ptr(), _stream()), "stx_adam_step")

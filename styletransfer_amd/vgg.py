@@ -170,6 +170,7 @@ class LossState:
     folded: bool = False                        # loss weights baked into coef
     alpha: float = 0.0
     amax: torch.Tensor = None                   # [16] max|.| slots of split-conv inputs
+    amax_cleared: bool = False                  # amax already zeroed (by the engine's Adam)
     pools: list = field(default_factory=lambda: [None] * 5)  # fused relu+pool outputs
     lws: list = field(default_factory=lambda: [None] * 5)    # per-layer style-loss scratch
     parts: list = field(default_factory=lambda: [None] * 5)  # deferred loss partials
@@ -195,8 +196,9 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     dev = x.device
     if st.amax is None:
         st.amax = torch.zeros(16 * N.STX_AMAX_SLOTS, device=dev, dtype=torch.float32)
-    else:
+    elif not st.amax_cleared:
         st.amax.zero_()
+    st.amax_cleared = False  # (the Gatys engine's Adam launch clears it for the next pass)
     if st.losses is None:
         # [style x5, content, feature, feature-mse]
         st.losses = torch.empty(N_LOSSES + 1, device=dev, dtype=torch.float32)
@@ -433,8 +435,10 @@ class GatysEngine:
                      folded_weights=(self.sw, self.cw), total=self.total)
         loss_backward(self.feat, self.st, dx=self.grad, feature_grad=False,
                       scratch=self.scratch)
+        # the Adam launch also zeroes the amax groups for the next iteration's forward
         ops.adam_step(self.x, self.grad, self.m, self.v, self.step_dev, self.adam_ws, self.lr,
-                      self.betas[0], self.betas[1], self.eps)
+                      self.betas[0], self.betas[1], self.eps, clear=self.st.amax)
+        self.st.amax_cleared = True
 
     def capture(self, warmup=2):
         """Capture one iteration into a hipGraph (after `warmup` eager iterations,

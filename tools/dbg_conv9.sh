@@ -6,7 +6,7 @@ p() { tag=$1; shift; env "$@" timeout -k 5 120 rocprofv3 --kernel-trace --stats 
   python3 - gpurun_out/c9_$tag/run_kernel_stats.csv $tag <<'PY'
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
-    if "conv9" in r["Name"]:
+    if "conv9" in r["Name"] or "fewout" in r["Name"]:
         print(sys.argv[2], r["Name"][:60], r["Calls"], "avg_us", round(float(r["AverageNs"]) / 1e3, 1))
 PY
 }
