@@ -237,7 +237,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     # conv layers whose Gram partials come out of the conv epilogue (no re-read of Z)
     hs = [H, H, H // 2, H // 2, H // 4]
     for l in range(5):
-        nt = feat.gram_tiles(l, hs[l], hs[l] * W // H) if split and not overlap else 0
+        nt = feat.gram_tiles(l, hs[l], hs[l] * W // H) if split else 0
         if nt == 0:
             st.grams[l] = None
         elif st.grams[l] is None or st.grams[l].numel() != B * nt * 4096:
