@@ -448,11 +448,6 @@ static int ew_blocks(long long n) {
 using namespace stx;
 
 namespace stx {
-// mse2_finalize_kernel for another translation unit (gram.hip's fused content pass)
-int mse2_finalize_launch(const float* parts, int nparts, double n, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(mse2_finalize_kernel, dim3(1), dim3(RB), 0, st, parts, nparts, n, out);
-  return 0;
-}
 }  // namespace stx
 
 extern "C" size_t stx_mse_ws(long long n) { return (size_t)(2 * red_blocks(n) + 4) * sizeof(float); }

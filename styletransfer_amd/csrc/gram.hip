@@ -584,9 +584,27 @@ __global__ void __launch_bounds__(FNT)
 gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scale,
                      float* __restrict__ g_out, const float* __restrict__ target, long long t_bstride,
                      float* __restrict__ coef, int cpad, float cA, float alpha,
-                     float* __restrict__ loss_parts) {
+                     float* __restrict__ loss_parts, const float* __restrict__ mse_parts = nullptr,
+                     int mse_nparts = 0, double mse_n = 1.0, float* __restrict__ mse_out = nullptr) {
   __shared__ float part[FKL][FEL + 1];
   __shared__ float red[FNT / 64];
+  // block (0, 0) also finalizes the content / feature MSE partials of a fused content
+  // pass (gram_tri_f16_kernel<128, true>): the launch a separate mse2 finalize would take
+  if (mse_out && blockIdx.x == 0 && blockIdx.y == 0) {
+    float s = 0.f, sr = 0.f;
+    for (int i = threadIdx.x; i < mse_nparts; i += FNT) {
+      s += mse_parts[2 * i];
+      sr += mse_parts[2 * i + 1];
+    }
+    s = block_sum<FNT>(s, red);
+    sr = block_sum<FNT>(sr, red);
+    if (threadIdx.x == 0) {
+      const float mr = (float)(sr / mse_n);
+      mse_out[0] = (float)(s / mse_n);
+      mse_out[1] = (float)((double)(mr * mr) / mse_n);
+      mse_out[2] = mr;
+    }
+  }
   const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
   const int tile = blockIdx.x / FSUB, sub = blockIdx.x % FSUB;
   int I, J;
@@ -743,8 +761,6 @@ struct MseCompanion {
   size_t parts_bytes;
 };
 
-int mse2_finalize_launch(const float* parts, int nparts, double n, float* out, hipStream_t st);
-
 static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_out,
                     const float* target, long long t_bstride, float* coef, float cA, float alpha, float* loss,
                     float loss_inv, const float* z_amax, void* ws, size_t ws_bytes,
@@ -766,6 +782,8 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
   }
   float* slabs = (float*)ws;
   float* parts = (float*)((char*)ws + gram_parts_offset(b, c, hw, nullptr));
+  const MseCompanion* mse_fin = nullptr;
+  int mse_nparts = 0;
   if (f16 && gram_tri_on(c, hw)) {
     nsplit = gram_tri_splits(c, hw, b);
     split_len = rup(cdiv(hw, nsplit), 64);
@@ -774,7 +792,8 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
         mse->parts_bytes >= (size_t)2 * b * nsplit * sizeof(float)) {
       hipLaunchKernelGGL((gram_tri_f16_kernel<128, true>), dim3(nsplit, 1, b), dim3(256), 0, st,
                          z, slabs, hw, nsplit, split_len, z_amax, mse->content, mse->parts);
-      mse2_finalize_launch(mse->parts, b * nsplit, (double)b * c * hw, mse->out, st);
+      mse_fin = mse;  // finalized by the Gram finalize below
+      mse_nparts = b * nsplit;
       mse = nullptr;  // done
     } else if (c == 128)
       hipLaunchKernelGGL(gram_tri_f16_kernel<128>, dim3(nsplit, 1, b), dim3(256), 0, st, z, slabs,
@@ -797,7 +816,9 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
                        hw, nsplit, split_len);
   const int cpad = stx_gram_coef_pitch(c);
   hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(FNT), 0, st, slabs, c,
-                     nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts);
+                     nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts,
+                     mse_fin ? mse_fin->parts : nullptr, mse_nparts, (double)b * c * hw,
+                     mse_fin ? mse_fin->out : nullptr);
   if (target && loss)
     hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, parts, b * ntu * FSUB,
                        loss_inv, loss);
