@@ -114,6 +114,13 @@ typedef struct stx_conv_params {
    * hi/lo MFMA with a block-local power-of-two scale) to gram_part + (n * T + t) * 4096,
    * T = stx_conv_gram_tiles(p); stx_style_loss_from_parts reduces them. */
   float* gram_part;
+  /* with pool_out: pool_out = the 2x2 SUM of the output (no ReLU) and y is not written
+   * -- the backward of nearest x2 upsampling (torch.nn.Upsample(scale_factor=2), the
+   * ImageTransformNet's UpsampleConvLayer, stransfer/network.py:583-605) fused into the
+   * data-gradient conv of the upsampled conv.  Split path, stride 1, wo > 32, even
+   * ho / wo, plain epilogue only (no mask / aux / accumulate / acc_scale / up_dp / p2_z /
+   * relu_out / gram_part / out_amax). */
+  int pool_sum;
 } stx_conv_params;
 
 int stx_version(void);

@@ -36,7 +36,7 @@ class ConvParams(C.Structure):
         ("p2_z", vp), ("p2_wt", vp), ("p2_scale", vp), ("p2_c", i32), ("p2_wt_batch_stride", i64),
         ("up_dp", vp), ("up_z", vp),
         ("wt16", vp), ("w_amax", vp), ("in_amax", vp), ("out_amax", vp),
-        ("pool_out", vp), ("p2_amax", vp), ("gram_part", vp),
+        ("pool_out", vp), ("p2_amax", vp), ("gram_part", vp), ("pool_sum", i32),
     ]
 
 

@@ -19,6 +19,11 @@ def _split_on():
     return os.environ.get("STX_CONV_SPLIT", "1") != "0"
 
 
+def _upsample_fuse_on():
+    import os
+    return os.environ.get("STX_UPSAMPLE_FUSE", "1") != "0"
+
+
 def _grad_into(param, g, accumulate_fn):
     """Parameter gradients straight into an existing `param.grad` (e.g. the flat
     gradient buffer of train.FastStTrainer): `accumulate_fn(dst)` adds the gradient
@@ -125,9 +130,19 @@ class Conv2dFn(torch.autograd.Function):
                 skip = link.g if link is not None else None
                 if link is not None:
                     link.g = None
-                dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16,
-                                in_amax=dy_amax, aux=skip, aux_scale=1.0 if skip is not None
-                                else 0.0)
+                if split_d and in_mode == N.STX_IN_UPSAMPLE2 and skip is None and wv > 32 \
+                        and hv % 2 == 0 and wv % 2 == 0 and hv == 2 * h and wv == 2 * wd \
+                        and _upsample_fuse_on():
+                    # UpsampleConvLayer (stransfer/network.py:583-605): the nearest-x2
+                    # backward (2x2 sums) is fused into the data gradient's epilogue
+                    dx = torch.empty_like(x)
+                    ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16,
+                               in_amax=dy_amax, pool_out=dx, pool_sum=True)
+                    dv = None
+                else:
+                    dv = ops.conv2d(dy, wtT, cout, cin, ks, pad=ks - 1 - pad, wt16=wtT16,
+                                    in_amax=dy_amax, aux=skip, aux_scale=1.0 if skip is not None
+                                    else 0.0)
             elif stride == 2:
                 # stride-1 conv over the zero-dilated dy; the split kernel takes it too
                 if _split_on() and pad == 1 and ops.split_eligible(cout, cin, ks, 1):
@@ -143,7 +158,9 @@ class Conv2dFn(torch.autograd.Function):
                                     in_mode=N.STX_IN_DILATE2, hv=hv, wv=wv)
             else:
                 raise NotImplementedError("stride > 2")
-            if in_mode == N.STX_IN_UPSAMPLE2:
+            if dv is None:
+                pass  # dx came out of the fused epilogue
+            elif in_mode == N.STX_IN_UPSAMPLE2:
                 dx = ops.upsample2x_bwd(dv)
             elif in_mode == N.STX_IN_RELU:
                 dx = ops.relu_bwd(dv, x)

@@ -651,6 +651,15 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     set_error("stx_conv2d: unpool epilogue needs up_z");
     return STX_E_INVALID;
   }
+  if (p.pool_sum &&
+      (!p.pool_out || !p.wt16 || p.wt16 == (const void*)1 || p.ks != 3 || p.pad != 1 ||
+       p.stride != 1 || p.cin < 16 || p.cout <= 4 || p.wo <= 32 || (p.ho | p.wo) & 1 ||
+       p.mask || p.aux || p.accumulate || p.acc_scale || p.up_dp || p.p2_z || p.relu_out ||
+       p.gram_part || p.out_amax || p.wt_batch_stride)) {
+    set_error("stx_conv2d: pool_sum needs pool_out on the split path (3x3 stride 1, wo > 32, "
+              "even output dims) and the plain epilogue");
+    return STX_E_INVALID;
+  }
   if (p.gram_part && !stx_conv_gram_tiles(&p)) {
     set_error("stx_conv2d: fused Gram partials need the split path, stride 1, cout 64, "
               "wo > 32 and the plain epilogue");

@@ -192,7 +192,9 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
 
 // AUX: value += aux_scale * aux (a residual block's skip gradient, ResLink), loaded
 // through a descriptor at the store offsets
-template <int TW, int NI, bool ROWPAIR, bool RELU, int GDBG = 0, bool AUX = false>
+// POOLSUM: pool_out = 2x2 sum of the output and no y stores (stx_conv_params.pool_sum)
+template <int TW, int NI, bool ROWPAIR, bool RELU, int GDBG = 0, bool AUX = false,
+          bool POOLSUM = false>
 __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
                                                          const stx_conv_params& p,
                                                          const EpiTile& t, float scale,
@@ -243,7 +245,7 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
         float v = fmaf(acc[i][j][r], scale, bias_r[i][r]);
         if (AUX) v += p.aux_scale * buf_ld(raux, vo[j] + (uint32_t)row * pb);
         if (RELU) v = fmaxf(v, 0.f);
-        buf_st(ry, vo[j] + (uint32_t)row * pb, v);
+        if constexpr (!POOLSUM) buf_st(ry, vo[j] + (uint32_t)row * pb, v);
         acc[i][j][r] = v;  // kept for the fused pooled output
         uint32_t m = lmask[j];
         if (!rows_full) m = (row + 4 * h < rows) ? m : 0u;
@@ -270,6 +272,21 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
       const uint32_t a = (uint32_t)b & 0x7fffffffu;
       return a > 0x7f800000u ? a : (uint32_t)max(b, 0);  // NaN stays NaN (sign dropped)
     };
+    if constexpr (POOLSUM) {
+      // nearest-x2 upsampling backward: dx = (y00 + y10) + (y01 + y11) -- the window's
+      // two rows are this lane's two N-tiles, its other column is lane ^ 1 (DPP)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float s2 = acc[i][0][r] + acc[i][1][r];
+          const float sp = __int_as_float(
+              __builtin_amdgcn_mov_dpp(__float_as_int(s2), 0xB1, 0xF, 0xF, false));
+          const int row = i * 32 + (r & 3) + 8 * (r >> 2);
+          buf_st(rp, po + (uint32_t)row * ppb, s2 + sp);
+        }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -294,6 +311,11 @@ template <int TW, int NI, bool ROWPAIR, int GDBG = 0>
 __device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const stx_conv_params& p,
                                                     const EpiTile& t, float scale, char* smem) {
   if (p.mask || p.accumulate || p.acc_scale || p.up_dp || p.p2_z) return false;
+  if (p.pool_sum) {  // validated by stx_conv2d: plain epilogue, row-pair tiles
+    if constexpr (ROWPAIR)
+      conv_epilogue_plain_body<TW, NI, ROWPAIR, false, 0, false, true>(acc, p, t, scale, smem);
+    return true;
+  }
   if (p.aux) {
     if (p.relu_out || p.pool_out || p.gram_part) return false;
     conv_epilogue_plain_body<TW, NI, ROWPAIR, false, 0, true>(acc, p, t, scale, smem);

@@ -332,7 +332,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
            out=None, mask=None, aux=None, aux_scale=0.0, acc_scale=None, accumulate=False,
            relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
            p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
-           pool_out=None, p2_amax=None, split_1x1=False, gram_part=None):
+           pool_out=None, p2_amax=None, split_1x1=False, gram_part=None, pool_sum=False):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
     up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
@@ -341,7 +341,9 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
     out_amax (device scalar, zeroed by the caller) receives max|out|; pool_out
     [n][cout][ho/2][wo/2] receives maxpool2x2(relu(out)) (split path, wo > 32);
     gram_part [n * conv_gram_tiles(...) * 4096] receives the fused per-tile Gram
-    partials of out (stx_conv_params.gram_part)."""
+    partials of out (stx_conv_params.gram_part); pool_sum: pool_out receives the 2x2
+    SUM of the output instead and the full-resolution output is not written (returned:
+    pool_out) -- the nearest-x2 upsampling backward fused into a data gradient."""
     _req(x, "x")
     n, c, h, w = x.shape
     assert c == cin, (c, cin)
@@ -349,7 +351,10 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         pad = ks // 2
     hv, wv = virtual_hw(h, w, in_mode, hv, wv)
     ho, wo = conv_out_hw(hv, wv, ks, stride, pad)
-    if out is None:
+    if pool_sum:
+        assert pool_out is not None and out is None, "pool_sum writes pool_out only"
+        out = pool_out  # p.y must be set; the kernel never writes it with pool_sum
+    elif out is None:
         out = torch.empty((n, cout, ho, wo), device=x.device, dtype=torch.float32)
     else:
         _req(out, "out")
@@ -389,6 +394,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         _req(pool_out, "pool_out")
         assert pool_out.shape == (n, cout, ho // 2, wo // 2), pool_out.shape
         p.pool_out = pool_out.data_ptr()
+        p.pool_sum = int(bool(pool_sum))
     if gram_part is not None:
         _req(gram_part, "gram_part")
         nt = lib().stx_conv_gram_tiles(C.byref(p))

@@ -435,3 +435,23 @@ def test_weight_prep16_pair(dev, shape):
     b1, bm1 = ops.conv_weight_prep16(w, transpose=True)
     assert torch.equal(a, a1) and torch.equal(b, b1)
     assert float(am.max()) == float(am1.max()) == float(w.abs().max())
+
+
+@pytest.mark.parametrize("case", [(2, 64, 128, 32, 48), (1, 32, 64, 64, 64), (2, 64, 128, 17, 40)])
+def test_split_dgrad_upsample_sum(dev, case):
+    """UpsampleConvLayer backward (stransfer/network.py:583-605): the data gradient of a
+    conv over the nearest-x2 upsampled input with the 2x2 sums fused into its epilogue
+    (stx_conv_params.pool_sum) vs fp64 autograd of conv(upsample(x)), and against the
+    unfused path (full-resolution dgrad + stx_upsample2x_bwd)."""
+    n, cin, cout, h, w = case
+    x = rnd(n, cin, h, w, dev=dev, seed=31, scale=2, shift=-1).double().cpu().requires_grad_()
+    wgt = rnd(cout, cin, 3, 3, dev=dev, seed=32, scale=0.2, shift=-0.1)
+    y = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), wgt.double().cpu(), padding=1)
+    dy = rnd(*y.shape, dev=dev, seed=33, scale=2e-3, shift=-1e-3)
+    (ref,) = torch.autograd.grad(y, x, dy.double().cpu())
+    w16 = ops.conv_weight_prep16(wgt, transpose=True)
+    dx = torch.full((n, cin, h, w), 7.0, device=dev)
+    ops.conv2d(dy, None, cout, cin, 3, wt16=w16, in_amax=ops.amax(dy), pool_out=dx, pool_sum=True)
+    assert rel(dx, ref) < TOL64
+    dv = ops.conv2d(dy, None, cout, cin, 3, wt16=w16, in_amax=ops.amax(dy))
+    assert rel(dx, ops.upsample2x_bwd(dv)) < 1e-6

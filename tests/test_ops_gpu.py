@@ -205,6 +205,26 @@ def test_adam(dev):
     assert rel(p, pr.detach().to(dev)) < 1e-6
 
 
+def test_adam_step_clear(dev):
+    """stx_adam_step_clear (the Gatys engine's Adam launch that also zeroes its amax
+    groups for the next iteration): the same update bits as stx_adam_step, and the clear
+    buffer zeroed (sizes below, at and above one 256-thread pass)."""
+    for nclear in (7, 256, 512, 1000):
+        n = 4099
+        p = rnd(n, dev=dev, seed=63)
+        g = rnd(n, dev=dev, seed=64, scale=2, shift=-1)
+        st = [(p.clone(), torch.zeros_like(p), torch.zeros_like(p),
+               torch.zeros(1, dtype=torch.int32, device=dev),
+               torch.empty(16, dtype=torch.float32, device=dev)) for _ in range(2)]
+        clear = torch.full((nclear,), 3.0, device=dev)
+        for it in range(2):
+            ops.adam_step(st[0][0], g * (it + 1), *st[0][1:])
+            ops.adam_step(st[1][0], g * (it + 1), *st[1][1:], clear=clear)
+            assert float(clear.abs().max()) == 0.0
+            clear.fill_(5.0)
+        assert torch.equal(st[0][0], st[1][0]) and int(st[1][3].item()) == 2
+
+
 @pytest.mark.parametrize("relu,res,hw", [(False, False, (12, 20)), (True, False, (12, 20)),
                                          (False, True, (12, 20)), (True, True, (64, 64)),
                                          (True, False, (128, 128)), (False, True, (256, 256)),
