@@ -326,6 +326,11 @@ __global__ void upsample_bwd_kernel(const float* __restrict__ dy, float* __restr
 // summed over the whole batch.  abs'(0) = 0 (torch sign).
 __device__ __forceinline__ float sgn(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
 
+// 32-bit index math (64-bit div/mod is a long software sequence per element) and
+// branch-free neighbour loads / gradient stores through buffer descriptors: a load
+// behind `if (xx + 1 < w)` is a branch with a vmcnt(0) at its join, one round trip per
+// neighbour.  Out-of-image neighbours are selected away after the (in-range) load, so
+// the sums and gradients are the same bits as the branchy form (adding +0 is exact).
 __global__ void __launch_bounds__(RB)
 tv_kernel(const float* __restrict__ y, float* __restrict__ parts, float* __restrict__ grad,
           float gscale, const float* __restrict__ gscale_dev, long long total, int h, int w,
@@ -334,25 +339,30 @@ tv_kernel(const float* __restrict__ y, float* __restrict__ parts, float* __restr
   float gs = gscale * factor;
   if (gscale_dev) gs *= *gscale_dev;
   float sh = 0.f, sv = 0.f;
-  const long long stride = (long long)gridDim.x * RB;
-  for (long long i = blockIdx.x * (long long)RB + threadIdx.x; i < total; i += stride) {
-    const int xx = (int)(i % w);
-    const int yy = (int)((i / w) % h);
-    const float v = y[i];
+  const int n = (int)total;  // stx_tv_loss checks total < 2^29
+  const uint32_t bytes = (uint32_t)n * 4u;
+  const auto ry = make_srd(y, bytes);
+  const auto rg = make_srd(grad ? grad : y, grad ? bytes : 0u);
+  const int stride = gridDim.x * RB;
+  for (int i = blockIdx.x * RB + threadIdx.x; i < n; i += stride) {
+    const int q = i / w, xx = i - q * w;
+    const int yy = q % h;
+    const uint32_t o = (uint32_t)i * 4u;
+    const float v = buf_ld(ry, o);
+    const bool r_ok = xx + 1 < w, l_ok = xx > 0, d_ok = yy + 1 < h, u_ok = yy > 0;
+    const float vr = buf_ld(ry, r_ok ? o + 4u : o);
+    const float vl = buf_ld(ry, l_ok ? o - 4u : o);
+    const float vd = buf_ld(ry, d_ok ? o + 4u * (uint32_t)w : o);
+    const float vu = buf_ld(ry, u_ok ? o - 4u * (uint32_t)w : o);
     float g = 0.f;
-    if (xx + 1 < w) {
-      const float d = v - y[i + 1];
-      sh += fabsf(d);
-      g += sgn(d);
-    }
-    if (xx > 0) g -= sgn(y[i - 1] - v);
-    if (yy + 1 < h) {
-      const float d = v - y[i + w];
-      sv += fabsf(d);
-      g += sgn(d);
-    }
-    if (yy > 0) g -= sgn(y[i - w] - v);
-    if (grad) grad[i] = gs * g;
+    const float dr = v - vr, dd = v - vd;
+    sh += r_ok ? fabsf(dr) : 0.f;
+    g += r_ok ? sgn(dr) : 0.f;
+    g -= l_ok ? sgn(vl - v) : 0.f;
+    sv += d_ok ? fabsf(dd) : 0.f;
+    g += d_ok ? sgn(dd) : 0.f;
+    g -= u_ok ? sgn(vu - v) : 0.f;
+    buf_st(rg, o, gs * g);
   }
   sh = block_sum<RB>(sh, red);
   sv = block_sum<RB>(sv, red);
@@ -598,8 +608,8 @@ extern "C" int stx_tv_loss(const float* y, float* loss, float* grad, float gscal
                            const float* gscale_dev, int n, int c, int h, int w, float factor,
                            void* ws, size_t ws_bytes, void* stream) {
   const long long total = (long long)n * c * h * w;
-  if (total <= 0 || !y || !loss) {
-    set_error("stx_tv_loss: invalid args");
+  if (total <= 0 || !y || !loss || total >= (1ll << 29)) {
+    set_error("stx_tv_loss: invalid args (or more than 2^29 elements)");
     return STX_E_INVALID;
   }
   if (!ws || ws_bytes < stx_tv_ws(n, c, h, w)) {
