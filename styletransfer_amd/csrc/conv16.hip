@@ -600,7 +600,18 @@ template <int TW, int LM>
 static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
   const long long blocks2 = (long long)cdiv(p.wo, TW) * cdiv(p.ho, 256 / TW) *
                             cdiv(p.cout, 64) * p.n;
-  if (blocks2 < 512 && !p.pool_out && !p.p2_z && !p.gram_part) return launch16<TW, LM, 1>(p, st);
+  if (blocks2 < 512 && !p.pool_out && !p.p2_z && !p.gram_part) {
+    // 128-pixel tiles as 32 x 4 rather than 64 x 2: a 34 x 6 halo instead of 66 x 4 (23 %
+    // less staging per tile) -- Gatys NI=1 launches 37-40 -> 35-39 us, ITN residual convs
+    // 35.3 -> 34.7 us (same-box profile); STX_TW32_NI1=0 restores 64 x 2
+    static const bool tw32 = [] {
+      const char* e = getenv("STX_TW32_NI1");
+      return !(e && atoi(e) == 0);
+    }();
+    if constexpr (TW == 64)
+      if (tw32) return launch16<32, LM, 1>(p, st);
+    return launch16<TW, LM, 1>(p, st);
+  }
   return launch16<TW, LM, 2>(p, st);
 }
 
