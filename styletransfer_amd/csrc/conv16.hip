@@ -612,6 +612,19 @@ static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
       if (tw32) return launch16<32, LM, 1>(p, st);
     return launch16<TW, LM, 1>(p, st);
   }
+  // 256-pixel tiles of the transforming loaders (ReLU, nearest x2, zero-dilation) without
+  // a row-pair epilogue (no pool output / unpool / Gram / Gram-backward phase): 32 x 8
+  // (34 x 10 halo) instead of 64 x 4 (66 x 6) -- same-box profile of the fast_st step:
+  // upsampling convs 92 -> 84 and 49 -> 45 us, dilated (stride-2 dgrad) 89 -> 85 and
+  // 55 -> 52, ReLU 101 -> 98; raw-input launches measured 1 % slower and keep 64 x 4.
+  // STX_TW32_NI2=0 restores 64 x 4 everywhere.
+  static const bool tw32b = [] {
+    const char* e = getenv("STX_TW32_NI2");
+    return !(e && atoi(e) == 0);
+  }();
+  if constexpr (TW == 64 && LM != STX_IN_RAW)
+    if (tw32b && !p.pool_out && !p.gram_part && !p.p2_z && !p.up_dp)
+      return launch16<32, LM, 2>(p, st);
   return launch16<TW, LM, 2>(p, st);
 }
 
