@@ -600,7 +600,11 @@ template <int TW, int LM>
 static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
   const long long blocks2 = (long long)cdiv(p.wo, TW) * cdiv(p.ho, 256 / TW) *
                             cdiv(p.cout, 64) * p.n;
-  if (blocks2 < 512 && !p.pool_out && !p.p2_z && !p.gram_part) {
+  static const int ni1_below = [] {  // 256-pixel-tile grids smaller than this use 128-px tiles
+    const char* e = getenv("STX_NI1_BELOW");
+    return e ? atoi(e) : 512;
+  }();
+  if (blocks2 < ni1_below && !p.pool_out && !p.p2_z && !p.gram_part) {
     // 128-pixel tiles as 32 x 4 rather than 64 x 2: a 34 x 6 halo instead of 66 x 4 (23 %
     // less staging per tile) -- Gatys NI=1 launches 37-40 -> 35-39 us, ITN residual convs
     // 35.3 -> 34.7 us (same-box profile); STX_TW32_NI1=0 restores 64 x 2
