@@ -365,14 +365,15 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
 // dW[co][ci][kh][kw] (+)= sum over splits (fixed order); thread -> (tap, co, ci), ci fastest
 __global__ void wgrad16_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw,
                                       Wg16 g, int accumulate) {
-  const long long per = (long long)g.cout * g.cin;
-  const long long total = per * 9;
+  // 32-bit index math (the 64-bit div/mod is a long software sequence per element;
+  // weights are < 2^31 / 9 elements)
+  const int per = g.cout * g.cin;
+  const int total = per * 9;
   const size_t sstride = (size_t)9 * g.cout32 * g.cin32;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int tap = (int)(i / per);
-    const long long rem = i - tap * per;
-    const int co = (int)(rem / g.cin), ci = (int)(rem - (long long)co * g.cin);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int tap = i / per;
+    const int rem = i - tap * per;
+    const int co = rem / g.cin, ci = rem - co * g.cin;
     const float* src = ws + ((size_t)tap * g.cout32 + co) * g.cin32 + ci;
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int k = 0;
@@ -394,17 +395,17 @@ __global__ void __launch_bounds__(256)
 wgrad16_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg16 g,
                        int accumulate) {
   __shared__ float part[4][64];
-  const long long per = (long long)g.cout * g.cin;
-  const long long total = per * 9;
+  const int per = g.cout * g.cin;  // 32-bit index math (see wgrad16_reduce_kernel)
+  const int total = per * 9;
   const int q = threadIdx.x >> 6;
-  const long long i = blockIdx.x * 64ll + (threadIdx.x & 63);
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   float s = 0.f;
   int tap = 0, co = 0, ci = 0;
   if (i < total) {
-    tap = (int)(i / per);
-    const long long rem = i - tap * per;
-    co = (int)(rem / g.cin);
-    ci = (int)(rem - (long long)co * g.cin);
+    tap = i / per;
+    const int rem = i - tap * per;
+    co = rem / g.cin;
+    ci = rem - co * g.cin;
     const size_t sstride = (size_t)9 * g.cout32 * g.cin32;
     const float* src = ws + ((size_t)tap * g.cout32 + co) * g.cin32 + ci;
     const int quarter = (g.nsplit + 3) / 4;
@@ -702,6 +703,7 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   if (wv % 16 != 0 || cin < 16 || cout < 16 || n <= 0 || hv <= 0) return false;
   // 32-bit buffer offsets over the whole dy / x tensors
   if ((size_t)n * std::max(cin, cout) * hv * wv * 4 >= (1ull << 31)) return false;
+  if ((long long)cin * cout * 9 >= (1ll << 31)) return false;  // 32-bit reduce indices
   if (in_mode != STX_IN_RAW && in_mode != STX_IN_RELU && in_mode != STX_IN_UPSAMPLE2 &&
       in_mode != WG16_S2)
     return false;
