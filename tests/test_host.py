@@ -44,6 +44,26 @@ def test_invalid_args_rejected():
     assert b"unsupported" in N.lib().stx_last_error_string()
 
 
+def test_pool_sum_contract_rejected():
+    """stx_conv_params.pool_sum (the fused nearest-x2 upsampling backward) is refused
+    before any launch unless it comes with pool_out on the split path's plain epilogue."""
+    from styletransfer_amd import _native as N
+    import ctypes as C
+    cp, op = N.lib(), None
+    # a well-formed split-path data gradient geometry (64 -> 128 at 64x64), fake pointers
+    p = N.ConvParams(x=16, y=32, n=1, cin=64, h=64, w=64, cout=128, ks=3, stride=1, pad=1,
+                     in_mode=0, hv=64, wv=64, ho=64, wo=64, cin_pad=64, cout_pad=128,
+                     wt16=48, w_amax=64, in_amax=80, pool_sum=1)
+    rc = cp.stx_conv2d(C.byref(p), op)  # no pool_out
+    assert rc == 1001 and b"pool_sum" in cp.stx_last_error_string()
+    p.pool_out, p.relu_out = 96, 1      # pool_out given, but a ReLU epilogue
+    rc = cp.stx_conv2d(C.byref(p), op)
+    assert rc == 1001 and b"pool_sum" in cp.stx_last_error_string()
+    p.relu_out, p.ho, p.wo, p.hv, p.wv, p.h, p.w = 0, 63, 63, 63, 63, 63, 63  # odd output
+    rc = cp.stx_conv2d(C.byref(p), op)
+    assert rc == 1001 and b"pool_sum" in cp.stx_last_error_string()
+
+
 def test_image_loader_matches_reference():
     from styletransfer_amd import img_utils
     d = np.load(os.path.join(GOLDEN, "images.npz"))
