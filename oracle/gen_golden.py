@@ -451,6 +451,47 @@ def case_config1(N, I, iters=50):
             "image_u8": np.asarray(Image.open(path))}
 
 
+def case_gatys512(N, H=512, iters=3):
+    """BASELINE config 2's workload at full size: the reference's StyleNetwork on the
+    bench's rank-0 inputs (synthetic 512^2 style / content, seeds 1000 / 2000), 3 Gatys
+    Adam iterations (get_content_optimizer's default optimiser).  Stores
+    the totals, iteration 1's seven loss values, the image gradients of iterations 1
+    and 3 and the image after 3 steps (norm + 32 projections each), and the sign bits
+    of the first update (Adam step 1 is ~lr*sign(g))."""
+    style = t(W.synthetic_image(1000, (1, 3, H, H)))
+    content = t(W.synthetic_image(2000, (1, 3, H, H)))
+    res = {}
+    for tag, net in (("ref", N.StyleNetwork(style, content)),
+                     ("ora", O.StyleNetwork(style, content, vgg_seed=VGG_SEED))):
+        x = content.clone()
+        opt = net.get_content_optimizer(x)
+        tot, grads, xs, per = [], [], [], None
+        for it in range(iters):
+            opt.zero_grad()
+            net(x, content)
+            total = (net.get_total_current_style_loss(100_000)
+                     + net.get_total_current_content_loss(1))
+            total.backward()
+            if it == 0:
+                per = [float(l.loss) for l, _ in net.style_losses] + \
+                      [float(net.content_losses[0][0].loss), float(net.feature_losses[0][0].loss)]
+            grads.append(O.to_np(x.grad).copy())
+            tot.append(float(total))
+            opt.step()
+            xs.append(O.to_np(x).copy())
+        res[tag] = (np.array(tot), np.array(per), grads, xs)
+    (tot, per, grads, xs), (otot, oper, og, oxs) = res["ref"], res["ora"]
+    close(otot, tot, rtol=1e-5, what="gatys512 losses")
+    close(og[0], grads[0], rtol=2e-5, what="gatys512 dx1")
+    c0 = content.numpy().astype(np.float64)
+    nproj = lambda a: np.concatenate([[np.linalg.norm(a)], proj32(a)])  # noqa: E731
+    return {"size": np.array(H), "style_seed": np.array(1000), "content_seed": np.array(2000),
+            "losses": tot, "losses_it1": per,
+            "dx1_proj": nproj(grads[0]), "dx3_proj": nproj(grads[2]),
+            "upd3_proj": nproj(xs[2] - c0),
+            "upd1_sign": np.packbits((xs[0] - c0).ravel() > 0)}
+
+
 def case_video_train(N, H=64, B=3, T=3, epochs=2):
     """The reference's own VideoTransformNet.video_train (stransfer/network.py:905-1069)
     for 2 epochs over one batch of B=3 synthetic clips of T=3 frames at 64^2 (B >= 3:
@@ -594,6 +635,7 @@ def main():
         "lbfgs": lambda: case_lbfgs(N),
         "config1": lambda: case_config1(N, I),
         "video_train": lambda: case_video_train(N),
+        "gatys512": lambda: case_gatys512(N),
     }
     os.makedirs(GOLDEN, exist_ok=True)
     only = [c for c in args.only.split(",") if c]

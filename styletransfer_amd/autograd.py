@@ -46,10 +46,11 @@ class ResLink:
     gradient contributions (one elementwise pass per block) disappears.  The IN's
     backward always runs first: the first conv's output gradient depends on it."""
 
-    __slots__ = ("g",)
+    __slots__ = ("g", "accepted")
 
     def __init__(self):
         self.g = None
+        self.accepted = False  # set by the conv that will add g in its epilogue
 
 
 class Conv2dFn(torch.autograd.Function):
@@ -62,6 +63,9 @@ class Conv2dFn(torch.autograd.Function):
         x = _c(x)
         # link (ResLink): a skip gradient to add into dx (raw-input stride-1 convs only)
         ctx.link = link if (stride == 1 and in_mode == N.STX_IN_RAW) else None
+        if link is not None:
+            # only a consuming conv takes the hand-off; otherwise the IN returns dres
+            link.accepted = ctx.link is not None
         cout, cin, ks, _ = w.shape
         # 3x3 stride-1 layers with cin >= 16 run on the fp16 hi/lo split MFMA kernel
         # (no fp32 slab needed); max|x| is computed once and kept for the wgrad.
@@ -271,7 +275,7 @@ class InstanceNormFn(torch.autograd.Function):
         dg, db, dcb = (None, None, None) if acc else bufs
         dres = None
         if ctx.has_res:
-            if ctx.res_link is not None and ctx.needs_input_grad[1]:
+            if ctx.res_link is not None and ctx.res_link.accepted and ctx.needs_input_grad[1]:
                 ctx.res_link.g = du  # added by the block's first conv (ResLink)
             else:
                 dres = du
@@ -400,10 +404,9 @@ class FastStLossFn(torch.autograd.Function):
     in one pass: the loss weights are folded into the backward operators (vgg.py
     folded mode: no per-loss scale vector, the content term rides on A_4), the TV loss
     and its gradient come from one kernel in the forward, and the weighted total is
-    summed in the same launch as the five style losses.  The backward assumes a unit
-    upstream gradient, i.e. `total.backward()` or a plain sum with other terms (as the
-    trainers use it; checking the value would cost a host sync).  Other callers use
-    VGGLossFn + TVLossFn."""
+    summed in the same launch as the five style losses.  The backward computes the
+    gradient for a unit upstream gradient and scales it by the device-side g (no
+    host sync), so `k * total` or a weighted sum with other terms is exact too."""
 
     @staticmethod
     def forward(ctx, y, c4, feat, targets, sw, cw, tv_factor):
@@ -423,7 +426,7 @@ class FastStLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         dx = V.loss_backward(ctx.feat, ctx.st, feature_grad=False)
-        dx.add_(ctx.tvg)
+        dx.add_(ctx.tvg).mul_(g)
         ctx.st = ctx.tvg = None
         return dx, None, None, None, None, None, None
 

@@ -19,6 +19,8 @@
 // writing the three planes of the [B][3][size][size] fp32 output (coalesced along x).
 #include <math.h>
 
+#include <vector>
+
 #include "common.h"
 #include "../../include/stx.h"
 
@@ -120,8 +122,7 @@ extern "C" int stx_resample_coeffs(int in_size, int out_size, int* bounds, int* 
   if (!bounds || !kk) return ksize;  // size query
   if (kk_stride < ksize) return -1;
   const double ss = 1.0 / filterscale;
-  double w[64];
-  if (ksize > 64) return -1;
+  std::vector<double> w(ksize);  // any down-scale factor (a crop of ~8000 px at 256 needs > 64)
   for (int xx = 0; xx < out_size; ++xx) {
     const double center = (xx + 0.5) * scale;
     double ww = 0.0;

@@ -22,9 +22,9 @@ constexpr int TPARTS = 512;  // partial blocks (fixed: the reduction order never
 __global__ void __launch_bounds__(TB)
 temporal_partial_kernel(const float* __restrict__ y, const float* __restrict__ yo,
                         const float* __restrict__ x, const float* __restrict__ xo, long long n,
-                        float* __restrict__ parts) {
+                        float* __restrict__ parts, int vec) {
   float sy = 0.f, sx = 0.f;
-  const long long n4 = n >> 2;
+  const long long n4 = vec ? n >> 2 : 0;  // a misaligned tensor: scalar loop throughout
   const long long stride = (long long)gridDim.x * TB;
   for (long long i = blockIdx.x * (long long)TB + threadIdx.x; i < n4; i += stride) {
     const f32x4 a = reinterpret_cast<const f32x4*>(y)[i] - reinterpret_cast<const f32x4*>(yo)[i];
@@ -70,10 +70,10 @@ temporal_final_kernel(const float* __restrict__ parts, float w, float* __restric
 __global__ void __launch_bounds__(TB)
 temporal_bwd_kernel(const float* __restrict__ y, const float* __restrict__ yo, long long n,
                     const float* __restrict__ fwd, float w, const float* __restrict__ g,
-                    float* __restrict__ grad, int accumulate) {
+                    float* __restrict__ grad, int accumulate, int vec) {
   const float a = fwd[1], c = fwd[2];
   const float s = a > 0.f ? (g ? *g : 1.f) * w / ((c + 1.f) * a) : 0.f;
-  const long long n4 = n >> 2;
+  const long long n4 = vec ? n >> 2 : 0;
   const long long stride = (long long)gridDim.x * TB;
   for (long long i = blockIdx.x * (long long)TB + threadIdx.x; i < n4; i += stride) {
     f32x4 d = s * (reinterpret_cast<const f32x4*>(y)[i] - reinterpret_cast<const f32x4*>(yo)[i]);
@@ -109,13 +109,12 @@ extern "C" int stx_temporal_loss(const float* y, const float* y_old, const float
     set_error("stx_temporal_loss: workspace");
     return STX_E_WORKSPACE;
   }
-  if (!aligned16(y) || !aligned16(y_old) || !aligned16(x) || !aligned16(x_old)) {
-    set_error("stx_temporal_loss: 16-byte aligned tensors required");
-    return STX_E_INVALID;
-  }
+  // views at odd offsets (e.g. the previous frame inside a [B, 6, H, W] input at an odd
+  // H*W) take the scalar loop: same result, no alignment contract on the caller
+  const int vec = aligned16(y) && aligned16(y_old) && aligned16(x) && aligned16(x_old);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(temporal_partial_kernel, dim3(TPARTS), dim3(TB), 0, st, y, y_old, x, x_old,
-                     n, (float*)ws);
+                     n, (float*)ws, vec);
   hipLaunchKernelGGL(temporal_final_kernel, dim3(1), dim3(TB), 0, st, (const float*)ws, weight,
                      out);
   return check_launch("stx_temporal_loss");
@@ -128,11 +127,8 @@ extern "C" int stx_temporal_loss_bwd(const float* y, const float* y_old, long lo
     set_error("stx_temporal_loss_bwd: invalid arguments");
     return STX_E_INVALID;
   }
-  if (!aligned16(y) || !aligned16(y_old) || !aligned16(grad)) {
-    set_error("stx_temporal_loss_bwd: 16-byte aligned tensors required");
-    return STX_E_INVALID;
-  }
+  const int vec = aligned16(y) && aligned16(y_old) && aligned16(grad);
   hipLaunchKernelGGL(temporal_bwd_kernel, dim3(tgrid(n)), dim3(TB), 0, (hipStream_t)stream, y,
-                     y_old, n, fwd, weight, g_dev, grad, accumulate);
+                     y_old, n, fwd, weight, g_dev, grad, accumulate, vec);
   return check_launch("stx_temporal_loss_bwd");
 }

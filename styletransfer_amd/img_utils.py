@@ -109,26 +109,20 @@ class ImageConditioner:
             t = self._tables[m] = (np.concatenate([bounds.ravel(), kk.ravel()]), k, y0, y1)
         return t
 
-    def __call__(self, images) -> torch.Tensor:
-        """images: sequence of HxWx3 uint8 arrays (or PIL images) -> [B, 3, S, S]."""
-        from ._native import ImageMeta, check, lib
-        arrs = [np.ascontiguousarray(np.asarray(im.convert("RGB") if isinstance(im, Image.Image)
-                                                else im, dtype=np.uint8)) for im in images]
-        B, S = len(arrs), self.size
-        if B == 0:
-            raise ValueError("empty image batch")
+    def _plan(self, shapes):
+        """Per-image metadata, the coefficient tables and workspace sizes of a batch of
+        HxW images: (metas, coef int32 array, max_rows, tmp bytes, src bytes)."""
+        from ._native import ImageMeta
+        B, S = len(shapes), self.size
         metas = (ImageMeta * B)()
         tables, coef_off, chunks, max_rows = {}, 0, [], 0
         src_off, tmp_off = 0, 0
-        for i, a in enumerate(arrs):
-            if a.ndim != 3 or a.shape[2] != 3:
-                raise ValueError(f"image {i}: HxWx3 uint8 expected, got {a.shape}")
-            h, w = a.shape[:2]
+        for i, (h, w) in enumerate(shapes):
             m = min(h, w)
             top, left = int(round((h - m) / 2.0)), int(round((w - m) / 2.0))
             md = metas[i]
             md.offset, md.h, md.w, md.top, md.left = src_off, h, w, top, left
-            src_off += a.nbytes
+            src_off += h * w * 3
             if m == S:  # torchvision Resize is a no-op at the target size
                 md.y0, md.y1, md.resize_w, md.resize_h = 0, m, 0, 0
             else:
@@ -144,8 +138,30 @@ class ImageConditioner:
                 md.tmp_offset = tmp_off
                 tmp_off += (y1 - y0) * S * 3
                 max_rows = max(max_rows, y1 - y0)
+        coef = np.concatenate(chunks) if chunks else np.zeros(1, np.int32)
+        return metas, coef, max_rows, tmp_off, src_off
+
+    def _launch(self, src, meta, b, max_rows, coef, out, tmp):
+        from ._native import check, lib
+        check(lib().stx_image_condition(src.data_ptr(), meta.data_ptr(), b, max_rows,
+                                        coef.data_ptr(), self.size, self._mean, self._std,
+                                        out.data_ptr(), tmp.data_ptr(), tmp.numel(),
+                                        torch.cuda.current_stream(self.device).cuda_stream),
+              "stx_image_condition")
+
+    def __call__(self, images) -> torch.Tensor:
+        """images: sequence of HxWx3 uint8 arrays (or PIL images) -> [B, 3, S, S]."""
+        arrs = [np.ascontiguousarray(np.asarray(im.convert("RGB") if isinstance(im, Image.Image)
+                                                else im, dtype=np.uint8)) for im in images]
+        B, S = len(arrs), self.size
+        if B == 0:
+            raise ValueError("empty image batch")
+        for i, a in enumerate(arrs):
+            if a.ndim != 3 or a.shape[2] != 3:
+                raise ValueError(f"image {i}: HxWx3 uint8 expected, got {a.shape}")
+        metas, coef, max_rows, tmp_bytes, src_bytes = self._plan([a.shape[:2] for a in arrs])
         dev = self.device
-        packed = torch.empty(src_off, dtype=torch.uint8, pin_memory=True)
+        packed = torch.empty(src_bytes, dtype=torch.uint8, pin_memory=True)
         pk = packed.numpy()
         o = 0
         for a in arrs:
@@ -153,12 +169,48 @@ class ImageConditioner:
             o += a.nbytes
         src = packed.to(dev, non_blocking=True)
         meta = torch.frombuffer(bytearray(bytes(metas)), dtype=torch.uint8).to(dev)
-        coef = torch.from_numpy(np.concatenate(chunks) if chunks else np.zeros(1, np.int32)).to(dev)
-        tmp = torch.empty(max(tmp_off, 16), dtype=torch.uint8, device=dev)
+        coef = torch.from_numpy(coef).to(dev)
+        tmp = torch.empty(max(tmp_bytes, 16), dtype=torch.uint8, device=dev)
         out = torch.empty((B, 3, S, S), dtype=torch.float32, device=dev)
-        check(lib().stx_image_condition(src.data_ptr(), meta.data_ptr(), B, max_rows,
-                                        coef.data_ptr(), S, self._mean, self._std,
-                                        out.data_ptr(), tmp.data_ptr(), tmp.numel(),
-                                        torch.cuda.current_stream(dev).cuda_stream),
-              "stx_image_condition")
+        self._launch(src, meta, B, max_rows, coef, out, tmp)
         return out
+
+    def fixed(self, h: int, w: int, out: torch.Tensor | None = None) -> "FixedConditioner":
+        """A conditioner for a stream of HxW frames with static buffers (video_st)."""
+        return FixedConditioner(self, h, w, out)
+
+
+class FixedConditioner:
+    """image_loader_transform of a stream of same-size frames (video_st: every decoded
+    frame of a clip, stransfer/dataset.py:280-306) with everything static: the
+    coefficient tables and metadata are uploaded once, the frame's bytes go into a
+    device buffer `src` ([H][W][3] uint8) and the [1, 3, S, S] result into `out` (which
+    may be a view into a caller's buffer, e.g. FrameEngine's 6-channel input).  `run()`
+    is two kernel launches and no allocation or host transfer, so a hipGraph can
+    capture it."""
+
+    def __init__(self, cond: ImageConditioner, h: int, w: int, out: torch.Tensor | None = None):
+        self.cond, self.h, self.w = cond, int(h), int(w)
+        dev, S = cond.device, cond.size
+        metas, coef, self.max_rows, tmp_bytes, src_bytes = cond._plan([(self.h, self.w)])
+        self.meta = torch.frombuffer(bytearray(bytes(metas)), dtype=torch.uint8).to(dev)
+        self.coef = torch.from_numpy(coef).to(dev)
+        self.tmp = torch.empty(max(tmp_bytes, 16), dtype=torch.uint8, device=dev)
+        self.src = torch.empty((self.h, self.w, 3), dtype=torch.uint8, device=dev)
+        if out is None:
+            out = torch.empty((1, 3, S, S), dtype=torch.float32, device=dev)
+        if tuple(out.shape) != (1, 3, S, S) or not out.is_contiguous() or \
+                out.dtype != torch.float32 or out.device != self.src.device:
+            raise ValueError(f"out must be a contiguous fp32 [1, 3, {S}, {S}] device tensor")
+        self.out = out
+
+    def load(self, frame) -> None:
+        """Copy one HxWx3 uint8 frame (numpy array or tensor, host or device) into src."""
+        t = frame if isinstance(frame, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frame))
+        if tuple(t.shape) != (self.h, self.w, 3) or t.dtype != torch.uint8:
+            raise ValueError(f"frame must be uint8 [{self.h}, {self.w}, 3], got {tuple(t.shape)}")
+        self.src.copy_(t, non_blocking=True)
+
+    def run(self) -> torch.Tensor:
+        self.cond._launch(self.src, self.meta, 1, self.max_rows, self.coef, self.out, self.tmp)
+        return self.out

@@ -236,12 +236,21 @@ class TrainedSlabs:
 
     def __init__(self, convs):
         self.convs = list(convs)
+        self.generation = 0
+        self._retired = []
+        self.slabs = None
         self._build()
 
     def _build(self):
         split = os.environ.get("STX_CONV_SPLIT", "1") != "0"
         L = lib()
         jobs = []
+        if self.slabs is not None:
+            # a hipGraph captured earlier still holds the old slab / job pointers: keep
+            # them alive (as _Workspace retires scratch buffers) and bump the generation
+            # so the owner re-captures (train.FastStTrainer checks it before a replay)
+            self._retired.append((self.slabs, self._jobs))
+            self.generation += 1
         self.slabs = []
         for conv in self.convs:
             w = conv.weight

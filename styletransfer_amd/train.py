@@ -80,6 +80,9 @@ class FastStTrainer:
             return 0
         return dist.get_global_rank(self.pg, 0)
 
+    def _param_ptrs(self):
+        return tuple(p.data_ptr() for p in self.params) + (self.slabs.generation,)
+
     def resync_params(self):
         """No-op: load_state_dict copies into the flat views in place."""
 
@@ -151,8 +154,13 @@ class FastStTrainer:
             loss = self._fwd_bwd(static)
         with torch.cuda.graph(g_up, pool=g_fb.pool(), capture_error_mode="thread_local"):
             self.opt.step()
+        ptrs = self._param_ptrs()
 
         def replay():
+            if self._param_ptrs() != ptrs:
+                # the graphs hold the captured parameter, gradient and slab pointers
+                raise RuntimeError("FastStTrainer: parameters were re-homed after capture(); "
+                                   "capture again")
             g_fb.replay()
             self._exchange()
             g_up.replay()
@@ -168,10 +176,12 @@ class FastStTrainer:
         batch = batch.to(self.device, torch.float32).contiguous()
         if not graph:
             return self.step(batch)
+        if self._graph is not None and self._graph[3] != self._param_ptrs():
+            self._graph = None  # parameters re-homed: the captured pointers are stale
         if self._graph is None:
-            self._graph = self.capture(batch, warmup=1)
+            self._graph = self.capture(batch, warmup=1) + (self._param_ptrs(),)
             return self.warmup_loss
-        replay, static, loss = self._graph
+        replay, static, loss, _ = self._graph
         if static.shape != batch.shape:
             return self.step(batch)
         static.copy_(batch)

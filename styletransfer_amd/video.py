@@ -29,26 +29,20 @@ VIDEO_EXTS = (".mp4", ".avi", ".mov", ".mkv", ".gif", ".webm")
 FRAME_EXTS = (".png", ".jpg", ".jpeg", ".bmp")
 
 
-def iterate_frames(source, max_frames=90 * 24, imsize=None) -> Iterator[torch.Tensor]:
-    """Conditioned frames [1, 3, IMSIZE, IMSIZE] of a video (stransfer/dataset.py:280-310).
-
-    `source`: a video file (decoded with imageio when it is installed, as the
-    reference does), a directory of frame images (sorted by the integer in their
-    name, then by name), a `.npy` array [T, H, W, 3] uint8 (loaded with
-    allow_pickle=False), or an in-memory uint8 array of that shape."""
+def iterate_raw_frames(source, max_frames=90 * 24) -> Iterator[np.ndarray]:
+    """Decoded frames of a video as HxWx3 uint8 arrays (the sources of iterate_frames)."""
     from PIL import Image
     if isinstance(source, np.ndarray):
-        frames = (Image.fromarray(f) for f in source)
+        frames = iter(source)
     elif isinstance(source, str) and source.endswith(".npy"):
-        arr = np.load(source, allow_pickle=False, mmap_mode="r")
-        frames = (Image.fromarray(np.ascontiguousarray(f)) for f in arr)
+        frames = iter(np.load(source, allow_pickle=False, mmap_mode="r"))
     elif isinstance(source, str) and os.path.isdir(source):
         def key(name):
             stem = os.path.splitext(name)[0]
             digits = "".join(ch for ch in stem if ch.isdigit())
             return (int(digits) if digits else -1, name)
         names = sorted((n for n in os.listdir(source) if n.lower().endswith(FRAME_EXTS)), key=key)
-        frames = (Image.open(os.path.join(source, n)).convert("RGB") for n in names)
+        frames = (np.asarray(Image.open(os.path.join(source, n)).convert("RGB")) for n in names)
     elif isinstance(source, str) and source.lower().endswith(VIDEO_EXTS):
         try:
             import imageio
@@ -60,22 +54,44 @@ def iterate_frames(source, max_frames=90 * 24, imsize=None) -> Iterator[torch.Te
         def gen():
             try:
                 while True:
-                    yield Image.fromarray(reader.get_next_data())
+                    yield np.asarray(reader.get_next_data())
             except IndexError:
                 return
         frames = gen()
     else:
         raise ValueError(f"unsupported video source {source!r}")
-    for i, im in enumerate(frames):
+    for i, f in enumerate(frames):
         if i >= max_frames:
             break
-        yield img_utils.image_loader_transform(im, imsize)
+        f = np.ascontiguousarray(f, dtype=np.uint8)
+        if f.ndim == 3 and f.shape[2] == 4:
+            f = np.ascontiguousarray(f[:, :, :3])  # RGBA frame: .convert("RGB") drops alpha
+        yield f
+
+
+def iterate_frames(source, max_frames=90 * 24, imsize=None) -> Iterator[torch.Tensor]:
+    """Conditioned frames [1, 3, IMSIZE, IMSIZE] of a video (stransfer/dataset.py:280-310),
+    through the host-side PIL transforms (img_utils.image_loader_transform).
+
+    `source`: a video file (decoded with imageio when it is installed, as the
+    reference does), a directory of frame images (sorted by the integer in their
+    name, then by name), a `.npy` array [T, H, W, 3] uint8 (loaded with
+    allow_pickle=False), or an in-memory uint8 array of that shape."""
+    from PIL import Image
+    for f in iterate_raw_frames(source, max_frames):
+        yield img_utils.image_loader_transform(Image.fromarray(f), imsize)
 
 
 class FrameEngine:
-    """One stylised frame = one hipGraph replay of the VideoTransformNet forward."""
+    """One stylised frame = one hipGraph replay of the VideoTransformNet forward.
 
-    def __init__(self, net, shape, device=None, graph=True):
+    raw_hw=(H, W): frames arrive as decoded HxWx3 uint8 (`step_raw`) and the graph
+    also holds their conditioning (centre crop, Pillow-exact resize to the engine's
+    size, normalisation: img_utils.FixedConditioner) written straight into the
+    frame channels of the 6-channel input -- the per-frame path of
+    process_video (stransfer/network.py:1117-1131) with no host-side resize."""
+
+    def __init__(self, net, shape, device=None, graph=True, raw_hw=None):
         self.net = net
         self.dev = torch.device(device or constants.DEVICE)
         n, c, h, w = shape
@@ -90,8 +106,14 @@ class FrameEngine:
         self.graph = None
         self.use_graph = graph
         self.started = False
+        self.cond = None
+        if raw_hw is not None:
+            assert h == w, "frames are conditioned to IMSIZE x IMSIZE"
+            self.cond = img_utils.ImageConditioner(h, self.dev).fixed(*raw_hw, out=self.frame)
 
     def _forward(self):
+        if self.cond is not None:
+            self.cond.run()                # uint8 frame -> normalised frame channels
         with torch.no_grad():
             y = self.net(self.x6)
         if self.out is None:
@@ -106,11 +128,28 @@ class FrameEngine:
 
     def step(self, frame: torch.Tensor) -> torch.Tensor:
         """Stylise one conditioned frame [n, 3, H, W]; returns the (static) output."""
+        if self.cond is not None:
+            raise RuntimeError("FrameEngine(raw_hw=...) takes uint8 frames: use step_raw")
         self.frame.copy_(frame)
         if not self.started:
             self.prev.copy_(frame)         # first frame: old = the frame itself
             self.prev_frame.copy_(frame)
             self.started = True
+        return self._run()
+
+    def step_raw(self, frame_u8) -> torch.Tensor:
+        """Stylise one decoded HxWx3 uint8 frame (host array or device tensor)."""
+        if self.cond is None:
+            raise RuntimeError("FrameEngine without raw_hw takes conditioned frames: use step")
+        self.cond.load(frame_u8)
+        if not self.started:
+            self.cond.run()                # first frame: old = the frame itself
+            self.prev.copy_(self.frame)
+            self.prev_frame.copy_(self.frame)
+            self.started = True
+        return self._run()
+
+    def _run(self):
         if self.graph is not None:
             self.graph.replay()
         elif self.use_graph and self.out is not None:
@@ -139,10 +178,21 @@ def process_video(net, video_path, style_name="nsp", working_dir="workdir/", out
     os.makedirs(working_dir, exist_ok=True)
     os.makedirs(out_dir, exist_ok=True)
     eng = None
-    for i, frame in enumerate(iterate_frames(video_path, max_frames)):
-        if eng is None:
-            eng = FrameEngine(net, tuple(frame.shape), frame.device, graph=graph)
-        y = eng.step(frame)
+    S = constants.IMSIZE
+    for i, frame in enumerate(iterate_raw_frames(video_path, max_frames)):
+        # decoded uint8 frames go to the GPU as they are; crop, resize and normalisation
+        # run inside the per-frame graph (bit-identical to image_loader_transform)
+        if eng is None or eng.cond.h != frame.shape[0] or eng.cond.w != frame.shape[1]:
+            if eng is not None:  # a clip whose frame size changes: a new engine, as the
+                prev = eng.out.clone()  # reference, but keep the recurrence going
+            eng2 = FrameEngine(net, (1, 3, S, S), constants.DEVICE, graph=graph,
+                               raw_hw=frame.shape[:2])
+            if eng is not None:
+                eng2.prev.copy_(prev)
+                eng2.prev_frame.copy_(eng.prev_frame)
+                eng2.started = True
+            eng = eng2
+        y = eng.step_raw(frame)
         img_utils.imshow(y[0], path=os.path.join(working_dir, f"{i}.png"))
     final = os.path.join(out_dir, f"video_st_{style_name}.mp4")
     try:

@@ -43,7 +43,8 @@ def test_oracle_condition_equals_image_loader():
 
 
 @pytest.mark.parametrize("n_in,n_out", [(444, 256), (100, 256), (513, 256), (5, 3), (1, 4),
-                                        (4000, 256), (640, 512), (256, 255)])
+                                        (4000, 256), (640, 512), (256, 255),
+                                        (9000, 256), (20000, 64)])  # ksize > 64
 def test_native_coeffs_equal_oracle(n_in, n_out):
     import ctypes as C
     from styletransfer_amd import _native as N

@@ -24,13 +24,17 @@ def rel(a, b):
     return float((a - b).norm() / b.norm())
 
 
-def test_frame_engine_matches_oracle(dev):
+@pytest.mark.parametrize("size", [64, 65, 256], ids=["64", "odd65", "config5_256"])
+def test_frame_engine_matches_oracle(dev, size):
+    """64: the r1 case; 65: an odd frame (the previous stylised frame is a view at an
+    odd offset inside the 6-channel input -- ADVICE r2); 256: BASELINE config 5's
+    per-frame shape (IMSIZE 256; stransfer/dataset.py:299-300)."""
     sd = {k: torch.from_numpy(v) for k, v in W.itn_synthetic(777, in_channels=6)}
     net = network.VideoTransformNet(torch.rand([3, 64, 64]))
     net.load_state_dict(sd)
     ref_net = O.image_transform_net(777, in_channels=6).eval()
-    frames = [torch.from_numpy(W.synthetic_image(900 + t, (1, 3, 64, 64))) for t in range(4)]
-    eng = video.FrameEngine(net, (1, 3, 64, 64), dev, graph=True)
+    frames = [torch.from_numpy(W.synthetic_image(900 + t, (1, 3, size, size))) for t in range(4)]
+    eng = video.FrameEngine(net, (1, 3, size, size), dev, graph=True)
     prev_ours = None
     for t, f in enumerate(frames):
         y = eng.step(f.to(dev)).clone()
@@ -56,6 +60,47 @@ def test_process_video_from_npy(dev, tmp_path, monkeypatch):
                               out_dir=str(tmp_path / "out") + "/")
     assert sorted(p.name for p in (tmp_path / "wd").iterdir()) == ["0.png", "1.png", "2.png"]
     assert out
+    # the GPU-conditioned frames give the PNGs of the PIL-conditioned recurrence
+    from PIL import Image
+    eng = video.FrameEngine(net, (1, 3, 256, 256), dev, graph=False)
+    for i, f in enumerate(video.iterate_frames(arr)):
+        want = np.asarray(img_utils_to_pil(eng.step(f)[0]))
+        got = np.asarray(Image.open(tmp_path / "wd" / f"{i}.png"))
+        assert np.array_equal(got, want), i
+
+
+def img_utils_to_pil(t):
+    from styletransfer_amd import img_utils
+    return img_utils.to_pil(t)
+
+
+def test_raw_frames_config5_1080p_equal_pil_path(dev):
+    """BASELINE config 5 as written: decoded 1080p uint8 frames go to the GPU as they
+    are and are conditioned inside the per-frame graph (FrameEngine(raw_hw=...)); the
+    stylised frames equal those of the PIL-conditioned path (image_loader_transform,
+    stransfer/dataset.py:280-306) bit for bit."""
+    sd = {k: torch.from_numpy(v) for k, v in W.itn_synthetic(777, in_channels=6)}
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 256, (1080, 1920, 3), dtype=np.uint8)
+    frames = [np.roll(base, 7 * t, axis=1) for t in range(4)]  # a panning clip
+    from PIL import Image
+    from styletransfer_amd import img_utils
+    outs = {}
+    for raw in (False, True):
+        net = network.VideoTransformNet(torch.rand([3, 64, 64]))
+        net.load_state_dict(sd)
+        eng = video.FrameEngine(net, (1, 3, 256, 256), dev, graph=True,
+                                raw_hw=(1080, 1920) if raw else None)
+        outs[raw] = []
+        for f in frames:
+            if raw:
+                y = eng.step_raw(f)
+            else:
+                y = eng.step(img_utils.image_loader_transform(Image.fromarray(f), 256))
+            outs[raw].append(y.cpu().clone())
+        assert eng.graph is not None
+    for t, (a, b) in enumerate(zip(outs[False], outs[True])):
+        assert torch.equal(a, b), t
 
 
 def test_frame_engine_replay_after_idle(dev):
