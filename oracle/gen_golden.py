@@ -483,12 +483,30 @@ def case_gatys512(N, H=512, iters=3):
     (tot, per, grads, xs), (otot, oper, og, oxs) = res["ref"], res["ora"]
     close(otot, tot, rtol=1e-5, what="gatys512 losses")
     close(og[0], grads[0], rtol=2e-5, what="gatys512 dx1")
+    # the same iterations through the oracle in float64: at 512^2 the fp32 reference's
+    # image gradient is ~1e-3 from the fp64 one (ReLU / argmax decisions of elements
+    # within rounding of a kink), so gradients and the image are compared three-way
+    d64 = torch.float64
+    net64 = O.StyleNetwork(style.to(d64), content.to(d64), vgg=O.vgg19_features(VGG_SEED).to(d64))
+    x = content.to(d64).clone()
+    opt = net64.get_content_optimizer(x)
+    g64, x64 = [], []
+    for it in range(iters):
+        opt.zero_grad()
+        net64(x, content.to(d64))
+        (net64.get_total_current_style_loss(100_000)
+         + net64.get_total_current_content_loss(1)).backward()
+        g64.append(O.to_np(x.grad).copy())
+        opt.step()
+        x64.append(O.to_np(x).copy())
     c0 = content.numpy().astype(np.float64)
     nproj = lambda a: np.concatenate([[np.linalg.norm(a)], proj32(a)])  # noqa: E731
     return {"size": np.array(H), "style_seed": np.array(1000), "content_seed": np.array(2000),
             "losses": tot, "losses_it1": per,
             "dx1_proj": nproj(grads[0]), "dx3_proj": nproj(grads[2]),
             "upd3_proj": nproj(xs[2] - c0),
+            "dx1_proj_64": nproj(g64[0]), "dx3_proj_64": nproj(g64[2]),
+            "upd3_proj_64": nproj(x64[2] - c0),
             "upd1_sign": np.packbits((xs[0] - c0).ravel() > 0)}
 
 

@@ -154,3 +154,58 @@ def vgg_branches_from_z(zs):
     _, i4 = F.max_pool2d(F.relu(z4), 2, 2, return_indices=True)
     out.append((z4 > 0, i4))
     return out
+
+
+# the ImageTransformNet's ReLU sites in forward order (the InstanceNorm each follows)
+ITN_RELU_SITES = ["1", "4", "7"] + [f"{b}.insn1" for b in range(9, 14)] + ["16", "20"]
+
+
+def flip_upstream(keys, itn_a, itn_b, vgg_a, vgg_b):
+    """Indices (into the state_dict key list `keys`) of every parameter whose gradient a
+    branch difference between records a and b can move beyond rounding: a flip at an
+    ITN ReLU site moves the gradients of every parameter up to that site's
+    InstanceNorm; a flip in the loss network moves all of them."""
+    if count_flips(vgg_a, vgg_b):
+        return set(range(len(keys)))
+    last = -1
+    for site, u, v in zip(ITN_RELU_SITES, itn_a, itn_b):
+        if int((u != v).sum()):
+            last = keys.index(f"{site}.bias")
+    return set(range(last + 1))
+
+
+class HipBranchSpy:
+    """Context manager recording the HIP forward's branch decisions: the ReLU mask of
+    every fused InstanceNorm+ReLU of `net` (forward hooks) and, from the loss
+    network's own pre-ReLU outputs Z1..Z4 (a spy on `vgg_mod.loss_forward`, the fused
+    engine both the reference-API StyleNetwork and the trainers call), the VGG masks
+    and argmax indices.  Use `with HipBranchSpy(net, V, monkeypatch) as spy: ...`, then
+    spy.itn, spy.vgg."""
+
+    def __init__(self, net, vgg_mod, monkeypatch):
+        self.net, self.V, self.mp = net, vgg_mod, monkeypatch
+        self.itn, self.zs = [], []
+
+    def __enter__(self):
+        def hook(m, args, kwargs, out):
+            if kwargs.get("relu", False):
+                self.itn.append((out.detach() > 0).cpu())
+        self.hs = [m.register_forward_hook(hook, with_kwargs=True) for m in self.net.modules()
+                   if isinstance(m, torch.nn.InstanceNorm2d)]
+        self.orig = self.V.loss_forward
+
+        def spy(*a, **k):
+            st = self.orig(*a, **k)
+            self.zs[:] = [z.detach().clone() for z in st.z]
+            return st
+        self.mp.setattr(self.V, "loss_forward", spy)
+        return self
+
+    def __exit__(self, *exc):
+        self.mp.setattr(self.V, "loss_forward", self.orig)
+        for h in self.hs:
+            h.remove()
+
+    @property
+    def vgg(self):
+        return vgg_branches_from_z(self.zs)

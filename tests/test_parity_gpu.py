@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 import torch
 
+import forced_ref as R
 from conftest import GOLDEN
 from styletransfer_amd import network, ops
 from styletransfer_amd import vgg as V
@@ -187,9 +188,12 @@ def test_gatys_config2_512_engine_golden(dev):
     """BASELINE config 2 at full size: GatysEngine at 512^2 (the bench's rank-0 inputs and
     its exact launches: the fused Gram partials of 1024 tiles, 256x2 grids, the data
     gradients of 1024 blocks; one eager iteration, then hipGraph replays) against the
-    reference's own StyleNetwork (gatys512.npz, 3 Adam iterations).  Losses and image
-    gradients within 1e-4; the first update ~lr*sign(g) agrees in sign except on a
-    negligible fraction of pixels (|g| ~ rounding); the image after 3 steps within 1e-3."""
+    reference's own StyleNetwork (gatys512.npz, 3 Adam iterations).  Losses within 1e-4;
+    the first update ~lr*sign(g) agrees in sign except on a negligible fraction of
+    pixels (|g| ~ rounding).  At this size the fp32 reference's image gradient is itself
+    ~1.1e-3 from the fp64 run's (elements within rounding of a ReLU / argmax kink), so
+    gradients and the image after 3 steps are compared three-way: HIP's distance from
+    the fp64 run <= 2.5x the fp32 reference's (32 projections + norm)."""
     d = g("gatys512")
     H = int(d["size"])
     style = T(W.synthetic_image(int(d["style_seed"]), (1, 3, H, H)), dev)
@@ -211,14 +215,17 @@ def test_gatys_config2_512_engine_golden(dev):
     assert rel(tot, d["losses"]) < 1e-4, (tot, d["losses"])
     # style x5 (unweighted), content; the feature loss is computed but not optimised
     assert rel(per, d["losses_it1"]) < 1e-4, (per, d["losses_it1"])
-    assert rel(nproj(dx1), d["dx1_proj"]) < 1e-4
-    assert rel(nproj(dx3), d["dx3_proj"]) < 1e-4
+    errs = {}
+    for k, v in (("dx1", dx1), ("dx3", dx3), ("upd3", x3 - c0)):
+        e, r = rel(nproj(v), d[f"{k}_proj_64"]), rel(d[f"{k}_proj"], d[f"{k}_proj_64"])
+        errs[k] = (e, r)
+        assert e <= max(2.5 * r, 1e-5), (k, e, r)
     s_hip = (x1 - c0).ravel() > 0
     s_ref = np.unpackbits(d["upd1_sign"])[:s_hip.size].astype(bool)
     flips = float(np.mean(s_hip != s_ref))
     assert flips <= 1e-3, flips
-    assert rel(nproj(x3 - c0), d["upd3_proj"]) < 1e-3
-    print(f"gatys512: losses {tot}; step-1 sign flips {flips:.2e}")
+    print(f"gatys512: losses {tot}; vs fp64 (hip, fp32 reference): {errs}; "
+          f"step-1 sign flips {flips:.2e}")
 
 
 @pytest.fixture(scope="module")
@@ -236,15 +243,17 @@ def test_itn_state_dict_keys(itn_case):
     assert keys == [k for k, _ in W.itn_synthetic(4321)]
 
 
-def test_itn_forward_backward_golden(itn_case, dev):
+def test_itn_forward_backward_golden(itn_case, dev, monkeypatch):
     d, net = itn_case
     batch = T(d["batch"], dev)
     ln = network.StyleNetwork(T(d["style"], dev),
                               T(W.synthetic_image(23, (1, 3, 64, 64)), dev))
     net.zero_grad()
-    y = net(batch)
-    assert rel(y, d["y"]) < 1e-4
-    ln(y, content_image=batch)
+    with R.HipBranchSpy(net, V, monkeypatch) as spy:
+        y = net(batch)
+        assert rel(y, d["y"]) < 1e-4
+        ln(y, content_image=batch)
+    hip_branches = (spy.itn, spy.vgg)
     sl = ln.get_total_current_style_loss(100_000)
     cl = ln.get_total_current_content_loss(1)
     tv = net.get_total_variation_regularization_loss(y)
@@ -254,35 +263,34 @@ def test_itn_forward_backward_golden(itn_case, dev):
     assert rel(cl, d["content_loss"]) < 1e-4
     assert rel(tv, d["tv_loss"]) < 1e-4
     assert rel(total, d["total"]) < 1e-4
-    # parameter gradients, three-way against fp64 truth (itn_fp64.npz: the pinned
-    # oracle evaluated in float64 on the same inputs).  The fp32 reference itself is
-    # ~7e-4 from fp64 here (rounding propagated through 15 InstanceNorm layers).
-    # Walking from the output back towards the input, the HIP gradient is within
-    # 2.5x of that until the backward crosses a ReLU boundary element (an IN output
-    # within rounding of 0 whose mask the fp32-class forward decides differently
-    # from fp64; measured: block 11's insn1, 11.insn1.bias 2.4e-2).  Every parameter
-    # upstream of that single flip inherits its effect, bounded here by 3e-2, and
-    # there must be no second jump.  Each layer's kernels are held to 3x the fp32
-    # error vs fp64 in isolation by tests/test_itn_layers_gpu.py, which has no such
-    # cascade.
+    # parameter gradients vs fp64 truth (itn_fp64.npz: the pinned oracle in float64 on
+    # the same inputs).  A ReLU / argmax branch decided differently from fp64 (an
+    # element within rounding of a kink) moves every parameter gradient upstream of it;
+    # which parameters those are is read from the branch records themselves (HIP's, and
+    # an fp32 oracle run's standing in for the fp32 reference), never inferred from the
+    # size of an error.  Downstream of every flip: HIP within 2.5x the fp32 reference's
+    # error.  All parameters, flips included, are held to fp32-class error against fp64
+    # with the branches forced in tests/test_itn_masks_gpu.py.
     f64 = g("itn_fp64")
     norms = f64["grad64_proj"][:, 0]
     params = list(net.parameters())
-    flipped, errs = False, []
-    for i in reversed(range(len(params))):          # output side first
+    flipped = itn_flipped_params(hip_branches)
+    errs = []
+    for i in range(len(params)):
         gp = params[i].grad.detach().cpu().numpy()
         if norms[i] < 1e-7 * norms.max():
             # conv bias followed by InstanceNorm: exactly 0 in exact arithmetic (fp64
             # |g| ~ 1e-14; fp32 rounding noise ~1e-5 in the reference)
             assert np.linalg.norm(gp) < 1e-6 * norms.max(), i
             continue
+        if i in flipped:
+            continue
         e64 = rel(proj32(gp), f64["grad64_proj"][i, 1:])
         r32 = float(f64["ref32_err"][i])
         errs.append((e64, r32, i))
-        if not flipped and e64 > max(2.5 * r32, 1e-5):
-            flipped = True                             # the one boundary crossing
-        assert e64 <= (3e-2 if flipped else max(2.5 * r32, 1e-5)), (i, e64, r32)
-    print("ITN grad error vs fp64 (hip, fp32-ref, param):", sorted(errs)[-3:])
+        assert e64 <= max(2.5 * r32, 1e-5), (i, e64, r32)
+    print("ITN grad error vs fp64 downstream of every flip (hip, fp32-ref, param):",
+          sorted(errs)[-3:], "flip-affected params:", len(flipped))
     with torch.no_grad():
         assert rel(net(batch[:1]), d["y_single"]) < 1e-4
 
@@ -293,22 +301,21 @@ def proj32(a, seed=77):
     return r @ a
 
 
-def itn_flipped_params(net):
-    """Indices of the parameters upstream of the backward's first ReLU-boundary flip
-    (test_itn_forward_backward_golden), from the gradients held in net."""
-    f64 = g("itn_fp64")
-    norms = f64["grad64_proj"][:, 0]
-    params = list(net.parameters())
-    for i in reversed(range(len(params))):
-        if norms[i] < 1e-7 * norms.max():
-            continue
-        e64 = rel(proj32(params[i].grad.detach().cpu().numpy()), f64["grad64_proj"][i, 1:])
-        if e64 > max(2.5 * float(f64["ref32_err"][i]), 1e-5):
-            return set(range(i + 1))
-    return set()
+def itn_flipped_params(hip_branches):
+    """Parameters (indices) whose gradient a branch flip can move: upstream of any
+    element where HIP's decision or the fp32 reference's (an fp32 oracle run on the
+    golden inputs) differs from the fp64 run's."""
+    d = g("itn")
+    sd = W.itn_synthetic(4321)
+    keys = [k for k, _ in sd]
+    vgg = W.vgg19_synthetic(1234, 5)
+    n64 = R.natural_branches(sd, vgg, d["batch"], torch.float64)
+    n32 = R.natural_branches(sd, vgg, d["batch"], torch.float32)
+    return (R.flip_upstream(keys, hip_branches[0], n64[0], hip_branches[1], n64[1])
+            | R.flip_upstream(keys, n32[0], n64[0], n32[1], n64[1]))
 
 
-def test_itn_adam_step_golden(itn_case, dev):
+def test_itn_adam_step_golden(itn_case, dev, monkeypatch):
     """itn.npz["adam1_proj"]: the reference's ImageTransformNet.get_optimizer() Adam
     step (stransfer/network.py:643-649) after the golden forward/backward."""
     d, _ = itn_case
@@ -318,12 +325,14 @@ def test_itn_adam_step_golden(itn_case, dev):
     ln = network.StyleNetwork(T(d["style"], dev), T(W.synthetic_image(23, (1, 3, 64, 64)), dev))
     opt = net.get_optimizer()
     opt.zero_grad()
-    y = net(batch)
-    ln(y, content_image=batch)
+    with R.HipBranchSpy(net, V, monkeypatch) as spy:
+        y = net(batch)
+        ln(y, content_image=batch)
     (ln.get_total_current_style_loss(100_000) + ln.get_total_current_content_loss(1)
      + net.get_total_variation_regularization_loss(y)).backward()
     gnorm = [float(p.grad.norm()) for p in net.parameters()]
-    flipped = itn_flipped_params(net)
+    grads = [p.grad.detach().clone() for p in net.parameters()]
+    flipped = itn_flipped_params((spy.itn, spy.vgg))
     p0 = [p.detach().clone() for p in net.parameters()]
     opt.step()
     errs = []
@@ -342,6 +351,13 @@ def test_itn_adam_step_golden(itn_case, dev):
         assert e < (2e-2 if i in flipped else 2e-3), (i, e)
     print("ITN Adam step vs reference (rel err, param):", sorted(errs)[-3:],
           "flip-affected params:", len(flipped))
+    # the optimizer itself, flips aside: torch.optim.Adam on the same gradients
+    for p0i, gi, p in zip(p0, grads, net.parameters()):
+        q = p0i.clone().requires_grad_()
+        q.grad = gi.clone()
+        torch.optim.Adam([q]).step()
+        assert float((q.detach() - p.detach()).abs().max()) <= 1e-6 * max(
+            1.0, float(p0i.abs().max())), "Adam step 1 vs torch.optim.Adam"
 
 
 def test_fast_st_trainer_matches_api(itn_case, dev):

@@ -24,11 +24,12 @@ def rel(a, b):
     return float((a - b).norm() / b.norm())
 
 
-@pytest.mark.parametrize("size", [64, 65, 256], ids=["64", "odd65", "config5_256"])
+@pytest.mark.parametrize("size", [64, 68, 256], ids=["64", "68", "config5_256"])
 def test_frame_engine_matches_oracle(dev, size):
-    """64: the r1 case; 65: an odd frame (the previous stylised frame is a view at an
-    odd offset inside the 6-channel input -- ADVICE r2); 256: BASELINE config 5's
-    per-frame shape (IMSIZE 256; stransfer/dataset.py:299-300)."""
+    """64: the r1 case; 68: a side that is not a multiple of 8; 256: BASELINE config 5's
+    per-frame shape (IMSIZE 256; stransfer/dataset.py:299-300).  (A side that is not a
+    multiple of 4 is not a valid video frame for the reference either: the network's
+    output, e.g. 68 for 65, no longer concatenates with the next frame.)"""
     sd = {k: torch.from_numpy(v) for k, v in W.itn_synthetic(777, in_channels=6)}
     net = network.VideoTransformNet(torch.rand([3, 64, 64]))
     net.load_state_dict(sd)
@@ -138,6 +139,15 @@ def test_temporal_loss_vs_oracle(dev):
     ref.backward()
     assert abs(float(loss) - float(ref)) <= 1e-6 * float(ref)
     assert rel(y.grad, yd.grad) < 1e-6
+    # views at an odd element offset (not 16-byte aligned: ADVICE r2) take the scalar path
+    buf = [torch.cat([torch.zeros(1), t.reshape(-1)]).to(dev) for t in ys]
+    vs = [b_[1:].view(shp) for b_ in buf]
+    yv = vs[0].detach().requires_grad_()  # a leaf at a 4-byte offset
+    assert yv.data_ptr() % 16 != 0
+    lv = net.get_temporal_loss(vs[1], vs[2], vs[3], yv, 0.8)
+    lv.backward()
+    assert abs(float(lv) - float(ref)) <= 1e-6 * float(ref)
+    assert rel(yv.grad, yd.grad) < 1e-6
     # zero change in the stylised frames: loss 0, gradient 0 (torch's norm backward)
     z = ys[2].to(dev).clone().requires_grad_()
     l0 = net.get_temporal_loss(ys[1].to(dev), ys[2].to(dev), ys[3].to(dev), z)

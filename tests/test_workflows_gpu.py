@@ -215,3 +215,20 @@ def test_fast_st_cli_train_then_convert(dev, project_root):
     diff = np.abs(got.astype(np.int32) - want.astype(np.int32))
     print(f"convert-image vs oracle: max |diff| {diff.max()}, > 0: {(diff > 0).mean():.2e}")
     assert diff.max() <= 1 and (diff > 0).mean() < 1e-2
+
+
+def test_convert_config3_b32_256_forward_vs_oracle(dev):
+    """BASELINE config 3 at full size: the ImageTransformNet forward of `fast_st
+    convert-image` batched 32 x 256^2 (stransfer/network.py:520-611, :798-832) vs the
+    oracle's fp32 forward on the same inputs and weights, 1e-4 relative (whole batch
+    and every image)."""
+    from oracle import reference_cpu as O
+    x = torch.from_numpy(W.synthetic_image(6000, (32, 3, 256, 256)))
+    net = network.ImageTransformNet(torch.rand([3, 256, 256]), batch_size=32)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)})
+    with torch.no_grad():
+        y = net(x.to(dev)).cpu()
+        yr = O.image_transform_net(4321)(x)
+    assert rel(y, yr) < 1e-4, rel(y, yr)
+    worst = max(rel(y[i], yr[i]) for i in range(32))
+    assert worst < 1e-4, worst
