@@ -531,6 +531,336 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
                                          reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
 }
 
+// ------------------------------------------------------------------ v2 main loop
+// One block per 64-cout x 256 (128) pixel tile, two blocks per CU.  K
+// runs in STEPS of (16-channel chunk, kernel row kh): the step's 3 taps x 64 couts of
+// split weights (12 KB) and the chunk's halo sit in double-buffered LDS, so the next
+// step's weights and a third of the next chunk's halo are converted and written while
+// this step's MFMAs run, with ONE barrier per step (v1: two barriers per chunk and the
+// whole restaging between them, and 36 KB of weights per chunk in one buffer).  Halo
+// buffers are sized to the exact item count (v1 pads to a multiple of 256).  Stride 1,
+// cin >= 16 only.
+template <int TW, int NI>
+struct C16v2 {
+  static constexpr int BM = 64, NPIX = 128 * NI, TH = NPIX / TW;
+  static constexpr int RH = TH + 2, RW = TW + 2, NPOS = RH * RW;
+  static constexpr int NITEM = 2 * NPOS;               // (channel group, position) units
+  static constexpr int NIT = (NITEM + 255) / 256;      // items per thread
+  static constexpr int HB = 2 * NITEM * 16;            // one halo buffer: hi plane, lo plane
+  static constexpr int WU = 3 * 4 * BM;                // weight units per step: [tap][P][cg][co]
+  static constexpr int NWU = WU / 256;
+  static constexpr int WB = WU * 16;                   // one weight buffer
+  static constexpr int LDS_BYTES = 2 * HB + 2 * WB;
+  static_assert(WU % 256 == 0, "weight units per thread");
+  static_assert(16 * NPIX * 4 + 16 * BM * 4 <= LDS_BYTES, "phase-2 staging fits");
+  static_assert(TW != 64 || NI != 2 || GramPlanes<256>::BYTES <= LDS_BYTES, "Gram planes fit");
+};
+
+// TR: operands swapped in the MFMAs (accumulators D[pixel][co]) and the transposed
+// forward epilogue (conv_epilogue_tr): 64 x 4 tiles, the plain forward epilogue only
+template <int TW, int LM, int P2, int NI, bool TR = false>
+__global__ void __launch_bounds__(256, 2)
+conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
+  using C = C16v2<TW, NI>;
+  constexpr bool RP = TW == 64 && NI == 2;  // row-pair tiles (fused pool / unpool)
+  static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
+  static_assert(P2 != 2, "1x1 mode: v1 kernel");
+  constexpr int BM = C::BM;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int co0 = blockIdx.y * BM;
+  const int n = blockIdx.z;
+  // the blocks of one XCD (blockIdx % 8 under round-robin placement) take consecutive
+  // tiles, so neighbouring halos meet in the same L2 (speed only)
+  const int G = gridDim.x;
+  const int first = (G & 7) == 0 ? (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3)
+                                 : (int)blockIdx.x;
+  if (first >= ntiles) return;
+
+  const int nchunks = cdiv(p.cin, 16);
+  const int nsteps = 3 * nchunks;
+  const int ex = amax_exp(read_amax(p.in_amax));
+  const int ew = amax_exp(read_amax(p.w_amax));
+  const float sx = __builtin_ldexpf(1.f, 15 - ex);
+  const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
+
+  const int plane_in = p.h * p.w;
+  const float* __restrict__ xn = p.x + (size_t)n * p.cin * plane_in;
+  const uint32_t pb = (uint32_t)plane_in * 4u, wrow = 4u * (uint32_t)p.w;
+
+  // weight units of a step: u = tid + q*256 -> (seg = tap*4 + P*2 + cg, co)
+  const int cout64 = rup(p.cout, 64);
+  const uint32_t chunk_bytes = (uint32_t)(36 * cout64 * 16);
+  const uint32_t step_bytes = (uint32_t)(12 * cout64 * 16);
+  uint32_t woff[C::NWU];
+#pragma unroll
+  for (int q = 0; q < C::NWU; ++q) {
+    const int u = tid + q * 256;
+    const int seg = u / BM, co = u - seg * BM;
+    woff[q] = (uint32_t)((seg * cout64 + co0 + co) * 16);
+  }
+  const char* __restrict__ wt16 = reinterpret_cast<const char*>(p.wt16);
+
+  uint32_t hoff[C::NIT];
+  int ty0 = 0, tx0 = 0;
+  auto halo_offsets = [&](int tile) {
+    ty0 = (tile / tiles_x) * C::TH;
+    tx0 = (tile % tiles_x) * TW;
+    const int vy0 = ty0 - 1, vx0 = tx0 - 1;
+#pragma unroll
+    for (int r = 0; r < C::NIT; ++r) {
+      const int idx = tid + r * 256;
+      const int cg = idx / C::NPOS, pos = idx - cg * C::NPOS;
+      const int rr = pos / C::RW, cc = pos - rr * C::RW;
+      const int vy = vy0 + rr, vx = vx0 + cc;
+      bool ok = idx < C::NITEM && vy >= 0 && vx >= 0 && vy < p.hv && vx < p.wv;
+      int sy = vy, sx_ = vx;
+      if (LM == STX_IN_RELU_POOL2) {
+        sy = 2 * vy;
+        sx_ = 2 * vx;
+      } else if (LM == STX_IN_UPSAMPLE2) {
+        sy = vy >> 1;
+        sx_ = vx >> 1;
+      } else if (LM == STX_IN_DILATE2) {
+        ok = ok && !((vy | vx) & 1);
+        sy = vy >> 1;
+        sx_ = vx >> 1;
+        ok = ok && sy < p.h && sx_ < p.w;
+      }
+      hoff[r] = ok ? (uint32_t)((cg * 8) * plane_in + sy * p.w + sx_) * 4u : BUF_OOB;
+    }
+  };
+
+  float hv[C::NIT][8];
+  f32x4 wreg[C::NWU];
+  auto ld_halo = [&](int chunk, int r) {
+    const int c0 = chunk * 16;
+    const auto rs = make_srd(xn + (size_t)c0 * plane_in, (uint32_t)(p.cin - c0) * pb);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint32_t o = hoff[r] + (uint32_t)c * pb;
+      if (LM == STX_IN_RELU_POOL2)
+        hv[r][c] = fmaxf(fmaxf(buf_ld(rs, o), buf_ld(rs, o + 4)),
+                         fmaxf(buf_ld(rs, o + wrow), buf_ld(rs, o + wrow + 4)));
+      else
+        hv[r][c] = buf_ld(rs, o);
+    }
+  };
+  auto st_halo = [&](int buf, int r) {
+    const int idx = tid + r * 256;
+    if (r + 1 < C::NIT || C::NITEM % 256 == 0 || idx < C::NITEM) {
+      f16x8 hi, lo;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float v = hv[r][c];
+        if (LM == STX_IN_RELU || LM == STX_IN_RELU_POOL2) v = fmaxf(v, 0.f);
+        v *= sx;
+        const _Float16 vh = (_Float16)v;
+        hi[c] = vh;
+        lo[c] = (_Float16)(v - (float)vh);
+      }
+      char* hb = smem + buf * C::HB;
+      *reinterpret_cast<f16x8*>(hb + idx * 16) = hi;
+      *reinterpret_cast<f16x8*>(hb + (C::NITEM + idx) * 16) = lo;
+    }
+  };
+  auto ld_w = [&](int step) {  // step = chunk * 3 + kh
+    const int chunk = step / 3, kh = step - 3 * chunk;
+    const auto rw = make_srd(reinterpret_cast<const float*>(wt16 + (size_t)chunk * chunk_bytes +
+                                                            (size_t)kh * step_bytes),
+                             step_bytes);
+#pragma unroll
+    for (int q = 0; q < C::NWU; ++q) wreg[q] = buf_ld4(rw, woff[q]);
+  };
+  auto st_w = [&](int buf) {
+    char* wbp = smem + 2 * C::HB + buf * C::WB;
+#pragma unroll
+    for (int q = 0; q < C::NWU; ++q)
+      *reinterpret_cast<f32x4*>(wbp + (tid + q * 256) * 16) = wreg[q];
+  };
+
+  // per-lane operand bases (bytes) relative to buffer 0
+  int boff[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    int ty, tx;
+    tile_pix<TW, RP, NI>(wave, j, l32, ty, tx);
+    boff[j] = (h * C::NPOS + ty * C::RW + tx) * 16;
+  }
+  const int aoff = 2 * C::HB + (h * BM + l32) * 16;
+
+  const int tile = first;
+  halo_offsets(tile);
+#pragma unroll
+  for (int r = 0; r < C::NIT; ++r) ld_halo(0, r);
+  ld_w(0);
+  {
+    // chunk 0's halo and step 0's weights -> buffers 0
+#pragma unroll
+    for (int r = 0; r < C::NIT; ++r) st_halo(0, r);
+    st_w(0);
+    // staged for step 0: step 1's weights, part 0 of chunk 1's halo
+    if (nsteps > 1) ld_w(1);
+    if (nchunks > 1) {
+#pragma unroll
+      for (int r = 0; r < C::NIT; r += 3) ld_halo(1, r);
+    }
+    __syncthreads();
+
+    f32x16 acc[2][NI];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    for (int c = 0; c < nchunks; ++c) {
+      const int hbo = (c & 1) * C::HB;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int s = 3 * c + k;
+        const int wbo = (s & 1) * C::WB;
+        const char* abase = smem + aoff + wbo;
+        const char* bbase[NI];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) bbase[j] = smem + boff[j] + hbo;
+        auto rdA = [&](int tl, int P, f16x8 (&a)[2]) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            a[i] = *reinterpret_cast<const f16x8*>(abase + (tl * 4 * BM + P * 2 * BM + i * 32) * 16);
+        };
+        auto rdB = [&](int tl, int P, f16x8 (&b)[NI]) {
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            b[j] = *reinterpret_cast<const f16x8*>(bbase[j] + (P * C::NITEM + k * C::RW + tl) * 16);
+        };
+        auto phase = [&](const f16x8 (&a)[2], const f16x8 (&b)[NI]) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+              acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_f16(b[j], a[i], acc[i][j], 0, 0, 0)
+                             : __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        };
+        f16x8 ahi[2], alo[2], bhi[NI], blo[NI];
+        rdA(0, 0, ahi);
+        rdB(0, 0, bhi);
+#pragma unroll
+        for (int tl = 0; tl < 3; ++tl) {
+          rdB(tl, 1, blo);
+          __builtin_amdgcn_sched_group_barrier(0x100, NI, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
+          phase(ahi, bhi);
+          rdA(tl, 1, alo);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
+          phase(ahi, blo);
+          f16x8 nah[2], nbh[NI];
+          if (tl + 1 < 3) {
+            rdA(tl + 1, 0, nah);
+            rdB(tl + 1, 0, nbh);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 + NI, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
+          phase(alo, bhi);
+          __builtin_amdgcn_sched_barrier(0);
+          if (tl == 0) {
+            // staged data -> the other buffers: step s+1's weights and part k of chunk
+            // c+1's halo (loaded one step ago); then the loads for step s+1's staging:
+            // step s+2's weights and the next part of the halo
+            if (s + 1 < nsteps) st_w((s + 1) & 1);
+            if (c + 1 < nchunks) {
+#pragma unroll
+              for (int r = k; r < C::NIT; r += 3) st_halo((c + 1) & 1, r);
+            }
+            if (s + 2 < nsteps) ld_w(s + 2);
+            const int cn = k < 2 ? c + 1 : c + 2;  // chunk of the next halo part
+            if (cn < nchunks) {
+#pragma unroll
+              for (int r = (k + 1) % 3; r < C::NIT; r += 3) ld_halo(cn, r);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (tl + 1 < 3) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) ahi[i] = nah[i];
+#pragma unroll
+            for (int j = 0; j < NI; ++j) bhi[j] = nbh[j];
+          }
+        }
+        __syncthreads();  // this step's reads done; the staged buffers are complete
+      }
+    }
+
+    EpiTile et{n, co0, ty0, tx0, 0, wave, h, l32};
+    et.tile = tile;
+    et.ntiles = ntiles;
+    if constexpr (TR) {
+      static_assert(TW == 64 && NI == 2 && P2 == 0, "transposed epilogue: 64 x 4 forward tiles");
+      if (p.relu_out)
+        conv_epilogue_tr<true>(acc, p, et, descale, smem);
+      else
+        conv_epilogue_tr<false>(acc, p, et, descale, smem);
+    } else if constexpr (P2 == 1) {
+      conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, true>(acc, p, et, descale,
+                                                       reinterpret_cast<float*>(smem),
+                                                       reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
+    } else {
+      if (!conv_epilogue_plain<TW, NI, RP>(acc, p, et, descale, smem))
+        conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, false>(acc, p, et, descale,
+                                                          reinterpret_cast<float*>(smem),
+                                                          reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
+    }
+  }
+}
+
+// STX_CONV_V2=0 selects the v1 main loop (read per launch, so a tool can A/B both in
+// one process)
+static bool v2_on() {
+  const char* e = getenv("STX_CONV_V2");
+  return !(e && atoi(e) == 0);
+}
+
+// STX_CONV_TR=1: the transposed accumulators + epilogue for the forward launches.  Off by
+// default: measured (tools/ab_v2.py, same process) conv1_2 fwd +pool+Gram 86.1 -> 87.1 us,
+// plain 66.1 -> 64.2, conv2_2 +pool 58.6 -> 60.7, B8 conv1_2 +pool 127.2 -> 133.4 -- the
+// register-resident Gram and 16-B stores do not pay for themselves in these launches
+static bool tr_on() {
+  const char* e = getenv("STX_CONV_TR");
+  return e && atoi(e) != 0;
+}
+
+template <int TW, int LM, int NI>
+static int launch16v2(const stx_conv_params& p, hipStream_t st) {
+  using C = C16v2<TW, NI>;
+  const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
+  const int ntiles = tiles_x * tiles_y;
+  const int gy = cdiv(p.cout, C::BM), gz = p.n;
+  dim3 grid(ntiles, gy, gz);
+  if constexpr (TW == 64 && NI == 2) {
+    if (tr_on() && !p.p2_z && !p.mask && !p.aux && !p.accumulate && !p.acc_scale && !p.up_dp &&
+        !p.pool_sum && p.wo % 4 == 0) {
+      hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI, true>), grid, dim3(256), 0, st,
+                         p, tiles_x, ntiles);
+      return check_launch("stx_conv2d(f16x3 v2, transposed)");
+    }
+  }
+  if constexpr (NI == 2 && LM == STX_IN_RAW) {
+    if (p.p2_z) {
+      hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 1, NI>), grid, dim3(256), 0, st, p,
+                         tiles_x, ntiles);
+      return check_launch("stx_conv2d(f16x3 v2 + phase 2)");
+    }
+  }
+    hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI>), grid, dim3(256), 0, st, p,
+                       tiles_x, ntiles);
+  return check_launch("stx_conv2d(f16x3 v2)");
+}
+
 static int dbg_mode() {
   static const int m = [] {
     const char* e = getenv("STX_CONV16_DBG");
@@ -550,6 +880,16 @@ static int stagger_mode() {
 template <int TW, int LM, int NI>
 static int launch16(const stx_conv_params& p, hipStream_t st) {
   using C = C16<TW, NI, LM == LM_S2 ? 2 : 1>;
+  if constexpr (LM != LM_S2) {
+    // the v2 main loop (stride 1, a 3x3 K loop; not the 1x1 Gram-backward mode, the
+    // split phase-2 variant or the profiling builds)
+    static const bool split_p2 = [] {
+      const char* e = getenv("STX_P2_SPLIT");
+      return e && atoi(e) != 0;
+    }();
+    if (v2_on() && p.cin > 0 && dbg_mode() == 0 && !(p.p2_z && split_p2))
+      return launch16v2<TW, LM, NI>(p, st);
+  }
   const int tiles_x0 = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
   const int tiles_x = tiles_x0 | (stagger_mode() << 24);
   dim3 grid(tiles_x0 * tiles_y, cdiv(p.cout, C::BM), p.n);

@@ -347,6 +347,246 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
+// ---------------------------------------------------------------------------------
+// conv1_1 (3x3, cin 3, cout 32 * MT) on the split MFMA with TRANSPOSED accumulators:
+// the MFMA operands are swapped (A = the im2col pixel fragment, B = the weight
+// fragment), so D[pixel][co] -- a lane holds one output channel and, per register r,
+// pixel 8(r/4) + 4h + r%4 of its 32-pixel N-block.  Two things follow:
+//  * stores are 16 B per lane (four consecutive pixels of one channel) instead of 4 B;
+//  * the fused Gram partial needs no LDS transpose: with the K (pixel) order of a
+//    16-deep step taken as the lane's own registers 8t..8t+7 (pixels 16t + 8(e/4) + 4h
+//    + e%4 -- a bijection onto [16t, 16t + 16) shared by both operands), the A fragment
+//    of channel block I and the B fragment of block J are both just the lane's split
+//    registers, so each wave adds all three upper 32 x 32 blocks of its own pixels,
+//    from registers, at its own power-of-two scale (no barrier per N-block); the four
+//    waves' partials are summed once per block through LDS in a fixed order.
+// wo % 4 == 0 (whole 16-B groups); otherwise the lane-per-pixel kernel above runs.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int MT>
+__global__ void __launch_bounds__(256, 2) conv_fewin16t_kernel(stx_conv_params p, int tiles_x) {
+  constexpr int KS = 3;
+  using F = Few16<KS>;
+  constexpr int KST = F::KST, NCO = 32 * MT;
+  constexpr int NW = KST * 2 * NCO * 8;
+  constexpr int NWR = (NW + 255) / 256;
+  constexpr bool GRAM = MT == 2;
+  __shared__ _Float16 tile16[2][F::NT];
+  __shared__ __attribute__((aligned(16))) _Float16 wa[KST][2][2][NCO][8];  // [t][P][h][co][e]
+  __shared__ float red[8];
+  __shared__ __attribute__((aligned(16))) float gsum[GRAM ? 4 * 3 * 1024 : 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x, n = blockIdx.z;
+  const int oy0 = ty * CF_TH, ox0 = tx * CF_TW;
+  constexpr int pad = KS / 2;
+  const int plane_in = p.h * p.w;
+  const float* __restrict__ xn = p.x + (size_t)n * CF_CIN * plane_in;
+
+  float xv[F::NR], wv[NWR];
+  float mx = 0.f, mw = 0.f;
+  {
+    const auto rx = make_srd(xn, (uint32_t)(CF_CIN * plane_in) * 4u);
+#pragma unroll
+    for (int r = 0; r < F::NR; ++r) {
+      const int i = tid + 256 * r;
+      const int ci = i / (F::RH * F::RW), rr = (i / F::RW) % F::RH, cc = i % F::RW;
+      const int y = oy0 - pad + rr, x = ox0 - pad + cc;
+      const bool ok = i < F::NIN && y >= 0 && y < p.h && x >= 0 && x < p.w;
+      xv[r] = buf_ld(rx, ok ? (uint32_t)(ci * plane_in + y * p.w + x) * 4u : BUF_OOB);
+      mx = fmaxf(mx, fabsf(xv[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < NWR; ++r) {
+      const int u = tid + 256 * r;
+      const int e = u & 7, co = (u >> 3) % NCO, hh = (u / (8 * NCO)) & 1, t = u / (16 * NCO);
+      const int k = 16 * t + 8 * hh + e;
+      const bool ok = u < NW && k < F::K && co < p.cout;
+      wv[r] = ok ? p.wt[(size_t)k * p.cout_pad + co] : 0.f;
+      mw = fmaxf(mw, fabsf(wv[r]));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    mw = fmaxf(mw, __shfl_xor(mw, o, 64));
+  }
+  if (lane == 0) {
+    red[wave] = mx;
+    red[4 + wave] = mw;
+  }
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  mw = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+  int ex = 0, ew = 0;
+  frexpf(mx, &ex);
+  frexpf(mw, &ew);
+  ex = min(max(ex, -60), 60);
+  ew = min(max(ew, -60), 60);
+  const float sx = __builtin_ldexpf(1.f, 15 - ex), sw = __builtin_ldexpf(1.f, 15 - ew);
+  const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
+#pragma unroll
+  for (int r = 0; r < F::NR; ++r) {
+    const int i = tid + 256 * r;
+    if (i < F::NIN) {
+      const int ci = i / (F::RH * F::RW), rr = (i / F::RW) % F::RH, cc = i % F::RW;
+      const int o = (ci * F::RH + rr) * F::RWP + cc;
+      const float v = xv[r] * sx;
+      const _Float16 vh = (_Float16)v;
+      tile16[0][o] = vh;
+      tile16[1][o] = (_Float16)(v - (float)vh);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NWR; ++r) {
+    const int u = tid + 256 * r;
+    if (u < NW) {
+      const int e = u & 7, co = (u >> 3) % NCO, hh = (u / (8 * NCO)) & 1, t = u / (16 * NCO);
+      const float v = wv[r] * sw;
+      const _Float16 vh = (_Float16)v;
+      wa[t][0][hh][co][e] = vh;
+      wa[t][1][hh][co][e] = (_Float16)(v - (float)vh);
+    }
+  }
+  __syncthreads();
+
+  const size_t plane = (size_t)p.ho * p.wo;
+  const uint32_t pb = (uint32_t)plane * 4u;
+  const auto ry = make_srd(p.y + (size_t)n * p.cout * plane, (uint32_t)p.cout * pb);
+  float bias_l[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int co = 32 * mt + l32;
+    bias_l[mt] = (p.bias && co < p.cout) ? p.bias[co] : 0.f;
+  }
+  uint32_t vmax_u = 0u;
+  const bool gram = GRAM && p.gram_part;
+  f32x16 g[3];
+#pragma unroll
+  for (int b3 = 0; b3 < 3; ++b3)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) g[b3][q] = 0.f;
+#pragma unroll 1
+  for (int b = 0; b < 4; ++b) {
+    const int row = 2 * wave + (b >> 1), col0 = 32 * (b & 1);
+    const int base = row * F::RWP + col0 + l32;  // the B-gather pixel of this lane
+    f32x16 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < KST; ++t) {
+      f16x8 bh, bl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int o0 = F::koff(16 * t + e), o1 = F::koff(16 * t + 8 + e);
+        const int o = h ? o1 : o0;
+        const bool ok = o >= 0;
+        const int oo = ok ? o : 0;
+        const _Float16 zh = (_Float16)0.f;
+        bh[e] = ok ? tile16[0][base + oo] : zh;
+        bl[e] = ok ? tile16[1][base + oo] : zh;
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(&wa[t][0][h][32 * mt + l32][0]);
+        const f16x8 al = *reinterpret_cast<const f16x8*>(&wa[t][1][h][32 * mt + l32][0]);
+        // D[pixel][co]: the pixel fragment is the A operand, the weights the B operand
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh, ah, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl, ah, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh, al, acc[mt], 0, 0, 0);
+      }
+    }
+    // outputs: lane's channel 32 mt + l32; registers 4q..4q+3 -> pixels 8q + 4h + 0..3
+    const int oy = oy0 + row;
+    uint32_t wmax = 0u;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int co = 32 * mt + l32;
+      const bool cok = co < p.cout;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ox = ox0 + col0 + 8 * q + 4 * h;
+        const bool in = cok && oy < p.ho && ox < p.wo;
+        f32x4 v4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = fmaf(acc[mt][4 * q + e], descale, bias_l[mt]);
+          if (p.relu_out) v = fmaxf(v, 0.f);
+          v4[e] = v;
+          const uint32_t bits = in ? (__float_as_uint(v) & 0x7fffffffu) : 0u;
+          vmax_u = max(vmax_u, bits);
+          wmax = max(wmax, bits);
+          acc[mt][4 * q + e] = in ? v : 0.f;  // the Gram's copy: pixels outside count 0
+        }
+        const uint32_t off = in ? (uint32_t)co * pb + (uint32_t)(oy * p.wo + ox) * 4u : BUF_OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v4), ry, off, 0, 0);
+      }
+    }
+    if constexpr (GRAM) if (gram) {
+      // this wave's 64 channels x 32 pixels at the wave's own power-of-two scale
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
+      int e2 = 0;
+      frexpf(__uint_as_float(wmax), &e2);
+      e2 = min(max(e2, -60), 60);
+      const float gs = __builtin_ldexpf(1.f, 15 - e2);
+      f16x8 fh[2][2], fl[2][2];  // [mt][t]
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = acc[mt][8 * t + e] * gs;
+            const _Float16 vh = (_Float16)v;
+            fh[mt][t][e] = vh;
+            fl[mt][t][e] = (_Float16)(v - (float)vh);
+          }
+      const float ginv = __builtin_ldexpf(1.f, 2 * e2 - 30);
+#pragma unroll
+      for (int b3 = 0; b3 < 3; ++b3) {
+        const int I = b3 == 2 ? 1 : 0, J = b3 == 0 ? 0 : 1;
+        f32x16 gc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) gc[q] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[I][t], fh[J][t], gc, 0, 0, 0);
+          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[I][t], fl[J][t], gc, 0, 0, 0);
+          gc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl[I][t], fh[J][t], gc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) g[b3][q] = fmaf(gc[q], ginv, g[b3][q]);
+      }
+    }
+  }
+  if constexpr (GRAM) if (gram) {
+    // the four waves' partials, summed in wave order; waves 0..2 store one block each
+#pragma unroll
+    for (int b3 = 0; b3 < 3; ++b3)
+      *reinterpret_cast<f32x16*>(&gsum[((wave * 3 + b3) * 64 + lane) * 16]) = g[b3];
+    __syncthreads();
+    if (wave < 3) {
+      f32x16 s = *reinterpret_cast<const f32x16*>(&gsum[((0 * 3 + wave) * 64 + lane) * 16]);
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const f32x16 o = *reinterpret_cast<const f32x16*>(&gsum[((w * 3 + wave) * 64 + lane) * 16]);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) s[q] += o[q];
+      }
+      gram_store(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, s, wave, h,
+                 l32);
+    }
+  }
+  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
+}
+
+static bool few16t_on() {
+  const char* e = getenv("STX_FEW16T");
+  return !(e && atoi(e) == 0);
+}
+
 static bool few16_on() {
   static const bool on = [] {
     const char* e = getenv("STX_FEW16");
@@ -360,7 +600,10 @@ int launch_fewin(const stx_conv_params& p, hipStream_t st) {
   const int tiles_x = (p.wo + CF_TW - 1) / CF_TW, tiles_y = (p.ho + CF_TH - 1) / CF_TH;
   // 9x9 (K = 243) stays on the fp32 kernel: its B gathers (16 16-bit LDS reads per
   // K step) cost more than the matrix cycles saved (150 vs 105 us, ITN conv0 B8 256^2)
-  if (KS == 3 && few16_on())
+  if (KS == 3 && few16_on() && few16t_on() && p.wo % 4 == 0)
+    hipLaunchKernelGGL((conv_fewin16t_kernel<MT>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256),
+                       0, st, p, tiles_x);
+  else if (KS == 3 && few16_on())
     hipLaunchKernelGGL((conv_fewin16_kernel<KS, MT>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256),
                        0, st, p, tiles_x);
   else

@@ -71,6 +71,10 @@ def _three_way(style, batch, sd, dev, monkeypatch, max_flips):
     s_np, b_np = style.numpy(), batch.numpy()
     ni, nv = R.natural_branches(sd, vgg, b_np)
     flips = R.count_flips(bi, ni) + R.count_flips(bv, nv)
+    # the fp32 reference's own flips against the same fp64 run (the count an fp32
+    # implementation is entitled to)
+    ni32, nv32 = R.natural_branches(sd, vgg, b_np, torch.float32)
+    flips32 = R.count_flips(ni32, ni) + R.count_flips(nv32, nv)
     n_el = sum(int(m.numel()) for m in bi) + sum(int(m[0].numel()) for m in bv)
     g64, l64 = R.forced_grads(sd, vgg, s_np, b_np, bi, bv, torch.float64)
     g32, _ = R.forced_grads(sd, vgg, s_np, b_np, bi, bv, torch.float32)
@@ -85,10 +89,10 @@ def _three_way(style, batch, sd, dev, monkeypatch, max_flips):
         worst.append((e / max(r, FLOOR), e, r, k))
         assert e <= max(K * r, FLOOR), f"{k}: hip {e:.2e} vs fp32 {r:.2e} (forced branches)"
     worst.sort()
-    print(f"flips {flips} of {n_el}; loss hip {loss_hip:.7g} fp64 {l64:.7g}; "
-          f"worst (ratio, hip, fp32, param): {worst[-3:]}")
+    print(f"flips {flips} (fp32 reference: {flips32}) of {n_el}; loss hip {loss_hip:.7g} "
+          f"fp64 {l64:.7g}; worst (ratio, hip, fp32, param): {worst[-3:]}")
     assert abs(loss_hip - l64) <= 1e-4 * abs(l64)
-    assert flips <= max_flips, flips
+    assert flips <= max(3 * flips32, max_flips), (flips, flips32)
     return flips
 
 
@@ -97,7 +101,7 @@ def test_itn_grads_forced_branches_golden(dev, monkeypatch):
     d = np.load(os.path.join(GOLDEN, "itn.npz"))
     sd = W.itn_synthetic(4321)
     _three_way(torch.from_numpy(d["style"]), torch.from_numpy(d["batch"]), sd, dev,
-               monkeypatch, max_flips=4)
+               monkeypatch, max_flips=8)
 
 
 def test_fast_st_step_config4_b8_256_forced_branches(dev, monkeypatch):
@@ -105,7 +109,7 @@ def test_fast_st_step_config4_b8_256_forced_branches(dev, monkeypatch):
     of the 8 data-parallel ranks trains)."""
     style = torch.from_numpy(W.synthetic_image(41, (1, 3, 256, 256)))
     batch = torch.from_numpy(W.synthetic_image(42, (8, 3, 256, 256)))
-    _three_way(style, batch, W.itn_synthetic(4321), dev, monkeypatch, max_flips=64)
+    _three_way(style, batch, W.itn_synthetic(4321), dev, monkeypatch, max_flips=32)
 
 
 # --------------------------------------------------------------- block-level fp64

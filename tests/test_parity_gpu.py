@@ -216,10 +216,13 @@ def test_gatys_config2_512_engine_golden(dev):
     # style x5 (unweighted), content; the feature loss is computed but not optimised
     assert rel(per, d["losses_it1"]) < 1e-4, (per, d["losses_it1"])
     errs = {}
-    for k, v in (("dx1", dx1), ("dx3", dx3), ("upd3", x3 - c0)):
+    # iteration 1's gradient: 2.5x; after two Adam steps (~lr*sign(g) per pixel, so a pixel
+    # whose |g| is at rounding level steps either way in any fp32 run) the trajectories of
+    # fp32 runs fan out from the fp64 one by their own sign flips: 4x
+    for k, v, f in (("dx1", dx1, 2.5), ("dx3", dx3, 4.0), ("upd3", x3 - c0, 4.0)):
         e, r = rel(nproj(v), d[f"{k}_proj_64"]), rel(d[f"{k}_proj"], d[f"{k}_proj_64"])
         errs[k] = (e, r)
-        assert e <= max(2.5 * r, 1e-5), (k, e, r)
+        assert e <= max(f * r, 1e-5), (k, e, r)
     s_hip = (x1 - c0).ravel() > 0
     s_ref = np.unpackbits(d["upd1_sign"])[:s_hip.size].astype(bool)
     flips = float(np.mean(s_hip != s_ref))
