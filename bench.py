@@ -58,28 +58,34 @@ PEAK_SPLIT_TFLOPS = PEAK_F16_MFMA_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0
 
 
-# the dominant kernel instance and its per-launch HBM traffic (rocprofv3 PMC passes
-# of tools/gpu_round.sh, summarised by tools/pmc_summary.py)
-ROOFLINE_KERNEL = "conv3x3_f16x3_kernel<64, 1, 0, 0, 2>"
-PMC_FILE = os.path.join(REPO, "profiles", "r2_pmc_conv1_2_fwd.json")
-# algorithmic bytes of conv1_2 fwd @512^2: read Z1 + write Z2 (64 MiB each) + the fused
-# relu+pool output P2 (16 MiB) + weights (fp16 hi/lo slab) + bias
-# conv1_2 forward at 512^2 as the iteration launches it: Z1 in, Z2 + relu/pool(Z2) out,
-# weights + bias, and the fused Gram partials (1024 tiles x 64 x 64 fp32)
+# the roofline kernel instance and its per-launch HBM traffic (rocprofv3 FETCH_SIZE /
+# WRITE_SIZE passes of tools/pmc_r3.sh over an eager Gatys iteration, calibrated on
+# kernels of known byte count: tools/pmc_r3_summary.py -> profiles/r3_pmc.json)
+ROOFLINE_KERNEL = "conv3x3_f16x3_v2_kernel<64, 1, 0, 2, false>"
+PMC_FILE = os.path.join(REPO, "profiles", "r3_pmc.json")
+# algorithmic bytes of conv1_2 fwd @512^2 as the iteration launches it: Z1 in, Z2 and the
+# fused relu+pool output P2 out, weights + bias, and the fused Gram partials (1024 tiles
+# x 64 x 64 fp32)
 CONV1_2_BYTES = (2 * 64 * 512 * 512 * 4 + 64 * 256 * 256 * 4 + 64 * 64 * 9 * 4 + 64 * 4
                  + 1024 * 64 * 64 * 4)
 
 
 def pmc_traffic():
-    """(bytes per launch, source) of ROOFLINE_KERNEL from the committed PMC record."""
+    """(bytes per launch, source, record) of ROOFLINE_KERNEL at 512^2 (grid 1024 blocks of
+    256 threads) from the committed PMC record: FETCH_SIZE calibrated with the 4-B/lane
+    read factor (the halo loads that carry the bytes), WRITE_SIZE with the 4-B store
+    factor."""
     try:
         with open(PMC_FILE) as f:
             rec = json.load(f)
     except OSError:
-        return None, None
-    if rec.get("kernel") != ROOFLINE_KERNEL:
-        return None, None
-    return round(rec["bytes_raw"]), os.path.relpath(PMC_FILE, REPO)
+        return None, None, None
+    for r in rec.get("kernels", []):
+        if ROOFLINE_KERNEL in r["kernel"] and r["grid"] == 1024 * 256 and \
+                "fetch_bytes_cal4" in r and "write_bytes_cal4" in r:
+            return (round(r["fetch_bytes_cal4"] + r["write_bytes_cal4"]),
+                    os.path.relpath(PMC_FILE, REPO), r)
+    return None, None, None
 
 
 def conv_gflop(cin, cout, h, w, ks=3):
@@ -202,10 +208,24 @@ def gatys_leg(args, world, rank, dev):
         zam = V.slot(eng.st.amax, 2).clone()
         gram = dict(ms=event_avg_ms(lambda: ops.gram(z2, z_amax=zam), reps=20), fused=False)
     gram.update(gflop=gf_gram, bytes=64 * H * H * 4)
+    # the iteration's largest launch: conv1_2's data gradient with the fused Gram-backward
+    # phase (dZ1 = mask * conv1_2^T(dZ2) + A1 Z1, vgg.loss_backward), same buffers and scales
+    st, sc = eng.st, eng.scratch
+    dz1 = torch.empty_like(sc["dz1"])
+    am_b = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+
+    def dgrad12():
+        return feat.dgrad(1, sc["dz2"], dz1, mask=st.z[0], p2_z=st.z[0], p2_coef=st.coef[0],
+                          p2_scale=None, in_amax=V.slot(st.amax, 9), out_amax=am_b,
+                          p2_amax=V.slot(st.amax, 1))
+    dg_ms = event_avg_ms(dgrad12, reps=20)
+    dg_gf = gf_conv + 2.0 * 64 * 64 * H * H / 1e9
     loss = float(eng.total)
     return dict(rate=rate, dt=dt, loss=loss, run=run, kernel=dict(fwd_ms=fwd_ms, gflop=gf,
                                                          gflop_conv=gf_conv, tflops=achieved,
-                                                         gram_fused=gp is not None),
+                                                         gram_fused=gp is not None,
+                                                         dg_ms=dg_ms, dg_gflop=dg_gf,
+                                                         dg_tflops=dg_gf / (dg_ms * 1e-3) / 1e3),
                 gram=gram)
 
 
@@ -448,7 +468,7 @@ def main():
         cpu = cpu_baseline(args)
     if rank == 0:
         k = g["kernel"]
-        traffic_bytes, traffic_src = pmc_traffic()
+        traffic_bytes, traffic_src, traffic_rec = pmc_traffic()
         res = {
             "metric": METRIC,
             "value": round(g["rate"], 3),
@@ -488,9 +508,21 @@ def main():
                                          + (" + Gram 2*64*64*H*W" if k["gram_fused"] else ""),
                 "fwd_ms": round(k["fwd_ms"], 4),
                 "traffic_source": traffic_src,
+                "traffic_raw": None if traffic_rec is None else {
+                    "fetch": traffic_rec.get("FETCH_SIZE_bytes_raw"),
+                    "write": traffic_rec.get("WRITE_SIZE_bytes_raw")},
                 "algorithmic_bytes": CONV1_2_BYTES if args.size == 512 else None,
                 "iteration_tflops": round(GATYS_GFLOP.get(args.size, float("nan")) * g["rate"]
                                           / world / 1e3, 3),
+                "dominant_kernel": {
+                    "kernel": "conv3x3_f16x3_v2_kernel<64, 0, 1, 2> (conv1_2 data gradient "
+                              f"@ {args.size}^2 with the fused Gram-backward phase: dZ1 = "
+                              "[Z1 > 0] conv1_2^T(dZ2) + A1 Z1; the iteration's longest launch)",
+                    "achieved": round(k["dg_tflops"], 3),
+                    "frac": round(k["dg_tflops"] / PEAK_SPLIT_TFLOPS, 4),
+                    "per_launch_gflop": round(k["dg_gflop"], 3),
+                    "ms": round(k["dg_ms"], 4),
+                },
             },
             "gram_roofline": {
                 "kernel": ("fused into conv1_2's epilogue (launch with gram_part minus launch "

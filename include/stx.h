@@ -294,6 +294,42 @@ int stx_style_loss_from_parts(const float* parts, int nparts, const float* targe
                               float* g_out, float* coef, float* loss, int b, int c, int hw,
                               int target_batched, float weight, float diag_alpha, void* ws,
                               size_t ws_bytes, void* stream);
+/* Deferred Gram finalizes.  The *_deferred forms of stx_style_loss,
+ * stx_style_content_loss and stx_style_loss_from_parts launch only their partial
+ * kernel(s) (if any) and describe the finalize (G, coef, loss partials, the fused content
+ * MSE) in *job; stx_gram_finalize_batch then runs up to STX_FIN_MAX such finalizes -- the
+ * five StyleLoss taps of a forward -- in ONE launch, block for block the same arithmetic
+ * (bit-identical to the immediate forms).  The loss partials land where
+ * stx_style_loss_parts says; reduce them with stx_loss_finalize. */
+#define STX_FIN_MAX 8
+typedef struct stx_gram_fin_job {
+  const float* parts;      /* partial slabs [b][ntiles][nsplit][64][64] */
+  float* g_out;            /* optional G */
+  const float* target;
+  float* coef;
+  float* loss_parts;
+  const float* mse_parts;  /* fused content pass (or NULL) */
+  float* mse_out;
+  long long t_bstride;
+  double mse_n;
+  float scale, cA, alpha;
+  int c, nsplit, b, cpad, mse_nparts;
+} stx_gram_fin_job;
+int stx_style_loss_deferred(const float* z, const float* target, float* coef, int b, int c,
+                            int hw, int target_batched, float weight, float diag_alpha,
+                            const float* z_amax, void* ws, size_t ws_bytes, stx_gram_fin_job* job,
+                            void* stream);
+int stx_style_content_loss_deferred(const float* z, const float* target, float* coef, int b,
+                                    int c, int hw, int target_batched, float weight,
+                                    float diag_alpha, const float* z_amax, const float* content,
+                                    float* mse_out, void* ws, size_t ws_bytes,
+                                    stx_gram_fin_job* job, void* stream);
+int stx_style_loss_from_parts_deferred(const float* parts, int nparts, const float* target,
+                                       float* coef, int b, int c, int hw, int target_batched,
+                                       float weight, float diag_alpha, void* ws, size_t ws_bytes,
+                                       stx_gram_fin_job* job, void* stream);
+int stx_gram_finalize_batch(const stx_gram_fin_job* jobs, int njobs, void* stream);
+
 /* *out = sum_i w_host[i] * s[i]   (k <= 16 device scalars, fixed order) */
 int stx_loss_combine(const float* s, int k, const float* w_host, float* out, void* stream);
 

@@ -70,6 +70,17 @@ class LossParts(C.Structure):
     _fields_ = [("parts", vp * 8), ("nparts", i32 * 8), ("inv", f32 * 8), ("k", i32)]
 
 
+class GramFinJob(C.Structure):
+    """Mirror of `stx_gram_fin_job` (include/stx.h)."""
+    _fields_ = [("parts", vp), ("g_out", vp), ("target", vp), ("coef", vp), ("loss_parts", vp),
+                ("mse_parts", vp), ("mse_out", vp), ("t_bstride", i64), ("mse_n", C.c_double),
+                ("scale", f32), ("cA", f32), ("alpha", f32), ("c", i32), ("nsplit", i32),
+                ("b", i32), ("cpad", i32), ("mse_nparts", i32)]
+
+
+STX_FIN_MAX = 8
+
+
 # name -> (restype, argtypes); every symbol include/stx.h declares
 SIGNATURES = {
     "stx_version": (i32, []),
@@ -111,6 +122,13 @@ SIGNATURES = {
     "stx_style_content_ws": (sz, [i32, i32, i32]),
     "stx_style_content_loss": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, vp, vp,
                                      vp, sz, vp]),
+    "stx_style_loss_deferred": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, vp, sz,
+                                      C.POINTER(GramFinJob), vp]),
+    "stx_style_content_loss_deferred": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, vp,
+                                              vp, vp, sz, C.POINTER(GramFinJob), vp]),
+    "stx_style_loss_from_parts_deferred": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, f32, f32,
+                                                 vp, sz, C.POINTER(GramFinJob), vp]),
+    "stx_gram_finalize_batch": (i32, [C.POINTER(GramFinJob), i32, vp]),
     "stx_gram_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, f32, i32, vp]),
     "stx_mse_ws": (sz, [i64]),
     "stx_mse": (i32, [vp, vp, i64, i32, i32, vp, vp, f32, vp, sz, vp]),

@@ -580,17 +580,17 @@ static bool gram_tri_on(int c, int hw) {
 // left the reduction latency-bound: 11.8 us for the 16.8 MB of C=64 @ 512^2 partials.)
 constexpr int FEL = 64, FKL = 64, FNT = FEL / 4 * FKL;  // elements, split-lanes, threads
 constexpr int FSUB = GT * GT / FEL;   // blocks per tile
-__global__ void __launch_bounds__(FNT)
-gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scale,
-                     float* __restrict__ g_out, const float* __restrict__ target, long long t_bstride,
-                     float* __restrict__ coef, int cpad, float cA, float alpha,
-                     float* __restrict__ loss_parts, const float* __restrict__ mse_parts = nullptr,
-                     int mse_nparts = 0, double mse_n = 1.0, float* __restrict__ mse_out = nullptr) {
+// block (bx, by) of a finalize over grid (ntu * FSUB, b)
+__device__ __forceinline__ void gram_finalize_body(
+    const float* __restrict__ ws, int c, int nsplit, float scale, float* __restrict__ g_out,
+    const float* __restrict__ target, long long t_bstride, float* __restrict__ coef, int cpad,
+    float cA, float alpha, float* __restrict__ loss_parts, const float* __restrict__ mse_parts,
+    int mse_nparts, double mse_n, float* __restrict__ mse_out, int bx, int by) {
   __shared__ float part[FKL][FEL + 1];
   __shared__ float red[FNT / 64];
   // block (0, 0) also finalizes the content / feature MSE partials of a fused content
   // pass (gram_tri_f16_kernel<128, true>): the launch a separate mse2 finalize would take
-  if (mse_out && blockIdx.x == 0 && blockIdx.y == 0) {
+  if (mse_out && bx == 0 && by == 0) {
     float s = 0.f, sr = 0.f;
     for (int i = threadIdx.x; i < mse_nparts; i += FNT) {
       s += mse_parts[2 * i];
@@ -606,10 +606,10 @@ gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scal
     }
   }
   const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
-  const int tile = blockIdx.x / FSUB, sub = blockIdx.x % FSUB;
+  const int tile = bx / FSUB, sub = bx % FSUB;
   int I, J;
   tile_ij(tile, nt, I, J);
-  const int b = blockIdx.y;
+  const int b = by;
   const float* src = ws + ((size_t)b * ntu + tile) * nsplit * (GT * GT) + sub * FEL;
   const int q4 = threadIdx.x % (FEL / 4), kl = threadIdx.x / (FEL / 4);
   {
@@ -658,8 +658,37 @@ gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scal
   }
   if (target) {
     const float t = block_sum<FNT>(sq, red);
-    if (threadIdx.x == 0) loss_parts[(size_t)b * ntu * FSUB + blockIdx.x] = t;
+    if (threadIdx.x == 0) loss_parts[(size_t)b * ntu * FSUB + bx] = t;
   }
+}
+
+__global__ void __launch_bounds__(FNT)
+gram_finalize_kernel(const float* __restrict__ ws, int c, int nsplit, float scale,
+                     float* __restrict__ g_out, const float* __restrict__ target, long long t_bstride,
+                     float* __restrict__ coef, int cpad, float cA, float alpha,
+                     float* __restrict__ loss_parts, const float* __restrict__ mse_parts = nullptr,
+                     int mse_nparts = 0, double mse_n = 1.0, float* __restrict__ mse_out = nullptr) {
+  gram_finalize_body(ws, c, nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha,
+                     loss_parts, mse_parts, mse_nparts, mse_n, mse_out, blockIdx.x, blockIdx.y);
+}
+
+// the finalizes of several style losses (one per VGG tap) in ONE launch: block ranges
+// per job, each block the body of gram_finalize_kernel (same arithmetic, same order)
+struct FinBatch {
+  stx_gram_fin_job job[STX_FIN_MAX];
+  int blk0[STX_FIN_MAX + 1];
+  int njobs;
+};
+
+__global__ void __launch_bounds__(FNT) gram_finalize_batch_kernel(FinBatch fb) {
+  int j = 0;
+  while (j + 1 < fb.njobs && (int)blockIdx.x >= fb.blk0[j + 1]) ++j;
+  const stx_gram_fin_job& q = fb.job[j];
+  const int local = blockIdx.x - fb.blk0[j];
+  const int nt = cdiv(q.c, GT), nbx = nt * (nt + 1) / 2 * FSUB;
+  gram_finalize_body(q.parts, q.c, q.nsplit, q.scale, q.g_out, q.target, q.t_bstride, q.coef,
+                     q.cpad, q.cA, q.alpha, q.loss_parts, q.mse_parts, q.mse_nparts, q.mse_n,
+                     q.mse_out, local % nbx, local / nbx);
 }
 
 // one wave: the fixed-order sum of n loss partials (4 lane-strided accumulators, then a
@@ -761,10 +790,35 @@ struct MseCompanion {
   size_t parts_bytes;
 };
 
+static void fill_job(stx_gram_fin_job* job, const float* parts, int c, int nsplit, float scale,
+                     float* g_out, const float* target, long long t_bstride, float* coef,
+                     int cpad, float cA, float alpha, float* loss_parts, const float* mse_parts,
+                     int mse_nparts, double mse_n, float* mse_out, int b) {
+  *job = stx_gram_fin_job{};
+  job->parts = parts;
+  job->c = c;
+  job->nsplit = nsplit;
+  job->b = b;
+  job->scale = scale;
+  job->g_out = g_out;
+  job->target = target;
+  job->t_bstride = t_bstride;
+  job->coef = coef;
+  job->cpad = cpad;
+  job->cA = cA;
+  job->alpha = alpha;
+  job->loss_parts = loss_parts;
+  job->mse_parts = mse_parts;
+  job->mse_nparts = mse_nparts;
+  job->mse_n = mse_n;
+  job->mse_out = mse_out;
+}
+
 static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_out,
                     const float* target, long long t_bstride, float* coef, float cA, float alpha, float* loss,
                     float loss_inv, const float* z_amax, void* ws, size_t ws_bytes,
-                    hipStream_t st, const MseCompanion* mse = nullptr) {
+                    hipStream_t st, const MseCompanion* mse = nullptr,
+                    stx_gram_fin_job* defer = nullptr) {
   if (b <= 0 || c <= 0 || hw <= 0 || !z) {
     set_error("gram: invalid dims");
     return STX_E_INVALID;
@@ -815,11 +869,17 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
     hipLaunchKernelGGL(gram_partial_kernel, dim3(nsplit, ntu, b), dim3(256), 0, st, z, slabs, c,
                        hw, nsplit, split_len);
   const int cpad = stx_gram_coef_pitch(c);
-  hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(FNT), 0, st, slabs, c,
-                     nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts,
-                     mse_fin ? mse_fin->parts : nullptr, mse_nparts, (double)b * c * hw,
-                     mse_fin ? mse_fin->out : nullptr);
-  if (target && loss)
+  if (defer) {  // the finalize joins a stx_gram_finalize_batch launch
+    fill_job(defer, slabs, c, nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha,
+             parts, mse_fin ? mse_fin->parts : nullptr, mse_nparts, (double)b * c * hw,
+             mse_fin ? mse_fin->out : nullptr, b);
+  } else {
+    hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(FNT), 0, st, slabs, c,
+                       nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts,
+                       mse_fin ? mse_fin->parts : nullptr, mse_nparts, (double)b * c * hw,
+                       mse_fin ? mse_fin->out : nullptr);
+  }
+  if (target && loss && !defer)
     hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, parts, b * ntu * FSUB,
                        loss_inv, loss);
   if (mse) {  // not fused (another Gram kernel ran): the separate content pass
@@ -891,9 +951,10 @@ extern "C" int stx_gram(const float* z, float* g, int b, int c, int hw, float sc
                   (hipStream_t)stream);
 }
 
-extern "C" int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
-                              float* loss, int b, int c, int hw, int target_batched, float weight, float diag_alpha,
-                              const float* z_amax, void* ws, size_t ws_bytes, void* stream) {
+static int style_loss_impl(const float* z, const float* target, float* g_out, float* coef,
+                           float* loss, int b, int c, int hw, int target_batched, float weight,
+                           float diag_alpha, const float* z_amax, void* ws, size_t ws_bytes,
+                           void* stream, stx_gram_fin_job* defer) {
   if (!target) {  // loss == NULL: partials stay in ws (stx_style_loss_parts)
     set_error("stx_style_loss: target is required");
     return STX_E_INVALID;
@@ -910,7 +971,27 @@ extern "C" int stx_style_loss(const float* z, const float* target, float* g_out,
                        dim3(256), 0, st, coef, cnt);
   }
   return gram_run(z, b, c, hw, scale, g_out, target, target_batched ? (long long)c * c : 0, coef, cA, diag_alpha, loss,
-                  (float)(1.0 / ((double)b * c * c)), z_amax, ws, ws_bytes, st);
+                  (float)(1.0 / ((double)b * c * c)), z_amax, ws, ws_bytes, st, nullptr, defer);
+}
+
+extern "C" int stx_style_loss(const float* z, const float* target, float* g_out, float* coef,
+                              float* loss, int b, int c, int hw, int target_batched, float weight,
+                              float diag_alpha, const float* z_amax, void* ws, size_t ws_bytes,
+                              void* stream) {
+  return style_loss_impl(z, target, g_out, coef, loss, b, c, hw, target_batched, weight,
+                         diag_alpha, z_amax, ws, ws_bytes, stream, nullptr);
+}
+
+extern "C" int stx_style_loss_deferred(const float* z, const float* target, float* coef, int b,
+                                       int c, int hw, int target_batched, float weight,
+                                       float diag_alpha, const float* z_amax, void* ws,
+                                       size_t ws_bytes, stx_gram_fin_job* job, void* stream) {
+  if (!job) {
+    set_error("stx_style_loss_deferred: job is required");
+    return STX_E_INVALID;
+  }
+  return style_loss_impl(z, target, nullptr, coef, nullptr, b, c, hw, target_batched, weight,
+                         diag_alpha, z_amax, ws, ws_bytes, stream, job);
 }
 
 static size_t style_content_parts_bytes(int b, int c, int hw) {
@@ -922,11 +1003,11 @@ extern "C" size_t stx_style_content_ws(int b, int c, int hw) {
   return rup((long long)gram_ws_bytes(b, c, hw), 256) + style_content_parts_bytes(b, c, hw);
 }
 
-extern "C" int stx_style_content_loss(const float* z, const float* target, float* coef,
-                                      float* loss, int b, int c, int hw, int target_batched,
-                                      float weight, float diag_alpha, const float* z_amax,
-                                      const float* content, float* mse_out, void* ws,
-                                      size_t ws_bytes, void* stream) {
+static int style_content_impl(const float* z, const float* target, float* coef, float* loss,
+                              int b, int c, int hw, int target_batched, float weight,
+                              float diag_alpha, const float* z_amax, const float* content,
+                              float* mse_out, void* ws, size_t ws_bytes, void* stream,
+                              stx_gram_fin_job* defer) {
   if (!target || !content || !mse_out) {
     set_error("stx_style_content_loss: target, content and mse_out are required");
     return STX_E_INVALID;
@@ -949,14 +1030,36 @@ extern "C" int stx_style_content_loss(const float* z, const float* target, float
   MseCompanion m{content, mse_out, (float*)((char*)ws + gb), ws_bytes - gb};
   return gram_run(z, b, c, hw, scale, nullptr, target, target_batched ? (long long)c * c : 0,
                   coef, cA, diag_alpha, loss, (float)(1.0 / ((double)b * c * c)), z_amax, ws, gb,
-                  st, &m);
+                  st, &m, defer);
 }
 
-extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const float* target,
-                                         float* g_out, float* coef, float* loss, int b, int c,
-                                         int hw, int target_batched, float weight,
-                                         float diag_alpha, void* ws, size_t ws_bytes,
-                                         void* stream) {
+extern "C" int stx_style_content_loss(const float* z, const float* target, float* coef,
+                                      float* loss, int b, int c, int hw, int target_batched,
+                                      float weight, float diag_alpha, const float* z_amax,
+                                      const float* content, float* mse_out, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  return style_content_impl(z, target, coef, loss, b, c, hw, target_batched, weight, diag_alpha,
+                            z_amax, content, mse_out, ws, ws_bytes, stream, nullptr);
+}
+
+extern "C" int stx_style_content_loss_deferred(const float* z, const float* target, float* coef,
+                                               int b, int c, int hw, int target_batched,
+                                               float weight, float diag_alpha,
+                                               const float* z_amax, const float* content,
+                                               float* mse_out, void* ws, size_t ws_bytes,
+                                               stx_gram_fin_job* job, void* stream) {
+  if (!job) {
+    set_error("stx_style_content_loss_deferred: job is required");
+    return STX_E_INVALID;
+  }
+  return style_content_impl(z, target, coef, nullptr, b, c, hw, target_batched, weight,
+                            diag_alpha, z_amax, content, mse_out, ws, ws_bytes, stream, job);
+}
+
+static int from_parts_impl(const float* gparts, int nparts, const float* target, float* g_out,
+                           float* coef, float* loss, int b, int c, int hw, int target_batched,
+                           float weight, float diag_alpha, void* ws, size_t ws_bytes,
+                           void* stream, stx_gram_fin_job* defer) {
   if (!gparts || !target || nparts <= 0 || b <= 0 || c <= 0 || c > GT || hw <= 0) {
     set_error("stx_style_loss_from_parts: invalid arguments (c <= 64)");
     return STX_E_INVALID;
@@ -976,6 +1079,12 @@ extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const 
                        dim3(256), 0, st, coef, cnt);
   }
   float* lparts = (float*)((char*)ws + gram_parts_offset(b, c, hw, nullptr));
+  if (defer) {
+    fill_job(defer, gparts, c, nparts, (float)(1.0 / n), g_out, target,
+             target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts, nullptr,
+             0, 1.0, nullptr, b);
+    return check_launch("stx_style_loss_from_parts_deferred");
+  }
   hipLaunchKernelGGL(gram_finalize_kernel, dim3(FSUB, b), dim3(FNT), 0, st, gparts, c, nparts,
                      (float)(1.0 / n), g_out, target,
                      target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts);
@@ -983,6 +1092,53 @@ extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const 
     hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, lparts, b * FSUB,
                        (float)(1.0 / ((double)b * c * c)), loss);
   return check_launch("stx_style_loss_from_parts");
+}
+
+extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const float* target,
+                                         float* g_out, float* coef, float* loss, int b, int c,
+                                         int hw, int target_batched, float weight,
+                                         float diag_alpha, void* ws, size_t ws_bytes,
+                                         void* stream) {
+  return from_parts_impl(gparts, nparts, target, g_out, coef, loss, b, c, hw, target_batched,
+                         weight, diag_alpha, ws, ws_bytes, stream, nullptr);
+}
+
+extern "C" int stx_style_loss_from_parts_deferred(const float* gparts, int nparts,
+                                                  const float* target, float* coef, int b, int c,
+                                                  int hw, int target_batched, float weight,
+                                                  float diag_alpha, void* ws, size_t ws_bytes,
+                                                  stx_gram_fin_job* job, void* stream) {
+  if (!job) {
+    set_error("stx_style_loss_from_parts_deferred: job is required");
+    return STX_E_INVALID;
+  }
+  return from_parts_impl(gparts, nparts, target, nullptr, coef, nullptr, b, c, hw,
+                         target_batched, weight, diag_alpha, ws, ws_bytes, stream, job);
+}
+
+extern "C" int stx_gram_finalize_batch(const stx_gram_fin_job* jobs, int njobs, void* stream) {
+  if (!jobs || njobs <= 0 || njobs > STX_FIN_MAX) {
+    set_error("stx_gram_finalize_batch: 1 <= njobs <= %d required", STX_FIN_MAX);
+    return STX_E_INVALID;
+  }
+  FinBatch fb{};
+  int blocks = 0;
+  for (int j = 0; j < njobs; ++j) {
+    const stx_gram_fin_job& q = jobs[j];
+    if (!q.parts || q.c <= 0 || q.nsplit <= 0 || q.b <= 0 || !q.loss_parts) {
+      set_error("stx_gram_finalize_batch: job %d invalid", j);
+      return STX_E_INVALID;
+    }
+    const int nt = cdiv(q.c, GT);
+    fb.job[j] = q;
+    fb.blk0[j] = blocks;
+    blocks += nt * (nt + 1) / 2 * FSUB * q.b;
+  }
+  fb.blk0[njobs] = blocks;
+  fb.njobs = njobs;
+  hipLaunchKernelGGL(gram_finalize_batch_kernel, dim3(blocks), dim3(FNT), 0, (hipStream_t)stream,
+                     fb);
+  return check_launch("stx_gram_finalize_batch");
 }
 
 extern "C" int stx_gram_bwd(const float* coef, const float* z, float* dz, int b, int c, int h,

@@ -516,8 +516,29 @@ def coef_pitch(c):
     return lib().stx_gram_coef_pitch(c)
 
 
+class FinalizeBatch:
+    """Deferred Gram finalizes of one forward (stx_gram_finalize_batch): the style-loss ops
+    given `fin=` append a job instead of launching their finalize; flush() runs them all
+    in one launch.  The job structs (and what they point at, via `keep`) live until then."""
+
+    def __init__(self):
+        self.jobs, self.keep = [], []
+
+    def new(self):
+        j = N.GramFinJob()
+        self.jobs.append(j)
+        return j
+
+    def flush(self):
+        if self.jobs:
+            arr = (N.GramFinJob * len(self.jobs))(*self.jobs)
+            check(lib().stx_gram_finalize_batch(arr, len(self.jobs), _stream()),
+                  "stx_gram_finalize_batch")
+        self.jobs, self.keep = [], []
+
+
 def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None, loss=None,
-               coef=None, z_amax=None, defer_ws=None):
+               coef=None, z_amax=None, defer_ws=None, fin=None):
     """mean((gram(z) - target)^2) -> 0-d loss; coef = d(weight*loss)/dz operator.
     defer_ws (uint8 device buffer >= stx_gram_ws): the loss is not reduced here; its
     partials stay in defer_ws for loss_finalize (returns (LossPart, coef))."""
@@ -541,9 +562,16 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
         wp, wn = defer_ws.data_ptr(), defer_ws.numel()
     else:
         wp, wn = WS.get(need, z.device)
-    check(L.stx_style_loss(z.data_ptr(), target.data_ptr(), _p(g_out), _p(coef) if want_coef
-                           else None, _p(loss), b, c, hw, int(tb), float(weight),
-                           float(diag_alpha), _p(z_amax), wp, wn, _stream()), "stx_style_loss")
+    if fin is not None:  # finalize deferred to fin.flush()
+        assert defer_ws is not None and g_out is None and want_coef
+        check(L.stx_style_loss_deferred(z.data_ptr(), target.data_ptr(), coef.data_ptr(), b, c,
+                                        hw, int(tb), float(weight), float(diag_alpha),
+                                        _p(z_amax), wp, wn, C.byref(fin.new()), _stream()),
+              "stx_style_loss_deferred")
+    else:
+        check(L.stx_style_loss(z.data_ptr(), target.data_ptr(), _p(g_out), _p(coef) if want_coef
+                               else None, _p(loss), b, c, hw, int(tb), float(weight),
+                               float(diag_alpha), _p(z_amax), wp, wn, _stream()), "stx_style_loss")
     if defer_ws is not None:
         npart = C.c_int()
         off = L.stx_style_loss_parts(b, c, hw, C.byref(npart))
@@ -552,7 +580,7 @@ def style_loss(z, target, weight=1.0, diag_alpha=0.0, want_coef=True, g_out=None
 
 
 def style_content_loss(z, target, content, mse_out, weight=1.0, diag_alpha=0.0, coef=None,
-                       z_amax=None, defer_ws=None):
+                       z_amax=None, defer_ws=None, fin=None):
     """style_loss(z, target, ..., defer_ws=...) and mse(z, content, mode=2, out=mse_out) in
     one pass over z where the Gram kernel allows it.  defer_ws >= stx_style_content_ws.
     Returns (deferred LossPart, coef)."""
@@ -572,17 +600,24 @@ def style_content_loss(z, target, content, mse_out, weight=1.0, diag_alpha=0.0, 
     need = L.stx_style_content_ws(b, c, hw)
     assert defer_ws is not None and defer_ws.numel() >= need, need
     wp, wn = defer_ws.data_ptr(), defer_ws.numel()
-    check(L.stx_style_content_loss(z.data_ptr(), target.data_ptr(), coef.data_ptr(), None, b, c,
-                                   hw, int(tb), float(weight), float(diag_alpha), _p(z_amax),
-                                   content.data_ptr(), mse_out.data_ptr(), wp, wn, _stream()),
-          "stx_style_content_loss")
+    if fin is not None:
+        check(L.stx_style_content_loss_deferred(z.data_ptr(), target.data_ptr(), coef.data_ptr(),
+                                                b, c, hw, int(tb), float(weight),
+                                                float(diag_alpha), _p(z_amax), content.data_ptr(),
+                                                mse_out.data_ptr(), wp, wn, C.byref(fin.new()),
+                                                _stream()), "stx_style_content_loss_deferred")
+    else:
+        check(L.stx_style_content_loss(z.data_ptr(), target.data_ptr(), coef.data_ptr(), None, b,
+                                       c, hw, int(tb), float(weight), float(diag_alpha),
+                                       _p(z_amax), content.data_ptr(), mse_out.data_ptr(), wp, wn,
+                                       _stream()), "stx_style_content_loss")
     npart = C.c_int()
     off = L.stx_style_loss_parts(b, c, hw, C.byref(npart))
     return (wp + off, npart.value, 1.0 / (b * c * c)), coef
 
 
 def style_loss_from_parts(gparts, nparts, b, c, hw, target, weight=1.0, diag_alpha=0.0,
-                          coef=None, defer_ws=None):
+                          coef=None, defer_ws=None, fin=None):
     """style_loss from the fused Gram partials a conv wrote (conv2d(gram_part=...)):
     gparts [b][nparts][64][64].  Returns (deferred LossPart, coef) as style_loss with
     defer_ws."""
@@ -598,10 +633,17 @@ def style_loss_from_parts(gparts, nparts, b, c, hw, target, weight=1.0, diag_alp
     need = L.stx_gram_ws(b, c, hw)
     assert defer_ws is not None and defer_ws.numel() >= need, need
     wp, wn = defer_ws.data_ptr(), defer_ws.numel()
-    check(L.stx_style_loss_from_parts(gparts.data_ptr(), int(nparts), target.data_ptr(), None,
-                                      coef.data_ptr(), None, b, c, hw, int(tb), float(weight),
-                                      float(diag_alpha), wp, wn, _stream()),
-          "stx_style_loss_from_parts")
+    if fin is not None:
+        check(L.stx_style_loss_from_parts_deferred(gparts.data_ptr(), int(nparts),
+                                                   target.data_ptr(), coef.data_ptr(), b, c, hw,
+                                                   int(tb), float(weight), float(diag_alpha), wp,
+                                                   wn, C.byref(fin.new()), _stream()),
+              "stx_style_loss_from_parts_deferred")
+    else:
+        check(L.stx_style_loss_from_parts(gparts.data_ptr(), int(nparts), target.data_ptr(), None,
+                                          coef.data_ptr(), None, b, c, hw, int(tb), float(weight),
+                                          float(diag_alpha), wp, wn, _stream()),
+              "stx_style_loss_from_parts")
     npart = C.c_int()
     off = L.stx_style_loss_parts(b, c, hw, C.byref(npart))
     return (wp + off, npart.value, 1.0 / (b * c * c)), coef

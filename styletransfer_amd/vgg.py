@@ -244,6 +244,10 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
             st.grams[l] = torch.empty(B * nt * 4096, device=dev, dtype=torch.float32)
 
     fuse_content = os.environ.get("STX_CONTENT_FUSE", "1") != "0"
+    # the five taps' Gram finalizes in one launch after the forward (STX_FIN_BATCH=0: one
+    # finalize launch per tap, right after its partials)
+    fin = ops.FinalizeBatch() if (os.environ.get("STX_FIN_BATCH", "1") != "0" and not overlap) \
+        else None
 
     def on_layer(l, z):
         # the style loss of layer l (and the content/feature losses at conv2_2) run on
@@ -267,18 +271,18 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
             if fuse_mse:  # style loss + content/feature/feature-mse in one pass over z
                 st.parts[i], st.coef[i] = ops.style_content_loss(
                     z, targets[i], c4, st.losses[5:8], weight=sw, diag_alpha=alpha,
-                    coef=st.coef[i], z_amax=slot(st.amax, l + 1), defer_ws=st.lws[i])
+                    coef=st.coef[i], z_amax=slot(st.amax, l + 1), defer_ws=st.lws[i], fin=fin)
                 return
             if st.grams[l] is not None:
                 st.parts[i], st.coef[i] = ops.style_loss_from_parts(
                     st.grams[l], st.grams[l].numel() // (b_ * 4096), b_, c_, z[0, 0].numel(),
                     targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
-                    coef=st.coef[i], defer_ws=st.lws[i])
+                    coef=st.coef[i], defer_ws=st.lws[i], fin=fin)
             else:
                 st.parts[i], st.coef[i] = ops.style_loss(
                     z, targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
                     coef=st.coef[i], z_amax=slot(st.amax, l + 1) if split else None,
-                    defer_ws=st.lws[i])
+                    defer_ws=st.lws[i], fin=fin)
             if l == CONTENT_CONV:  # content, feature, feature-mse: one pass
                 ops.mse(z, c4, mode=2, out=st.losses[5:8])
 
@@ -289,6 +293,8 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         if not capturing:
             for c in st.coef:
                 c.record_stream(main)
+    if fin is not None:
+        fin.flush()  # every tap's G, backward operator A and loss partials: one launch
     # the 5 style losses (+ the weighted total) in one launch
     w = None
     extra = None
