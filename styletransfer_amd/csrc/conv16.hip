@@ -558,8 +558,9 @@ struct C16v2 {
 
 // TR: operands swapped in the MFMAs (accumulators D[pixel][co]) and the transposed
 // forward epilogue (conv_epilogue_tr): 64 x 4 tiles, the plain forward epilogue only
+// 128-pixel tiles (NI = 1) fit three blocks per CU (50 KB of LDS each, <= 168 VGPRs)
 template <int TW, int LM, int P2, int NI, bool TR = false>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, (NI == 1 && TW <= 32) ? 3 : 2)
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   using C = C16v2<TW, NI>;
   constexpr bool RP = TW == 64 && NI == 2;  // row-pair tiles (fused pool / unpool)
@@ -580,6 +581,19 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
                                  : (int)blockIdx.x;
   if (first >= ntiles) return;
 
+  {  // experiments (STX_V2_KNOB): 1..7 = stagger the second-dispatched half of the blocks
+     // (blockIdx >> 8 odd: the co-resident partner under round-robin placement) by k x
+     // 1024 cycles; 8 = s_setprio(1) for that half
+    const int knob = tiles_x >> 24;
+    if (knob && ((blockIdx.x >> 8) & 1)) {
+      if (knob == 8) {
+        __builtin_amdgcn_s_setprio(1);
+      } else {
+        for (int k = 0; k < knob; ++k) __builtin_amdgcn_s_sleep(16);
+      }
+    }
+  }
+  tiles_x &= 0xffffff;
   const int nchunks = cdiv(p.cin, 16);
   const int nsteps = 3 * nchunks;
   const int ex = amax_exp(read_amax(p.in_amax));
@@ -818,6 +832,14 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   }
 }
 
+// default 8: s_setprio(1) for the second-dispatched half of the blocks (measured
+// tools/ab_engine.py, same process: Gatys 679.6 -> 674.5 us, fast_st within noise;
+// staggering that half by 1-4 x 1024 cycles instead: no gain)
+static int v2_knob() {
+  const char* e = getenv("STX_V2_KNOB");
+  return e ? (atoi(e) & 15) : 8;
+}
+
 // STX_CONV_V2=0 selects the v1 main loop (read per launch, so a tool can A/B both in
 // one process)
 static bool v2_on() {
@@ -837,8 +859,9 @@ static bool tr_on() {
 template <int TW, int LM, int NI>
 static int launch16v2(const stx_conv_params& p, hipStream_t st) {
   using C = C16v2<TW, NI>;
-  const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
-  const int ntiles = tiles_x * tiles_y;
+  const int tiles_x0 = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
+  const int ntiles = tiles_x0 * tiles_y;
+  const int tiles_x = tiles_x0 | (v2_knob() << 24);
   const int gy = cdiv(p.cout, C::BM), gz = p.n;
   dim3 grid(ntiles, gy, gz);
   if constexpr (TW == 64 && NI == 2) {
@@ -940,10 +963,9 @@ template <int TW, int LM>
 static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
   const long long blocks2 = (long long)cdiv(p.wo, TW) * cdiv(p.ho, 256 / TW) *
                             cdiv(p.cout, 64) * p.n;
-  static const int ni1_below = [] {  // 256-pixel-tile grids smaller than this use 128-px tiles
-    const char* e = getenv("STX_NI1_BELOW");
-    return e ? atoi(e) : 512;
-  }();
+  // 256-pixel-tile grids smaller than this use 128-px tiles (read per launch: A/B tools)
+  const char* ni1_env = getenv("STX_NI1_BELOW");
+  const int ni1_below = ni1_env ? atoi(ni1_env) : 512;
   if (blocks2 < ni1_below && !p.pool_out && !p.p2_z && !p.gram_part) {
     // 128-pixel tiles as 32 x 4 rather than 64 x 2: a 34 x 6 halo instead of 66 x 4 (23 %
     // less staging per tile) -- Gatys NI=1 launches 37-40 -> 35-39 us, ITN residual convs

@@ -753,7 +753,13 @@ __global__ void __launch_bounds__(256, 2) conv_fewout16_kernel(stx_conv_params p
   __shared__ float dt[27 * FO_RH * FO_RWP];
   __shared__ float red[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
-  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x, n = blockIdx.z;
+  // the blocks of one XCD (blockIdx % 8 under round-robin placement) take consecutive
+  // tiles in row-major order, so the input rows two vertically adjacent tiles share are
+  // fetched once into that XCD's L2 (speed only)
+  const int G = gridDim.x;
+  const int tile = (G & 7) == 0 ? (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3)
+                                : (int)blockIdx.x;
+  const int tx = tile % tiles_x, ty = tile / tiles_x, n = blockIdx.z;
   const int oy0 = ty * FO_TH, ox0 = tx * FO_TW;
   const int plane_in = p.h * p.w;
   const float* __restrict__ xn = p.x + (size_t)n * CIN * plane_in;
@@ -801,7 +807,11 @@ __global__ void __launch_bounds__(256, 2) conv_fewout16_kernel(stx_conv_params p
     const int r = item / 3, nb = item - r * 3;
     const int c0 = nb == 0 ? 0 : (nb == 1 ? 32 : FO_RW - 32);
     const int iy = oy0 - 1 + r, ix = ox0 - 1 + c0 + l32;
-    const bool ok = iy >= 0 && iy < p.h && ix >= 0 && ix < p.w;
+    // the third column block overlaps the first two: only its last two columns (the
+    // right halo) are new -- the other lanes read nothing (their D columns are written
+    // by the first two blocks)
+    const bool fresh = nb < 2 || c0 + l32 >= 64;
+    const bool ok = fresh && iy >= 0 && iy < p.h && ix >= 0 && ix < p.w;
     const uint32_t vo = ok ? (uint32_t)(8 * h * plane_in + iy * p.w + ix) * 4u : BUF_OOB;
 #pragma unroll
     for (int t = 0; t < KST; ++t)
@@ -832,10 +842,11 @@ __global__ void __launch_bounds__(256, 2) conv_fewout16_kernel(stx_conv_params p
     }
     const int r = item / 3, nb = item - r * 3;
     const int c0 = nb == 0 ? 0 : (nb == 1 ? 32 : FO_RW - 32);
+    const bool fresh = nb < 2 || c0 + l32 >= 64;  // (the overlap lanes read zeros)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int row = 8 * (q >> 2) + 4 * h + (q & 3);
-      if (row < 27) dt[(row * FO_RH + r) * FO_RWP + c0 + l32] = acc[q] * descale;
+      if (row < 27 && fresh) dt[(row * FO_RH + r) * FO_RWP + c0 + l32] = acc[q] * descale;
     }
   };
   // items wave, wave + 4, ... through a ring of three register buffers: two items'
