@@ -108,8 +108,12 @@ def parse():
     ap.add_argument("--fast-only", action="store_true", help="profiling: fast_st leg only")
     ap.add_argument("--skip-cpu", action="store_true")
     ap.add_argument("--skip-infer", action="store_true", help="skip the video/convert legs")
-    ap.add_argument("--cpu-iters", type=int, default=4)
-    ap.add_argument("--cpu-fast-batch", type=int, default=8, help="fast_st CPU leg batch")
+    ap.add_argument("--cpu-iters", type=int, default=8, help="timed Gatys iterations (CPU leg)")
+    ap.add_argument("--cpu-fast-batch", type=int, default=8,
+                    help="fast_st CPU leg batch (the per-GPU batch of config 4)")
+    ap.add_argument("--cpu-fast-steps", type=int, default=2, help="timed fast_st CPU steps")
+    ap.add_argument("--cpu-convert-batch", type=int, default=32,
+                    help="convert CPU leg batch (config 3)")
     ap.add_argument("--no-graph", action="store_true")
     return ap.parse_args()
 
@@ -377,24 +381,31 @@ def cpu_baseline(args):
         O.fast_st_closure(itn, ln, batch)
         aopt.step()
     fast_step()  # warm-up
+    nf = args.cpu_fast_steps
     t1 = time.perf_counter()
-    fast_step()
+    for _ in range(nf):
+        fast_step()
     dtf = time.perf_counter() - t1
+    Bc = args.cpu_convert_batch
+    cbatch = torch.from_numpy(W.synthetic_image(5000, (Bc, 3, 256, 256)))
+    nc = 3
     with torch.no_grad():
-        itn(batch)
+        itn(cbatch)
         t2 = time.perf_counter()
-        itn(batch)
+        for _ in range(nc):
+            itn(cbatch)
         dtc = time.perf_counter() - t2
     return dict(value=n / dt, unit="iters/s", cores=threads, kind="port",
                 sample=f"oracle/reference_cpu.py Gatys Adam loop {H}x{H}, {n} timed iters "
                        f"after 1 warm-up ({dt:.1f} s), reference schedule incl. prefix "
                        f"re-runs and VGG wgrad; torch {torch.__version__} CPU, {host}",
-                fast_st=dict(value=B / dtf, unit="images/s", batch=B, s=round(dtf, 2),
-                             sample=f"oracle fast_st_closure + torch.optim.Adam, B={B} 256^2, "
-                                    "1 timed step after 1 warm-up"),
-                convert=dict(value=B / dtc, unit="images/s", batch=B, s=round(dtc, 2),
-                             sample=f"oracle ImageTransformNet forward, B={B} 256^2, no_grad, "
-                                    "1 timed pass after 1 warm-up"))
+                fast_st=dict(value=nf * B / dtf, unit="images/s", batch=B, s=round(dtf, 2),
+                             sample=f"oracle fast_st_closure + torch.optim.Adam, B={B} 256^2 "
+                                    f"(config 4's per-GPU batch), {nf} timed steps after 1 "
+                                    "warm-up"),
+                convert=dict(value=nc * Bc / dtc, unit="images/s", batch=Bc, s=round(dtc, 2),
+                             sample=f"oracle ImageTransformNet forward, B={Bc} 256^2 (config 3), "
+                                    f"no_grad, {nc} timed passes after 1 warm-up"))
 
 
 def _free_port():

@@ -687,7 +687,7 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
         p.ho % 2 == 0 && p.wo % 16 == 0 && !p.bias && !p.accumulate && !p.relu_out &&
         (!p.up_dp || p.up_z == p.x) && (uint64_t)p.cin * p.ho * p.wo * 4 < (1ull << 31)) {
       Gb16 g{p.wt, p.wt_batch_stride, p.cout_pad, p.x, p.in_amax, p.acc_scale, p.up_dp,
-             p.aux, p.aux_scale, p.y, p.out_amax, p.ho, p.wo, 0};
+             p.aux, p.aux_scale, p.y, p.out_amax, p.ho, p.wo};
       return gram_bwd16_launch(g, p.n, p.cin, st);
     }
     stx_conv_params q = p;

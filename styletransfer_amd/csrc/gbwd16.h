@@ -17,7 +17,6 @@ struct Gb16 {
   float* out;             // [n][C][h][w]
   float* out_amax;        // amax group or NULL
   int h, w;
-  int dbg;                // profiling only ($STX_GB_DBG): 1 no A staging, 2 no MFMA, 4 no stores
 };
 
 // C in {64, 128}, h even, w % 32 == 0 (the caller checks the contract)
