@@ -3,7 +3,7 @@
 variant, then replayed in interleaved rounds (median per variant) and compared bit for
 bit against the first variant.
 
-    python tools/ab_engine.py "STX_FIN_BATCH=0" "STX_FIN_BATCH=1" [--rounds 7] [--no-fast]
+    python tools/ab_engine.py "STX_FIN_BATCH=0" "STX_FIN_BATCH=1" [--rounds 7] [--no-fast] [--no-gatys]
 
 A variant is a comma-separated list of NAME=VALUE settings applied while that variant's
 engine is built and captured (the library reads its switches at launch/capture time)."""
@@ -61,14 +61,14 @@ def main():
     content = torch.from_numpy(W.synthetic_image(2000, (1, 3, H, H))).to(dev)
     feat = V.VGGFeatures(V.load_vgg19_weights(), dev)
     engs = []
-    for spec in args:
+    for spec in ([] if "--no-gatys" in sys.argv else args):
         with Env(spec):
             engs.append(V.GatysEngine(feat, style, content).capture(warmup=1))
     res = [[] for _ in args]
     for _ in range(rounds):
         for i, e in enumerate(engs):
             res[i].append(ev(e.step, 50))
-    for i, spec in enumerate(args):
+    for i, spec in enumerate(args[:len(engs)]):
         m = statistics.median(res[i])
         same = torch.equal(engs[i].x, engs[0].x)
         print(f"gatys  {spec:40s} {m * 1e3:8.1f} us  {1e3 / m:7.0f} it/s  min {min(res[i]) * 1e3:.1f}"
