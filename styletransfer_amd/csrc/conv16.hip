@@ -559,9 +559,7 @@ struct C16v2 {
 // TR: operands swapped in the MFMAs (accumulators D[pixel][co]) and the transposed
 // forward epilogue (conv_epilogue_tr): 64 x 4 tiles, the plain forward epilogue only
 // 128-pixel tiles (NI = 1) fit three blocks per CU (50 KB of LDS each, <= 168 VGPRs)
-// IL: the per-step staging branch-free and spread over the step's three taps, each piece
-// interleaved with that tap's MFMAs (sched_group_barrier); same products, same order
-template <int TW, int LM, int P2, int NI, bool TR = false, bool IL = false>
+template <int TW, int LM, int P2, int NI, bool TR = false>
 __global__ void __launch_bounds__(256, (NI == 1 && TW <= 32) ? 3 : 2)
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   using C = C16v2<TW, NI>;
@@ -719,16 +717,10 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     for (int r = 0; r < C::NIT; ++r) st_halo(0, r);
     st_w(0);
     // staged for step 0: step 1's weights, part 0 of chunk 1's halo
-    if (IL) {  // unconditional (clamped) prologue loads: the IL loop stores them regardless
-      ld_w(min(1, nsteps - 1));
+    if (nsteps > 1) ld_w(1);
+    if (nchunks > 1) {
 #pragma unroll
-      for (int r = 0; r < C::NIT; r += 3) ld_halo(min(1, nchunks - 1), r);
-    } else {
-      if (nsteps > 1) ld_w(1);
-      if (nchunks > 1) {
-#pragma unroll
-        for (int r = 0; r < C::NIT; r += 3) ld_halo(1, r);
-      }
+      for (int r = 0; r < C::NIT; r += 3) ld_halo(1, r);
     }
     __syncthreads();
 
@@ -771,47 +763,15 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
         f16x8 ahi[2], alo[2], bhi[NI], blo[NI];
         rdA(0, 0, ahi);
         rdB(0, 0, bhi);
-        // IL: scheduling group of one MFMA phase (2 NI MFMAs), each MFMA followed by up to
-        // VK VALU ops / one VMEM read / one LDS write of the staging piece of this tap
-        constexpr int VK = NI == 2 ? 4 : 8;
-        static_assert(C::NIT <= 6, "IL staging: at most two halo items per step");
-        auto groups = [&](bool valu, bool vmem) {
-          if constexpr (IL) {
-#pragma unroll
-            for (int m = 0; m < 2 * NI; ++m) {
-              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-              if (valu) __builtin_amdgcn_sched_group_barrier(0x002, VK, 0);
-              if (vmem) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-              __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-            }
-          } else {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
-          }
-        };
 #pragma unroll
         for (int tl = 0; tl < 3; ++tl) {
           rdB(tl, 1, blo);
-          if constexpr (IL) {
-            // branch-free staging spread over the taps (indices clamped: past the last
-            // chunk / step the stores go to the idle buffers and the loads re-read valid
-            // rows); tap 0: weights + the loads, taps 1, 2: one full halo item each
-            if (tl == 0) {
-              st_w((s + 1) & 1);
-              ld_w(min(s + 2, nsteps - 1));
-              const int cn = min(k < 2 ? c + 1 : c + 2, nchunks - 1);
-#pragma unroll
-              for (int r = (k + 1) % 3; r < C::NIT; r += 3) ld_halo(cn, r);
-            } else {
-              const int r = k + 3 * (tl - 1);
-              if (r < C::NIT && (r + 1 < C::NIT || C::NITEM % 256 == 0)) st_halo((c + 1) & 1, r);
-            }
-          }
           __builtin_amdgcn_sched_group_barrier(0x100, NI, 0);
-          groups(tl > 0, tl == 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
           phase(ahi, bhi);
           rdA(tl, 1, alo);
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          groups(tl > 0, tl == 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
           phase(ahi, blo);
           f16x8 nah[2], nbh[NI];
           if (tl + 1 < 3) {
@@ -819,16 +779,10 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
             rdB(tl + 1, 0, nbh);
             __builtin_amdgcn_sched_group_barrier(0x100, 2 + NI, 0);
           }
-          groups(tl > 0, tl == 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * NI, 0);
           phase(alo, bhi);
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (IL) {
-            // the ragged last halo item (not every lane has one) keeps its guard
-            if (tl == 2 && C::NITEM % 256 != 0 && (C::NIT - 1) % 3 == k && c + 1 < nchunks) {
-              st_halo((c + 1) & 1, C::NIT - 1);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          } else if (tl == 0) {
+          if (tl == 0) {
             // staged data -> the other buffers: step s+1's weights and part k of chunk
             // c+1's halo (loaded one step ago); then the loads for step s+1's staging:
             // step s+2's weights and the next part of the halo
@@ -902,12 +856,6 @@ static bool tr_on() {
   return e && atoi(e) != 0;
 }
 
-// STX_CONV_IL=1: the IL form of the v2 main loop (read per launch: same-process A/B)
-static bool il_on() {
-  const char* e = getenv("STX_CONV_IL");
-  return e && atoi(e) != 0;
-}
-
 template <int TW, int LM, int NI>
 static int launch16v2(const stx_conv_params& p, hipStream_t st) {
   using C = C16v2<TW, NI>;
@@ -924,22 +872,13 @@ static int launch16v2(const stx_conv_params& p, hipStream_t st) {
       return check_launch("stx_conv2d(f16x3 v2, transposed)");
     }
   }
-  const bool il = il_on();
   if constexpr (NI == 2 && LM == STX_IN_RAW) {
     if (p.p2_z) {
-      if (il)
-        hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 1, NI, false, true>), grid,
-                           dim3(256), 0, st, p, tiles_x, ntiles);
-      else
-        hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 1, NI>), grid, dim3(256), 0, st, p,
-                           tiles_x, ntiles);
+      hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 1, NI>), grid, dim3(256), 0, st, p,
+                         tiles_x, ntiles);
       return check_launch("stx_conv2d(f16x3 v2 + phase 2)");
     }
   }
-  if (il)
-    hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI, false, true>), grid, dim3(256), 0,
-                       st, p, tiles_x, ntiles);
-  else
     hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI>), grid, dim3(256), 0, st, p,
                        tiles_x, ntiles);
   return check_launch("stx_conv2d(f16x3 v2)");

@@ -442,10 +442,8 @@ wgrad16_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg1
 // instead of 8 waves), so the split-K slab the reduce kernel reads is half as big.
 // CIB = cins per block (64; 128 for cout = 64, so each wave still owns two 32 x 32
 // (co, ci) tiles: 18 MFMAs per barrier instead of 9)
-// IL: each step reads all of its B fragments up front and runs the next image's staging
-// between its MFMAs (scheduling only: the same products in the same order)
-template <int WCO, bool UP, int PF, int CIB = 64, bool IL = false>  // WCO = couts / 32; UP:
-__global__ void __launch_bounds__(256, 1)  // nearest x2 input; PF + 1 steps of loads in flight
+template <int WCO, bool UP, int PF, int CIB = 64>  // WCO = couts / 32; UP: nearest x2
+__global__ void __launch_bounds__(256, 1)  // upsampled input; PF + 1 steps of loads in flight
 wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                    float* __restrict__ ws, const float* __restrict__ x_amax,
                    const float* __restrict__ dy_amax, Wg16 g) {
@@ -580,44 +578,6 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
       }
     }
   };
-  // IL form of one step: B reads first, then the dY split, the next image's staging and
-  // the MFMAs, interleaved by the scheduler
-  auto step_il = [&](const Ld& t, const char* img, const Ld& tn, char* imgn) {
-    h8 bh[NPAIR][3], bl[NPAIR][3];
-#pragma unroll
-    for (int pi = 0; pi < NPAIR; ++pi) {
-      const int ct = WCO == 4 ? pi : (wave >> 1) * NCI + (NPAIR > 1 ? pi : 0);
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        bh[pi][kw] = *reinterpret_cast<const h8*>(img + (((kw * 2 + 0) * 2 + h) * CIB + ct * 32 + l32) * 16);
-        bl[pi][kw] = *reinterpret_cast<const h8*>(img + (((kw * 2 + 1) * 2 + h) * CIB + ct * 32 + l32) * 16);
-      }
-    }
-    h8 ah, al;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float v = (e < 4 ? t.a0[e] : t.a1[e - 4]) * sd;
-      ah[e] = (_Float16)v;
-      al[e] = (_Float16)(v - (float)ah[e]);
-    }
-    stage(tn, imgn);
-#pragma unroll
-    for (int pi = 0; pi < NPAIR; ++pi)
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[pi][kw], acc[pi][kw], 0, 0, 0);
-        acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[pi][kw], acc[pi][kw], 0, 0, 0);
-        acc[pi][kw] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[pi][kw], acc[pi][kw], 0, 0, 0);
-      }
-    __builtin_amdgcn_sched_group_barrier(0x100, 6 * NPAIR, 0);  // the B reads
-    __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);         // dY split
-#pragma unroll
-    for (int i = 0; i < 9 * NPAIR; ++i) {                       // MFMA, staging VALU / stores
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-    }
-  };
   const int s0 = split * g.steps_per_split;
   const int nst = min(g.steps, s0 + g.steps_per_split) - s0;  // >= 1
   {
@@ -637,12 +597,8 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   for (int s = 0; s < nst; s += PF + 1) {
 #pragma unroll
     for (int k = 0; k <= PF; ++k) {
-      if constexpr (IL) {
-        step_il(ring[k], vimg[k & 1], ring[(k + 1) % (PF + 1)], vimg[(k + 1) & 1]);
-      } else {
-        stage(ring[(k + 1) % (PF + 1)], vimg[(k + 1) & 1]);  // the next step's V image
-        compute(ring[k], vimg[k & 1]);
-      }
+      stage(ring[(k + 1) % (PF + 1)], vimg[(k + 1) & 1]);  // the next step's V image
+      compute(ring[k], vimg[k & 1]);
       load(ring[k]);  // step s + k + PF + 1
       __syncthreads();  // lgkmcnt(0) + s_barrier: the global loads stay in flight
     }
@@ -701,8 +657,6 @@ static Wg16Kernel wg16_kernel(const Wg16& g) {
       const char* e = getenv("STX_WG16_LPF");
       return e ? atoi(e) : 3;
     }();
-    const char* il_e = getenv("STX_WG16_IL");  // read per plan: same-process A/B
-    if (g.cout == 128 && !up && il_e && atoi(il_e) != 0) return wgrad16_lds_kernel<4, false, 3, 64, true>;
     if (g.cout == 128)
       return up ? wgrad16_lds_kernel<4, true, 3>
                 : (lpf >= 7 ? wgrad16_lds_kernel<4, false, 7>
