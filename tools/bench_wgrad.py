@@ -1,8 +1,10 @@
 """The residual convs' 3x3 weight gradient (128 -> 128 @ 64^2, B=8, split MFMA; raw and
 ReLU input; plus small / ragged shapes) under the variants given as NAME=VALUE specs:
 HIP-event time of the whole stx_conv2d_wgrad16 call (main kernel + split-K reduce; max|x|,
-max|dy| precomputed) and each result's error against an fp64 torch reference.
-    python tools/bench_wgrad.py STX_WG16_K9=0 STX_WG16_K9=1"""
+max|dy| precomputed) and each result's error against an fp64 torch reference.  Each
+NAME=VALUE spec is set before its runs; only switches the library reads at every call
+(not its static-cached ones) differ within one process.
+    python tools/bench_wgrad.py [NAME=VALUE ...]"""
 import os
 import sys
 
@@ -27,7 +29,7 @@ def ev(fn, reps=50):
 
 
 def main():
-    specs = sys.argv[1:] or ["STX_WG16_K9=0", "STX_WG16_K9=1"]
+    specs = sys.argv[1:] or ["STX_DEFAULT=1"]
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     for (n, c, hw, mode) in ((8, 128, 64, N.STX_IN_RAW), (8, 128, 64, N.STX_IN_RELU),
