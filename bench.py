@@ -179,7 +179,9 @@ def gatys_leg(args, world, rank, dev):
     # fused ReLU+MaxPool output for conv2_1, max|Z2| for conv2_1's input scale
     z1 = eng.st.z[0]
     out = torch.empty_like(z1)
-    am = V.slot(eng.st.amax, 1).clone()
+    # max|Z1| as conv1_1's epilogue reports it (the iteration's slot itself was zeroed by
+    # its Adam launch for the next iteration)
+    am = ops.amax(z1)
     am_out = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
     pool = torch.empty_like(eng.st.pools[1])
     gparts = eng.st.grams[1]
@@ -219,10 +221,11 @@ def gatys_leg(args, world, rank, dev):
     dz1 = torch.empty_like(sc["dz1"])
     am_b = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
 
+    dz2_am, z1_am = ops.amax(sc["dz2"]), ops.amax(st.z[0])
+
     def dgrad12():
         return feat.dgrad(1, sc["dz2"], dz1, mask=st.z[0], p2_z=st.z[0], p2_coef=st.coef[0],
-                          p2_scale=None, in_amax=V.slot(st.amax, 9), out_amax=am_b,
-                          p2_amax=V.slot(st.amax, 1))
+                          p2_scale=None, in_amax=dz2_am, out_amax=am_b, p2_amax=z1_am)
     dg_ms = event_avg_ms(dgrad12, reps=20)
     dg_gf = gf_conv + 2.0 * 64 * 64 * H * H / 1e9
     loss = float(eng.total)

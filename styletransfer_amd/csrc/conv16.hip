@@ -559,9 +559,25 @@ struct C16v2 {
 // TR: operands swapped in the MFMAs (accumulators D[pixel][co]) and the transposed
 // forward epilogue (conv_epilogue_tr): 64 x 4 tiles, the plain forward epilogue only
 // 128-pixel tiles (NI = 1) fit three blocks per CU (50 KB of LDS each, <= 168 VGPRs)
-template <int TW, int LM, int P2, int NI, bool TR = false>
+// STAMP (diagnostic build only, STX_CONV_STAMP=1; never timed): per wave, shader-clock
+// sums of the loop's segments -> g_conv_stamps (read by stx_debug_conv_stamps):
+// [0] prologue (loads + first staging), [1] tap 0 MFMAs + the step's staging, [2] taps
+// 1-2 MFMAs, [3] the step's barrier wait, [4] epilogue, [5] steps
+__device__ unsigned long long g_conv_stamps[4096 * 8];
+
+__device__ __forceinline__ unsigned long long conv_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <int TW, int LM, int P2, int NI, bool TR = false, bool STAMP = false>
 __global__ void __launch_bounds__(256, (NI == 1 && TW <= 32) ? 3 : 2)
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
+  unsigned long long st_t0 = 0, st_seg[6] = {0, 0, 0, 0, 0, 0};
+  if constexpr (STAMP) st_t0 = conv_stamp();
   using C = C16v2<TW, NI>;
   constexpr bool RP = TW == 64 && NI == 2;  // row-pair tiles (fused pool / unpool)
   static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
@@ -584,13 +600,22 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   {  // experiments (STX_V2_KNOB): 1..7 = stagger the second-dispatched half of the blocks
      // (blockIdx >> 8 odd: the co-resident partner under round-robin placement) by k x
      // 1024 cycles; 8 = s_setprio(1) for that half
-    const int knob = tiles_x >> 24;
+    const int knob = (tiles_x >> 24) & 15;
     if (knob && ((blockIdx.x >> 8) & 1)) {
       if (knob == 8) {
         __builtin_amdgcn_s_setprio(1);
       } else {
         for (int k = 0; k < knob; ++k) __builtin_amdgcn_s_sleep(16);
       }
+    }
+    // STX_V2_PHASE = K (grids of more than one round of resident blocks): the second block
+    // of each CU in the FIRST round (linear block id in [256, 512)) starts K x 8128 cycles
+    // late; the slots it frees then stay out of phase with their partners for the later
+    // rounds, so one block's epilogue stores run under the other's MFMA loop
+    const int pk = (tiles_x >> 28) & 7;
+    const int lin = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    if (pk && lin >= 256 && lin < 512) {
+      for (int k = 0; k < pk; ++k) __builtin_amdgcn_s_sleep(127);
     }
   }
   tiles_x &= 0xffffff;
@@ -731,6 +756,11 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
       for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    unsigned long long st_a = 0;
+    if constexpr (STAMP) {
+      st_a = conv_stamp();
+      st_seg[0] += st_a - st_t0;
+    }
 
     for (int c = 0; c < nchunks; ++c) {
       const int hbo = (c & 1) * C::HB;
@@ -798,6 +828,11 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
               for (int r = (k + 1) % 3; r < C::NIT; r += 3) ld_halo(cn, r);
             }
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (STAMP) {
+              const unsigned long long t = conv_stamp();
+              st_seg[1] += t - st_a;
+              st_a = t;
+            }
           }
           if (tl + 1 < 3) {
 #pragma unroll
@@ -806,7 +841,18 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
             for (int j = 0; j < NI; ++j) bhi[j] = nbh[j];
           }
         }
+        if constexpr (STAMP) {
+          const unsigned long long t = conv_stamp();
+          st_seg[2] += t - st_a;
+          st_a = t;
+        }
         __syncthreads();  // this step's reads done; the staged buffers are complete
+        if constexpr (STAMP) {
+          const unsigned long long t = conv_stamp();
+          st_seg[3] += t - st_a;
+          st_a = t;
+          st_seg[5] += 1;
+        }
       }
     }
 
@@ -828,6 +874,14 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
         conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, false>(acc, p, et, descale,
                                                           reinterpret_cast<float*>(smem),
                                                           reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
+    }
+    if constexpr (STAMP) st_seg[4] += conv_stamp() - st_a;
+  }
+  if constexpr (STAMP) {
+    const int slot = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + wave;
+    if (lane == 0 && slot < 4096) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g_conv_stamps[(size_t)slot * 8 + k] = st_seg[k];
     }
   }
 }
@@ -856,14 +910,30 @@ static bool tr_on() {
   return e && atoi(e) != 0;
 }
 
+// the first-round phase offset (see the kernel), K x 8128 cycles, for grids of exactly two
+// rounds of resident blocks (513..1024 blocks: the Gatys conv1_2 launches at 512^2).
+// Measured (tools/ab_engine.py, same process): Gatys 663.5 -> 654.5 us per iteration at
+// K = 3-4, bit-identical; applied to every multi-round grid the fast_st step lost 13-66 us
+// (its B=8 grids run 4+ rounds).  STX_V2_PHASE=K overrides K for every multi-round grid;
+// STX_V2_PHASE=0 turns it off.  Read per launch.
+static int v2_phase(long long blocks) {
+  const char* e = getenv("STX_V2_PHASE");
+  if (e) return blocks > 512 ? (atoi(e) & 7) : 0;
+  return blocks > 512 && blocks <= 1024 ? 3 : 0;
+}
+
 template <int TW, int LM, int NI>
 static int launch16v2(const stx_conv_params& p, hipStream_t st) {
   using C = C16v2<TW, NI>;
   const int tiles_x0 = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
   const int ntiles = tiles_x0 * tiles_y;
-  const int tiles_x = tiles_x0 | (v2_knob() << 24);
+  int tiles_x = tiles_x0 | (v2_knob() << 24);
   const int gy = cdiv(p.cout, C::BM), gz = p.n;
   dim3 grid(ntiles, gy, gz);
+  if constexpr (NI == 2) {  // 2 blocks per CU x 256 CUs resident: only multi-round grids
+    const int pk = v2_phase((long long)ntiles * gy * gz);
+    if (pk) tiles_x |= pk << 28;
+  }
   if constexpr (TW == 64 && NI == 2) {
     if (tr_on() && !p.p2_z && !p.mask && !p.aux && !p.accumulate && !p.acc_scale && !p.up_dp &&
         !p.pool_sum && p.wo % 4 == 0) {
@@ -877,6 +947,14 @@ static int launch16v2(const stx_conv_params& p, hipStream_t st) {
       hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 1, NI>), grid, dim3(256), 0, st, p,
                          tiles_x, ntiles);
       return check_launch("stx_conv2d(f16x3 v2 + phase 2)");
+    }
+  }
+  if constexpr (TW == 64 && NI == 2 && LM == STX_IN_RELU) {
+    const char* se = getenv("STX_CONV_STAMP");  // diagnostic build (tools/stamp_conv.py)
+    if (se && atoi(se) != 0) {
+      hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI, false, true>), grid, dim3(256),
+                         0, st, p, tiles_x, ntiles);
+      return check_launch("stx_conv2d(f16x3 v2, stamps)");
     }
   }
     hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI>), grid, dim3(256), 0, st, p,
@@ -1325,4 +1403,11 @@ extern "C" int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax,
                      reinterpret_cast<_Float16*>(wt16), w_amax, cout, cin, transpose, gin16,
                      gout64);
   return check_launch("stx_conv_weight_prep16");
+}
+
+// diagnostic: copy out the STAMP build's per-wave segment sums (tools/stamp_conv.py)
+extern "C" int stx_debug_conv_stamps(unsigned long long* host, int n) {
+  if (!host || n <= 0 || n > 4096 * 8) return STX_E_INVALID;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(stx::g_conv_stamps), (size_t)n * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : STX_E_INVALID;
 }
