@@ -24,7 +24,7 @@ subprocess.check_call([sys.executable, "tools/pmc_r3_summary.py", tag], stdout=s
 out = [f"rocprofv3 --kernel-trace of the bench's Gatys legs (profiles/{tag}_bench_kernel_stats.csv):",
        "per-dispatch durations by grid (blocks x, y, z)",
        "kernel                                              grid            n   mean_us  median_us"]
-for K in ("conv3x3_f16x3_v2_kernel<64, 1, 0, 2, false>", "conv3x3_f16x3_v2_kernel<64, 0, 1, 2, false>"):
+for K in ("conv3x3_f16x3_v2_kernel<64, 1, 0, 2, false", "conv3x3_f16x3_v2_kernel<64, 0, 1, 2, false"):
     by = {}
     for r in csv.DictReader(open(f"{G}/prof/run_kernel_trace.csv")):
         if K in r["Kernel_Name"]:
