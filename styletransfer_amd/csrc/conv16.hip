@@ -910,16 +910,15 @@ static bool tr_on() {
   return e && atoi(e) != 0;
 }
 
-// the first-round phase offset (see the kernel), K x 8128 cycles, for grids of exactly two
-// rounds of resident blocks (513..1024 blocks: the Gatys conv1_2 launches at 512^2).
-// Measured (tools/ab_engine.py, same process): Gatys 663.5 -> 654.5 us per iteration at
-// K = 3-4, bit-identical; applied to every multi-round grid the fast_st step lost 13-66 us
-// (its B=8 grids run 4+ rounds).  STX_V2_PHASE=K overrides K for every multi-round grid;
-// STX_V2_PHASE=0 turns it off.  Read per launch.
+// the first-round phase offset (see the kernel), K x 8128 cycles, for multi-round grids:
+// STX_V2_PHASE=K (read per launch), off by default.  Measured: Gatys 663.5 -> 654.5 and
+// 662.1 -> 658.3 us per iteration in same-process A/Bs with K = 3 on the two-round grids,
+// but bench.py on one box 1419-1425 vs 1424-1431 it/s (noise) with the isolated conv1_2
+// launches 2 us slower each (back-to-back launches of one kernel already overlap across
+// the launch boundary); on every multi-round grid the fast_st step lost 13-66 us.
 static int v2_phase(long long blocks) {
   const char* e = getenv("STX_V2_PHASE");
-  if (e) return blocks > 512 ? (atoi(e) & 7) : 0;
-  return blocks > 512 && blocks <= 1024 ? 3 : 0;
+  return e && blocks > 512 ? (atoi(e) & 7) : 0;
 }
 
 template <int TW, int LM, int NI>
