@@ -107,6 +107,10 @@ def parse():
                     help="timed steps of the B=64-on-one-GPU fast_st leg (world 1; 0 = skip)")
     ap.add_argument("--gatys-run-iters", type=int, default=500,
                     help="config 2 as written: one timed run of this many Gatys iterations")
+    ap.add_argument("--lbfgs-steps", type=int, default=10,
+                    help="timed outer L-BFGS steps of the train_gatys leg (0 = skip)")
+    ap.add_argument("--lbfgs-fill", type=int, default=20,
+                    help="untimed outer L-BFGS steps at most, to fill the 100-pair history")
     ap.add_argument("--skip-fast", action="store_true")
     ap.add_argument("--fast-only", action="store_true", help="profiling: fast_st leg only")
     ap.add_argument("--skip-cpu", action="store_true")
@@ -237,6 +241,33 @@ def gatys_leg(args, world, rank, dev):
                                                          dg_ms=dg_ms, dg_gflop=dg_gf,
                                                          dg_tflops=dg_gf / (dg_ms * 1e-3) / 1e3),
                 gram=gram)
+
+
+def gatys_lbfgs_leg(args, world, rank, dev):
+    """The gatys_st CLI's default optimiser (StyleNetwork.train_gatys: torch.optim.LBFGS,
+    history 100, max_iter 20, stransfer/network.py:411-458) at 512^2 on the same
+    synthetic images: vgg.GatysLBFGS (one hipGraph replay + one host read per L-BFGS
+    iteration).  Outer steps run until the history holds its 100 pairs (at most
+    `lbfgs_fill` steps), then `lbfgs_steps` outer steps are timed.  Rates: closure
+    evaluations as torch counts them (func_evals), outer steps."""
+    H = args.size
+    style = torch.from_numpy(W.synthetic_image(1000 + rank, (1, 3, H, H))).to(dev)
+    content = torch.from_numpy(W.synthetic_image(2000 + rank, (1, 3, H, H))).to(dev)
+    feat = V.VGGFeatures(V.load_vgg19_weights(), dev)
+    eng = V.GatysLBFGS(feat, style, content).capture()
+    fill = 0
+    while fill < args.lbfgs_fill and eng.history()[0] < 100:
+        eng.step()
+        fill += 1
+    pairs0 = eng.history()[0]
+    ev0, runs0 = eng.func_evals, eng.closure_runs
+    dt = timed(eng.step, args.lbfgs_steps, world, dev)
+    evals, runs = eng.func_evals - ev0, eng.closure_runs - runs0
+    pairs1, n_iter = eng.history()
+    return dict(evals_per_s=world * evals / dt, steps_per_s=world * args.lbfgs_steps / dt,
+                dt=dt, steps=args.lbfgs_steps, evals=evals, closure_runs=runs,
+                fill_steps=fill, pairs_at_start=pairs0, pairs_at_end=pairs1, n_iter=n_iter,
+                loss=float(eng.total))
 
 
 def fast_st_leg(args, world, rank, dev, B=None, steps=None):
@@ -471,6 +502,7 @@ def main():
                               "ms_per_step": round(1e3 * fs["dt"] / fs["steps"], 3)}))
         return
     g = gatys_leg(args, world, rank, dev)
+    lb = gatys_lbfgs_leg(args, world, rank, dev) if args.lbfgs_steps > 0 else None
     fs = None if args.skip_fast else fast_st_leg(args, world, rank, dev)
     fs64 = None
     if not args.skip_fast and world == 1 and args.fast_b64_steps > 0:
@@ -570,6 +602,20 @@ def main():
                 "iters": r["iters"], "seconds": round(r["s"], 4), "value": round(r["rate"], 3),
                 "unit": "iters/s", "note": "BASELINE config 2 as written: one timed run of "
                 "500 Adam iterations at 512^2 (hipGraph replays), after the K timed steps"}
+        if lb:
+            res["gatys_lbfgs"] = {
+                "value": round(lb["evals_per_s"], 3), "unit": "closure evaluations/s",
+                "outer_steps_per_s": round(lb["steps_per_s"], 4),
+                "vs_adam_iteration_rate": round(lb["evals_per_s"] / g["rate"], 4),
+                "evals": lb["evals"], "closure_runs": lb["closure_runs"],
+                "steps": lb["steps"], "seconds": round(lb["dt"], 4),
+                "history_pairs": [lb["pairs_at_start"], lb["pairs_at_end"]],
+                "fill_steps": lb["fill_steps"], "torch_n_iter": lb["n_iter"],
+                "note": "gatys_st's default optimiser (StyleNetwork.train_gatys: L-BFGS, "
+                        "history 100, max_iter 20) at 512^2; timed after the history filled; "
+                        "per iteration one hipGraph replay (compact-form direction + x update + "
+                        "closure + gradient statistics) and one host read of the scalars "
+                        "torch's control flow tests; evaluations as torch counts them"}
         if fs:
             res["fast_st"] = {
                 "value": round(fs["rate"], 3), "unit": "images/s",

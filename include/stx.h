@@ -349,6 +349,33 @@ int stx_vec_axpby(float* y, const float* x, long long n, float a, const float* a
                   float a_sgn, float b, void* stream);
 int stx_scalar_op(float* s, int op, int i, int j, int k, void* stream);
 
+/* L-BFGS in the compact form (lbfgs.hip): torch.optim.LBFGS's search direction, step
+ * size and parameter update without line search (StyleNetwork.train_gatys,
+ * stransfer/network.py:435-456; torch/optim/lbfgs.py's two-loop recursion) in a fixed
+ * launch sequence whatever the history length.
+ *   hist   [2][m + 1][npad] floats (stx_lbfgs_hist_bytes): S slots then Y slots, a ring
+ *          of m committed pairs + one candidate; npad = n rounded up to 1024
+ *   state  stx_lbfgs_state_bytes(m) bytes, zeroed by the caller before the first call:
+ *          pair order, R = [s_i.y_j], Y^T Y, H_diag, t, torch's n_iter
+ *   prev_g npad floats (the previous gradient)
+ *   scal   >= 16 device floats the host reads: 0 loss, 1 max|g|, 2 sum|g|, 3 g.d, 4 t,
+ *          5 max|t d|, 6 stop flag (g.d > -tol_change: x not moved), 7 y.s, 8 pairs,
+ *          9 n_iter, 10 H_diag
+ * stx_lbfgs_grad_stats (after each closure evaluation): scal[0] = *loss (if loss),
+ *   scal[1] = max|g|, scal[2] = sum|g|; zeroes clear[0 .. clear_n).
+ * stx_lbfgs_direction (one torch loop iteration up to the next closure): n_iter += 1;
+ *   y = g - prev_g, s = t_prev d_prev, accept when y.s > 1e-10 (H_diag = y.s / y.y); t =
+ *   min(1, 1/sum|g|) * lr on the first iteration, else lr; d = -H g; g.d; x += t d unless
+ *   g.d > -tol_change.  1 <= m <= 256; 16-byte aligned vectors. */
+size_t stx_lbfgs_state_bytes(int m);
+size_t stx_lbfgs_hist_bytes(long long n, int m);
+size_t stx_lbfgs_ws(long long n, int m);
+int stx_lbfgs_direction(float* x, const float* g, float* prev_g, float* hist, long long n, int m,
+                        float lr, float tol_change, void* state, float* scal, void* ws,
+                        size_t ws_bytes, void* stream);
+int stx_lbfgs_grad_stats(const float* g, long long n, const float* loss, float* scal, float* clear,
+                         int clear_n, void* ws, size_t ws_bytes, void* stream);
+
 /* MaxPool2d(2,2) on (optionally relu'd) input; idx = flat y*w+x argmax per plane,
  * torch CPU semantics (first max in row-major window order; NaN propagates). idx may be NULL. */
 int stx_maxpool2x2_fwd(const float* x, float* y, long long* idx, int nc, int h, int w,

@@ -110,6 +110,11 @@ SIGNATURES = {
     "stx_vec_reduce": (i32, [vp, vp, i64, i32, vp, vp, vp, f32, vp, sz, vp]),
     "stx_vec_axpby": (i32, [vp, vp, i64, f32, vp, f32, f32, vp]),
     "stx_scalar_op": (i32, [vp, i32, i32, i32, i32, vp]),
+    "stx_lbfgs_state_bytes": (sz, [i32]),
+    "stx_lbfgs_hist_bytes": (sz, [i64, i32]),
+    "stx_lbfgs_ws": (sz, [i64, i32]),
+    "stx_lbfgs_direction": (i32, [vp, vp, vp, vp, i64, i32, f32, f32, vp, vp, vp, sz, vp]),
+    "stx_lbfgs_grad_stats": (i32, [vp, i64, vp, vp, vp, i32, vp, sz, vp]),
     "stx_bias_grad_ws": (sz, [i32, i32]),
     "stx_bias_grad": (i32, [vp, vp, i32, i32, i32, i32, vp, sz, vp]),
     "stx_gram_ws": (sz, [i32, i32, i32]),

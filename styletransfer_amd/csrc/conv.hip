@@ -647,6 +647,10 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     set_error("stx_conv2d: fused phase 2 needs stride 1, p2_wt and p2_c > 0");
     return STX_E_INVALID;
   }
+  if (p.p2_z && p.wt16 && p.wt16 != (const void*)1 && p.cin > 0 && p.in_mode != STX_IN_RAW) {
+    set_error("stx_conv2d: the fused Gram-backward phase needs a raw-input conv");
+    return STX_E_INVALID;
+  }
   if (p.up_dp && (!p.up_z || p.ho < 2 || p.wo < 2)) {
     set_error("stx_conv2d: unpool epilogue needs up_z");
     return STX_E_INVALID;

@@ -253,16 +253,17 @@ struct C16 {
                 "fused Gram planes fit");
 };
 
-// DBG (profiling experiments only, tools/bench_conv.py --dbg): bit 0 skips the
-// epilogue, bit 1 skips the per-chunk restaging after chunk 0
-// P2: 0 plain conv, 1 3x3 + fused fp32 Gram-backward phase (shared epilogue),
-//     2 the split Gram-backward phase alone (1x1 mode, cin == 0)
-template <int TW, int LM, int DBG = 0, int P2 = 0, int NI = 2>
+// The v1 main loop: the stride-2 downsampling convs (LM_S2) and the split
+// Gram-backward phase alone (P2 = 2, the 1x1 mode with cin == 0); every other
+// stride-1 launch runs the v2 loop below.
+// P2: 0 plain conv, 2 the split Gram-backward phase alone (1x1 mode, cin == 0)
+template <int TW, int LM, int P2 = 0, int NI = 2>
 __global__ void __launch_bounds__(256, 2)
 conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
   constexpr int S = LM == LM_S2 ? 2 : 1;
   using C = C16<TW, NI, S>;
   constexpr bool RP = TW == 64 && NI == 2 && S == 1;  // row-pair tiles (fused pool / unpool)
+  static_assert(P2 == 0 || P2 == 2, "v1 kernel: plain conv or the split phase alone");
   static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
   constexpr int BM = C::BM;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
@@ -272,20 +273,6 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
-  {  // experiment: stagger co-resident blocks (mode in tiles_x's top byte)
-    const int mode = tiles_x >> 24;
-    tiles_x &= 0xffffff;
-    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
-    bool late = false;
-    if (mode == 1) late = bid & 1;
-    else if (mode == 2) late = (bid >> 3) & 1;
-    else if (mode == 3) late = (bid >> 8) & 1;
-    else if (mode == 4) late = (blockIdx.x >> 4) & 1;
-    if (late) {
-      __builtin_amdgcn_s_sleep(31);
-      __builtin_amdgcn_s_sleep(31);
-    }
-  }
 
   const int tile = blockIdx.x;
   const int ty0 = (tile / tiles_x) * C::TH, tx0 = (tile % tiles_x) * TW;
@@ -404,9 +391,9 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
   if (nchunks) fetch(0);
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     __syncthreads();  // previous chunk's operand reads done
-    if (!(DBG & 2) || chunk == 0) store();
+    store();
     __syncthreads();
-    if (chunk + 1 < nchunks && !(DBG & 2)) fetch(chunk + 1);  // in flight across the MFMA loop
+    if (chunk + 1 < nchunks) fetch(chunk + 1);  // in flight across the MFMA loop
     // Operand reads run one product phase ahead of their use: a tap's three phases
     // (hi*hi, hi*lo, lo*hi; 2 x NI MFMAs each) are each preceded by the reads the NEXT
     // phase needs (B lo, then A lo, then the next tap's A hi + B hi), so every LDS
@@ -461,28 +448,8 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
       }
     }
   }
-  if ((DBG & 1) && P2 != 2) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[i][j][r];
-    if (t == 12345.f) p.y[tid] = t;
-    return;
-  }
   __syncthreads();  // the epilogue's phase 2 re-uses the LDS
   const EpiTile et{n, co0, ty0, tx0, 0, wave, h, l32};
-  if constexpr (P2 == 1) {
-    // 3x3 data-gradient + Gram-backward phase: the phase runs on fp32 MFMA inside the
-    // shared epilogue (its z/A streams are latency-bound either way; the split phase
-    // measured slower after the 3x3 main loop)
-    conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, true>(acc, p, et, descale,
-                                                     reinterpret_cast<float*>(smem),
-                                                     reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
-    return;
-  }
   if constexpr (P2 == 2) {
     // main accumulator first: de-scale, *acc_scale, ReLU mask (the order of the
     // fp32 path), then the split Gram-backward phase adds s2 * A[n] . p2_z
@@ -506,18 +473,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
           acc[i][j][r] = v;
         }
     }
-    if (!(DBG & 4)) phase2_f16<TW>(acc, p, n, co0, ty0, tx0, wave, h, l32, smem);
-    if (DBG & 1) {  // profiling: skip the epilogue
-      float t = 0.f;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) t += acc[i][j][r];
-      if (t == 12345.f) p.y[tid] = t;
-      return;
-    }
+    phase2_f16<TW>(acc, p, n, co0, ty0, tx0, wave, h, l32, smem);
     stx_conv_params q = p;
     q.p2_z = nullptr;
     q.acc_scale = nullptr;
@@ -526,7 +482,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
                                            reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
     return;
   }
-  if (conv_epilogue_plain<TW, NI, RP, (DBG >> 3) & 3>(acc, p, et, descale, smem)) return;
+  if (conv_epilogue_plain<TW, NI, RP>(acc, p, et, descale, smem)) return;
   conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, false>(acc, p, et, descale, reinterpret_cast<float*>(smem),
                                          reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
 }
@@ -556,28 +512,9 @@ struct C16v2 {
   static_assert(TW != 64 || NI != 2 || GramPlanes<256>::BYTES <= LDS_BYTES, "Gram planes fit");
 };
 
-// TR: operands swapped in the MFMAs (accumulators D[pixel][co]) and the transposed
-// forward epilogue (conv_epilogue_tr): 64 x 4 tiles, the plain forward epilogue only
-// 128-pixel tiles (NI = 1) fit three blocks per CU (50 KB of LDS each, <= 168 VGPRs)
-// STAMP (diagnostic build only, STX_CONV_STAMP=1; never timed): per wave, shader-clock
-// sums of the loop's segments -> g_conv_stamps (read by stx_debug_conv_stamps):
-// [0] prologue (loads + first staging), [1] tap 0 MFMAs + the step's staging, [2] taps
-// 1-2 MFMAs, [3] the step's barrier wait, [4] epilogue, [5] steps
-__device__ unsigned long long g_conv_stamps[4096 * 8];
-
-__device__ __forceinline__ unsigned long long conv_stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-
-template <int TW, int LM, int P2, int NI, bool TR = false, bool STAMP = false>
+template <int TW, int LM, int P2, int NI>
 __global__ void __launch_bounds__(256, (NI == 1 && TW <= 32) ? 3 : 2)
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
-  unsigned long long st_t0 = 0, st_seg[6] = {0, 0, 0, 0, 0, 0};
-  if constexpr (STAMP) st_t0 = conv_stamp();
   using C = C16v2<TW, NI>;
   constexpr bool RP = TW == 64 && NI == 2;  // row-pair tiles (fused pool / unpool)
   static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
@@ -597,28 +534,11 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
                                  : (int)blockIdx.x;
   if (first >= ntiles) return;
 
-  {  // experiments (STX_V2_KNOB): 1..7 = stagger the second-dispatched half of the blocks
-     // (blockIdx >> 8 odd: the co-resident partner under round-robin placement) by k x
-     // 1024 cycles; 8 = s_setprio(1) for that half
-    const int knob = (tiles_x >> 24) & 15;
-    if (knob && ((blockIdx.x >> 8) & 1)) {
-      if (knob == 8) {
-        __builtin_amdgcn_s_setprio(1);
-      } else {
-        for (int k = 0; k < knob; ++k) __builtin_amdgcn_s_sleep(16);
-      }
-    }
-    // STX_V2_PHASE = K (grids of more than one round of resident blocks): the second block
-    // of each CU in the FIRST round (linear block id in [256, 512)) starts K x 8128 cycles
-    // late; the slots it frees then stay out of phase with their partners for the later
-    // rounds, so one block's epilogue stores run under the other's MFMA loop
-    const int pk = (tiles_x >> 28) & 7;
-    const int lin = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-    if (pk && lin >= 256 && lin < 512) {
-      for (int k = 0; k < pk; ++k) __builtin_amdgcn_s_sleep(127);
-    }
-  }
-  tiles_x &= 0xffffff;
+  // the second-dispatched half of the blocks (blockIdx >> 8 odd: the co-resident partner
+  // under round-robin placement) at wave priority 1, so the two blocks of a CU drift
+  // apart instead of issuing their epilogue stores together (same-process A/B:
+  // Gatys 679.6 -> 674.5 us per iteration, fast_st within noise)
+  if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
   const int nchunks = cdiv(p.cin, 16);
   const int nsteps = 3 * nchunks;
   const int ex = amax_exp(read_amax(p.in_amax));
@@ -756,11 +676,6 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
       for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    unsigned long long st_a = 0;
-    if constexpr (STAMP) {
-      st_a = conv_stamp();
-      st_seg[0] += st_a - st_t0;
-    }
 
     for (int c = 0; c < nchunks; ++c) {
       const int hbo = (c & 1) * C::HB;
@@ -787,8 +702,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
           for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
-              acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_f16(b[j], a[i], acc[i][j], 0, 0, 0)
-                             : __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
         };
         f16x8 ahi[2], alo[2], bhi[NI], blo[NI];
         rdA(0, 0, ahi);
@@ -828,11 +742,6 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
               for (int r = (k + 1) % 3; r < C::NIT; r += 3) ld_halo(cn, r);
             }
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (STAMP) {
-              const unsigned long long t = conv_stamp();
-              st_seg[1] += t - st_a;
-              st_a = t;
-            }
           }
           if (tl + 1 < 3) {
 #pragma unroll
@@ -841,31 +750,14 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
             for (int j = 0; j < NI; ++j) bhi[j] = nbh[j];
           }
         }
-        if constexpr (STAMP) {
-          const unsigned long long t = conv_stamp();
-          st_seg[2] += t - st_a;
-          st_a = t;
-        }
         __syncthreads();  // this step's reads done; the staged buffers are complete
-        if constexpr (STAMP) {
-          const unsigned long long t = conv_stamp();
-          st_seg[3] += t - st_a;
-          st_a = t;
-          st_seg[5] += 1;
-        }
       }
     }
 
     EpiTile et{n, co0, ty0, tx0, 0, wave, h, l32};
     et.tile = tile;
     et.ntiles = ntiles;
-    if constexpr (TR) {
-      static_assert(TW == 64 && NI == 2 && P2 == 0, "transposed epilogue: 64 x 4 forward tiles");
-      if (p.relu_out)
-        conv_epilogue_tr<true>(acc, p, et, descale, smem);
-      else
-        conv_epilogue_tr<false>(acc, p, et, descale, smem);
-    } else if constexpr (P2 == 1) {
+    if constexpr (P2 == 1) {
       conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, true>(acc, p, et, descale,
                                                        reinterpret_cast<float*>(smem),
                                                        reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
@@ -875,161 +767,47 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
                                                           reinterpret_cast<float*>(smem),
                                                           reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
     }
-    if constexpr (STAMP) st_seg[4] += conv_stamp() - st_a;
   }
-  if constexpr (STAMP) {
-    const int slot = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + wave;
-    if (lane == 0 && slot < 4096) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) g_conv_stamps[(size_t)slot * 8 + k] = st_seg[k];
-    }
-  }
-}
-
-// default 8: s_setprio(1) for the second-dispatched half of the blocks (measured
-// tools/ab_engine.py, same process: Gatys 679.6 -> 674.5 us, fast_st within noise;
-// staggering that half by 1-4 x 1024 cycles instead: no gain)
-static int v2_knob() {
-  const char* e = getenv("STX_V2_KNOB");
-  return e ? (atoi(e) & 15) : 8;
-}
-
-// STX_CONV_V2=0 selects the v1 main loop (read per launch, so a tool can A/B both in
-// one process)
-static bool v2_on() {
-  const char* e = getenv("STX_CONV_V2");
-  return !(e && atoi(e) == 0);
-}
-
-// STX_CONV_TR=1: the transposed accumulators + epilogue for the forward launches.  Off by
-// default: measured (tools/ab_v2.py, same process) conv1_2 fwd +pool+Gram 86.1 -> 87.1 us,
-// plain 66.1 -> 64.2, conv2_2 +pool 58.6 -> 60.7, B8 conv1_2 +pool 127.2 -> 133.4 -- the
-// register-resident Gram and 16-B stores do not pay for themselves in these launches
-static bool tr_on() {
-  const char* e = getenv("STX_CONV_TR");
-  return e && atoi(e) != 0;
-}
-
-// the first-round phase offset (see the kernel), K x 8128 cycles, for multi-round grids:
-// STX_V2_PHASE=K (read per launch), off by default.  Measured: Gatys 663.5 -> 654.5 and
-// 662.1 -> 658.3 us per iteration in same-process A/Bs with K = 3 on the two-round grids,
-// but bench.py on one box 1419-1425 vs 1424-1431 it/s (noise) with the isolated conv1_2
-// launches 2 us slower each (back-to-back launches of one kernel already overlap across
-// the launch boundary); on every multi-round grid the fast_st step lost 13-66 us.
-static int v2_phase(long long blocks) {
-  const char* e = getenv("STX_V2_PHASE");
-  return e && blocks > 512 ? (atoi(e) & 7) : 0;
 }
 
 template <int TW, int LM, int NI>
 static int launch16v2(const stx_conv_params& p, hipStream_t st) {
   using C = C16v2<TW, NI>;
-  const int tiles_x0 = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
-  const int ntiles = tiles_x0 * tiles_y;
-  int tiles_x = tiles_x0 | (v2_knob() << 24);
-  const int gy = cdiv(p.cout, C::BM), gz = p.n;
-  dim3 grid(ntiles, gy, gz);
-  if constexpr (NI == 2) {  // 2 blocks per CU x 256 CUs resident: only multi-round grids
-    const int pk = v2_phase((long long)ntiles * gy * gz);
-    if (pk) tiles_x |= pk << 28;
-  }
-  if constexpr (TW == 64 && NI == 2) {
-    if (tr_on() && !p.p2_z && !p.mask && !p.aux && !p.accumulate && !p.acc_scale && !p.up_dp &&
-        !p.pool_sum && p.wo % 4 == 0) {
-      hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI, true>), grid, dim3(256), 0, st,
-                         p, tiles_x, ntiles);
-      return check_launch("stx_conv2d(f16x3 v2, transposed)");
-    }
-  }
-  if constexpr (NI == 2 && LM == STX_IN_RAW) {
-    if (p.p2_z) {
+  const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
+  const int ntiles = tiles_x * tiles_y;
+  dim3 grid(ntiles, cdiv(p.cout, C::BM), p.n);
+  if (p.p2_z) {
+    // the fused Gram-backward phase: 256-pixel tiles of a raw-input data gradient
+    if constexpr (NI == 2 && LM == STX_IN_RAW) {
       hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 1, NI>), grid, dim3(256), 0, st, p,
                          tiles_x, ntiles);
       return check_launch("stx_conv2d(f16x3 v2 + phase 2)");
     }
+    set_error("stx_conv2d: the fused Gram-backward phase needs a raw-input conv");
+    return STX_E_INVALID;
   }
-  if constexpr (TW == 64 && NI == 2 && LM == STX_IN_RELU) {
-    const char* se = getenv("STX_CONV_STAMP");  // diagnostic build (tools/stamp_conv.py)
-    if (se && atoi(se) != 0) {
-      hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI, false, true>), grid, dim3(256),
-                         0, st, p, tiles_x, ntiles);
-      return check_launch("stx_conv2d(f16x3 v2, stamps)");
-    }
-  }
-    hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI>), grid, dim3(256), 0, st, p,
-                       tiles_x, ntiles);
+  hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI>), grid, dim3(256), 0, st, p,
+                     tiles_x, ntiles);
   return check_launch("stx_conv2d(f16x3 v2)");
-}
-
-static int dbg_mode() {
-  static const int m = [] {
-    const char* e = getenv("STX_CONV16_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
-
-static int stagger_mode() {
-  static const int m = [] {
-    const char* e = getenv("STX_STAGGER");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
 }
 
 template <int TW, int LM, int NI>
 static int launch16(const stx_conv_params& p, hipStream_t st) {
   using C = C16<TW, NI, LM == LM_S2 ? 2 : 1>;
-  if constexpr (LM != LM_S2) {
-    // the v2 main loop (stride 1, a 3x3 K loop; not the 1x1 Gram-backward mode, the
-    // split phase-2 variant or the profiling builds)
-    static const bool split_p2 = [] {
-      const char* e = getenv("STX_P2_SPLIT");
-      return e && atoi(e) != 0;
-    }();
-    if (v2_on() && p.cin > 0 && dbg_mode() == 0 && !(p.p2_z && split_p2))
-      return launch16v2<TW, LM, NI>(p, st);
-  }
-  const int tiles_x0 = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
-  const int tiles_x = tiles_x0 | (stagger_mode() << 24);
-  dim3 grid(tiles_x0 * tiles_y, cdiv(p.cout, C::BM), p.n);
-  if constexpr (TW == 64 && LM == STX_IN_RELU && NI == 2) {
-    switch (dbg_mode()) {
-      case 1: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 1>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
-      case 2: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 2>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
-      case 3: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 3>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
-      case 8: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 8>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
-      case 16: hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 16>), grid, dim3(256), 0, st, p, tiles_x); return check_launch("dbg");
-      default: break;
-    }
-  }
+  // the v2 main loop: stride 1 with a 3x3 K loop (not the 1x1 Gram-backward mode)
+  if constexpr (LM != LM_S2)
+    if (p.cin > 0) return launch16v2<TW, LM, NI>(p, st);
+  const int tiles_x = cdiv(p.wo, TW), tiles_y = cdiv(p.ho, C::TH);
+  dim3 grid(tiles_x * tiles_y, cdiv(p.cout, C::BM), p.n);
   if (p.p2_z) {
     if constexpr (LM == STX_IN_RAW && NI == 2) {
-      static const bool split_p2 = [] {
-        const char* e = getenv("STX_P2_SPLIT");
-        return e && atoi(e) != 0;
-      }();
-      if (p.cin == 0 && TW == 64 && dbg_mode() >= 4) {  // profiling the 1x1 mode
-        if (dbg_mode() == 4)
-          hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 4, 2>), grid, dim3(256), 0, st, p, tiles_x);
-        else if (dbg_mode() == 5)
-          hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 5, 2>), grid, dim3(256), 0, st, p, tiles_x);
-        else
-          hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 1, 2>), grid, dim3(256), 0, st, p, tiles_x);
-      } else if (p.cin == 0 || split_p2)
-        hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 0, 2>), grid, dim3(256), 0, st, p,
-                           tiles_x);
-      else
-        hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 0, 1>), grid, dim3(256), 0, st, p,
-                           tiles_x);
-    } else {
-      set_error("stx_conv2d: the fused Gram-backward phase needs a raw-input conv");
-      return STX_E_INVALID;
+      hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 2>), grid, dim3(256), 0, st, p, tiles_x);
+      return check_launch("stx_conv2d(f16x3, split phase 2 alone)");
     }
-    return check_launch("stx_conv2d(f16x3 + phase 2)");
+    set_error("stx_conv2d: the fused Gram-backward phase needs a raw-input conv");
+    return STX_E_INVALID;
   }
-  hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 0, 0, NI>), grid, dim3(256), 0, st, p,
-                     tiles_x);
+  hipLaunchKernelGGL((conv3x3_f16x3_kernel<TW, LM, 0, NI>), grid, dim3(256), 0, st, p, tiles_x);
   return check_launch("stx_conv2d(f16x3)");
 }
 
@@ -1040,19 +818,12 @@ template <int TW, int LM>
 static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
   const long long blocks2 = (long long)cdiv(p.wo, TW) * cdiv(p.ho, 256 / TW) *
                             cdiv(p.cout, 64) * p.n;
-  // 256-pixel-tile grids smaller than this use 128-px tiles (read per launch: A/B tools)
-  const char* ni1_env = getenv("STX_NI1_BELOW");
-  const int ni1_below = ni1_env ? atoi(ni1_env) : 512;
-  if (blocks2 < ni1_below && !p.pool_out && !p.p2_z && !p.gram_part) {
+  // 256-pixel-tile grids smaller than two resident rounds use 128-px tiles
+  if (blocks2 < 512 && !p.pool_out && !p.p2_z && !p.gram_part) {
     // 128-pixel tiles as 32 x 4 rather than 64 x 2: a 34 x 6 halo instead of 66 x 4 (23 %
     // less staging per tile) -- Gatys NI=1 launches 37-40 -> 35-39 us, ITN residual convs
-    // 35.3 -> 34.7 us (same-box profile); STX_TW32_NI1=0 restores 64 x 2
-    static const bool tw32 = [] {
-      const char* e = getenv("STX_TW32_NI1");
-      return !(e && atoi(e) == 0);
-    }();
-    if constexpr (TW == 64)
-      if (tw32) return launch16<32, LM, 1>(p, st);
+    // 35.3 -> 34.7 us (same-box profile)
+    if constexpr (TW == 64) return launch16<32, LM, 1>(p, st);
     return launch16<TW, LM, 1>(p, st);
   }
   // 256-pixel tiles of the transforming loaders (ReLU, nearest x2, zero-dilation) without
@@ -1060,13 +831,8 @@ static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
   // (34 x 10 halo) instead of 64 x 4 (66 x 6) -- same-box profile of the fast_st step:
   // upsampling convs 92 -> 84 and 49 -> 45 us, dilated (stride-2 dgrad) 89 -> 85 and
   // 55 -> 52, ReLU 101 -> 98; raw-input launches measured 1 % slower and keep 64 x 4.
-  // STX_TW32_NI2=0 restores 64 x 4 everywhere.
-  static const bool tw32b = [] {
-    const char* e = getenv("STX_TW32_NI2");
-    return !(e && atoi(e) == 0);
-  }();
   if constexpr (TW == 64 && LM != STX_IN_RAW)
-    if (tw32b && !p.pool_out && !p.gram_part && !p.p2_z && !p.up_dp)
+    if (!p.pool_out && !p.gram_part && !p.p2_z && !p.up_dp)
       return launch16<32, LM, 2>(p, st);
   return launch16<TW, LM, 2>(p, st);
 }
@@ -1402,11 +1168,4 @@ extern "C" int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax,
                      reinterpret_cast<_Float16*>(wt16), w_amax, cout, cin, transpose, gin16,
                      gout64);
   return check_launch("stx_conv_weight_prep16");
-}
-
-// diagnostic: copy out the STAMP build's per-wave segment sums (tools/stamp_conv.py)
-extern "C" int stx_debug_conv_stamps(unsigned long long* host, int n) {
-  if (!host || n <= 0 || n > 4096 * 8) return STX_E_INVALID;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(stx::g_conv_stamps), (size_t)n * 8, 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : STX_E_INVALID;
 }

@@ -466,25 +466,8 @@ bool conv9_on() {
   return on;
 }
 
-int dbg9() {
-  static const int m = [] {
-    const char* e = getenv("STX_CONV9_DBG");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
-
-#define CONV9_LAUNCH(KERN, grid, st, p, tx, ty)                                            \
-  switch (dbg9()) {                                                                        \
-    case 1: hipLaunchKernelGGL(KERN<1>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
-    case 2: hipLaunchKernelGGL(KERN<2>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
-    case 3: hipLaunchKernelGGL(KERN<3>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
-    case 4: hipLaunchKernelGGL(KERN<4>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
-    case 7: hipLaunchKernelGGL(KERN<7>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
-    case 8: hipLaunchKernelGGL(KERN<8>, grid, dim3(NT), 0, st, p, tx, ty); break;          \
-    case 24: hipLaunchKernelGGL(KERN<24>, grid, dim3(NT), 0, st, p, tx, ty); break;        \
-    default: hipLaunchKernelGGL(KERN<0>, grid, dim3(NT), 0, st, p, tx, ty); break;         \
-  }
+#define CONV9_LAUNCH(KERN, grid, st, p, tx, ty) \
+  hipLaunchKernelGGL(KERN<0>, grid, dim3(NT), 0, st, p, tx, ty)
 
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);

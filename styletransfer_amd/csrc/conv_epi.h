@@ -149,7 +149,7 @@ __device__ __forceinline__ void gram_store(float* out, const f32x16& g, int wave
 }
 
 // conv16's 64 x 256 tile: acc holds y; lane_ok[j] marks pixels inside the image
-template <int NI, int GDBG = 0>  // GDBG (profiling): 1 skips the MFMAs, 2 the stores
+template <int NI>
 __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
                                                const stx_conv_params& p, const EpiTile& t,
                                                const bool (&lane_ok)[NI], uint32_t vmax_u,
@@ -171,7 +171,7 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
         gram_put(H, GP::HP, ch, wave * 64 + j * 32 + l32, lane_ok[j] ? acc[i][j][r] * sx : 0.f);
       }
   __syncthreads();
-  if (wave < 3 && !(GDBG & 1)) {
+  if (wave < 3) {
     f32x16 g;
 #pragma unroll
     for (int q = 0; q < 16; ++q) g[q] = 0.f;
@@ -182,13 +182,6 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
     const int tix = t.tile >= 0 ? t.tile : (int)blockIdx.x;
     const int ntl = t.tile >= 0 ? t.ntiles : (int)gridDim.x;
     float* out = p.gram_part + ((size_t)blockIdx.z * ntl + tix) * 4096;
-    if (GDBG & 2) {
-      float tt = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) tt += g[r];
-      if (tt == 12345.f) out[0] = tt;
-      return;
-    }
     gram_store(out, g, wave, h, l32);
   }
 }
@@ -196,7 +189,7 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
 // AUX: value += aux_scale * aux (a residual block's skip gradient, ResLink), loaded
 // through a descriptor at the store offsets
 // POOLSUM: pool_out = 2x2 sum of the output and no y stores (stx_conv_params.pool_sum)
-template <int TW, int NI, bool ROWPAIR, bool RELU, int GDBG = 0, bool AUX = false,
+template <int TW, int NI, bool ROWPAIR, bool RELU, bool AUX = false,
           bool POOLSUM = false>
 __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
                                                          const stx_conv_params& p,
@@ -305,188 +298,29 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
   }
   if constexpr (NI == 2 && TW == 64 && !RELU) if (p.gram_part) {
     // the max over valid pixels of all 64 rows (cout == 64: rows_full)
-    conv_gram_tile<NI, GDBG>(acc, p, t, lane_ok, vmax_u, smem);
+    conv_gram_tile<NI>(acc, p, t, lane_ok, vmax_u, smem);
   }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
-template <int TW, int NI, bool ROWPAIR, int GDBG = 0>
+template <int TW, int NI, bool ROWPAIR>
 __device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const stx_conv_params& p,
                                                     const EpiTile& t, float scale, char* smem) {
   if (p.mask || p.accumulate || p.acc_scale || p.up_dp || p.p2_z) return false;
   if (p.pool_sum) {  // validated by stx_conv2d: plain epilogue, row-pair tiles
     if constexpr (ROWPAIR)
-      conv_epilogue_plain_body<TW, NI, ROWPAIR, false, 0, false, true>(acc, p, t, scale, smem);
+      conv_epilogue_plain_body<TW, NI, ROWPAIR, false, false, true>(acc, p, t, scale, smem);
     return true;
   }
   if (p.aux) {
     if (p.relu_out || p.pool_out || p.gram_part) return false;
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, 0, true>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, true>(acc, p, t, scale, smem);
   } else if (p.relu_out) {
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, true, GDBG>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, true>(acc, p, t, scale, smem);
   } else {
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, GDBG>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false>(acc, p, t, scale, smem);
   }
   return true;
-}
-
-// ---- transposed accumulators (conv16 v2, TR) ----------------------------------------
-// The main loop ran v_mfma with the operands swapped, so acc[i][j] is D[pixel][co]: lane
-// (h, l32) holds output channel co0 + 32 i + l32 and, in register r, pixel
-// 8 (r / 4) + 4 h + r % 4 of N-block j (row-pair tiles: row 2 (wn / 2) + j, columns
-// 32 (wn % 2) + [0, 32)).  The forward epilogue of the VGG / ITN convs (bias, optional
-// ReLU, optional fused ReLU+MaxPool output, optional Gram partials, optional out_amax):
-//  * y: four consecutive pixels of one channel per 16-B store;
-//  * pool_out: the 2x2 window is registers (r, r + 1) of N-blocks 0 and 1 -- in the lane;
-//    two pooled pixels per 8-B store;
-//  * gram_part: the K (pixel) order of a 16-deep MFMA step taken as the lane's registers
-//    8t..8t+7 (a bijection onto 16 pixels shared by both operands), so channel blocks I
-//    and J are the lane's own split registers: each wave adds the three upper 32 x 32
-//    blocks over its 64 pixels at its own power-of-two scale (no LDS transpose, no
-//    barrier), then the four waves' partials are summed once through LDS in wave order.
-// Needs wo % 4 == 0 (whole 16-B groups) and TW == 64, NI == 2.
-typedef unsigned int u32x4_epi __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2_epi __attribute__((ext_vector_type(2)));
-
-template <bool RELU>
-__device__ __forceinline__ void conv_epilogue_tr(f32x16 (&acc)[2][2], const stx_conv_params& p,
-                                                 const EpiTile& t, float scale, char* smem) {
-  const size_t plane = (size_t)p.ho * p.wo;
-  const int h = t.h, l32 = t.l32, wn = t.wn;
-  const uint32_t pb = (uint32_t)plane * 4u;
-  const auto ry = make_srd(p.y + ((size_t)t.n * p.cout + t.co0) * plane,
-                           (uint32_t)max(0, p.cout - t.co0) * pb);
-  float bias_l[2];
-  bool cok[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int co = t.co0 + 32 * i + l32;
-    cok[i] = co < p.cout;
-    bias_l[i] = (p.bias && cok[i]) ? p.bias[co] : 0.f;
-  }
-  const int oyb = t.ty0 + 2 * (wn >> 1);          // row of N-block 0
-  const int oxb = t.tx0 + 32 * (wn & 1) + 4 * h;  // column of register 0
-  uint32_t vmax_u = 0u;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int oy = oyb + j;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ox = oxb + 8 * q;
-        const bool in = cok[i] && oy < p.ho && ox < p.wo;
-        f32x4 v4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = fmaf(acc[i][j][4 * q + e], scale, bias_l[i]);
-          if (RELU) v = fmaxf(v, 0.f);
-          v4[e] = v;
-          vmax_u = max(vmax_u, in ? (__float_as_uint(v) & 0x7fffffffu) : 0u);
-          acc[i][j][4 * q + e] = in ? v : 0.f;  // pooled / Gram copy: outside pixels 0
-        }
-        const uint32_t off = in ? (uint32_t)(32 * i + l32) * pb + (uint32_t)(oy * p.wo + ox) * 4u
-                                : BUF_OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_epi, v4), ry, off, 0, 0);
-      }
-    }
-  if (p.pool_out) {
-    // relu(maxpool2x2(y)) on IEEE bit patterns (relu = max_i32(bits, 0); a NaN beats every
-    // number), torch floor mode: the window needs both rows and both columns
-    const int hp = p.ho >> 1, wp = p.wo >> 1;
-    const int py = oyb >> 1;
-    const uint32_t ppb = (uint32_t)hp * (uint32_t)wp * 4u;
-    const auto rp = make_srd(p.pool_out + ((size_t)t.n * p.cout + t.co0) * hp * wp,
-                             (uint32_t)max(0, p.cout - t.co0) * ppb);
-    auto rb = [](float v) -> uint32_t {
-      const int b = __float_as_int(v);
-      const uint32_t a = (uint32_t)b & 0x7fffffffu;
-      return a > 0x7f800000u ? a : (uint32_t)max(b, 0);
-    };
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int px = (oxb + 8 * q) >> 1;
-        const bool ok = cok[i] && py < hp && px < wp && oyb + 1 < p.ho;
-        u32x2_epi m2;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int r = 4 * q + 2 * e;
-          m2[e] = max(max(rb(acc[i][0][r]), rb(acc[i][0][r + 1])),
-                      max(rb(acc[i][1][r]), rb(acc[i][1][r + 1])));
-        }
-        const uint32_t off = ok ? (uint32_t)(32 * i + l32) * ppb + (uint32_t)(py * wp + px) * 4u
-                                : BUF_OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(m2, rp, off, 0, 0);
-      }
-  }
-  if constexpr (!RELU) if (p.gram_part) {
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-    uint32_t wmax = 0u;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) wmax = max(wmax, __float_as_uint(acc[i][j][r]) & 0x7fffffffu);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
-    int e2 = 0;
-    frexpf(__uint_as_float(wmax), &e2);
-    e2 = min(max(e2, -60), 60);
-    const float gs = __builtin_ldexpf(1.f, 15 - e2);
-    f32x16 g[3];
-#pragma unroll
-    for (int b3 = 0; b3 < 3; ++b3)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) g[b3][q] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int tk = 0; tk < 2; ++tk) {
-        h8 fh[2], fl[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = acc[i][j][8 * tk + e] * gs;
-            const _Float16 vh = (_Float16)v;
-            fh[i][e] = vh;
-            fl[i][e] = (_Float16)(v - (float)vh);
-          }
-#pragma unroll
-        for (int b3 = 0; b3 < 3; ++b3) {
-          const int I = b3 == 2 ? 1 : 0, J = b3 == 0 ? 0 : 1;
-          g[b3] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[I], fh[J], g[b3], 0, 0, 0);
-          g[b3] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fh[I], fl[J], g[b3], 0, 0, 0);
-          g[b3] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fl[I], fh[J], g[b3], 0, 0, 0);
-        }
-      }
-    const float ginv = __builtin_ldexpf(1.f, 2 * e2 - 30);
-    float* gsum = reinterpret_cast<float*>(smem);  // [wave][block][lane][16]: 48 KB
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int b3 = 0; b3 < 3; ++b3) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) g[b3][q] *= ginv;
-      *reinterpret_cast<f32x16*>(gsum + ((wn * 3 + b3) * 64 + lane) * 16) = g[b3];
-    }
-    __syncthreads();
-    if (wn < 3) {
-      f32x16 sum = *reinterpret_cast<const f32x16*>(gsum + ((0 * 3 + wn) * 64 + lane) * 16);
-#pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        const f32x16 o = *reinterpret_cast<const f32x16*>(gsum + ((w * 3 + wn) * 64 + lane) * 16);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) sum[q] += o[q];
-      }
-      const int tix = t.tile >= 0 ? t.tile : (int)blockIdx.x;
-      const int ntl = t.tile >= 0 ? t.ntiles : (int)gridDim.x;
-      gram_store(p.gram_part + ((size_t)blockIdx.z * ntl + tix) * 4096, sum, wn, h, l32);
-    }
-  }
-  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
 template <int BM, int TW, int NPIX, int CIS2, bool ROWPAIR = false, int NI = 2,

@@ -590,8 +590,10 @@ int gram_bwd16_launch(const Gb16& p, int nimg, int c, hipStream_t st) {
     const char* e = getenv("STX_GB_NB");
     return e ? atoi(e) : 0;
   }();
-  const char* v1e = getenv("STX_GB_V1");  // read per launch: A/B of the two loop schedules
-  const bool v1 = v1e && atoi(v1e) != 0;
+  static const bool v1 = [] {  // STX_GB_V1=1: the run-time-branch loop schedule (A/B)
+    const char* e = getenv("STX_GB_V1");
+    return e && atoi(e) != 0;
+  }();
   const bool two = (nb_env ? nb_env : 2) == 2 && p.w % 32 == 0;
   if (c == 64) {
     if (v1 || p.aux)

@@ -333,6 +333,19 @@ class StyleNetwork(nn.Module):
         assert isinstance(style_image, torch.Tensor), "Images need to be already loaded"
         assert isinstance(content_image, torch.Tensor), "Images need to be already loaded"
         content_image = _dev(content_image)
+        if self._standard_layout() and content_image.is_cuda:
+            # the fused loss engine: direction, closure and gradient statistics replayed
+            # as one hipGraph per L-BFGS iteration (vgg.GatysLBFGS), torch's control flow
+            targets = [l.target for l, _ in self.style_losses]
+            eng = V.GatysLBFGS(self.features(), None, content_image.contiguous(),
+                               style_weight, content_weight, targets=targets)
+
+            def log(loss):
+                if LOGGER.isEnabledFor(logging.DEBUG):
+                    LOGGER.debug("Loss: %s", loss)
+            for _ in tqdm(range(steps)):
+                eng.step(on_eval=log)
+            return eng.x.requires_grad_()
         image = content_image.clone()
         opt = self.get_content_optimizer(image, optt=optim.LBFGS)  # -> the HIP L-BFGS
 

@@ -282,6 +282,12 @@ class TrainedSlabs:
         self._jobs = (N.WprepJob * len(jobs))(*jobs)
         self._njobs = len(jobs)
 
+    def release_retired(self):
+        """Drop the slabs of earlier generations: call after the owner re-captured its
+        graphs (a graph of an older generation refuses to replay, so nothing reads
+        them any more)."""
+        self._retired.clear()
+
     def prep(self):
         if any(c.weight.data_ptr() != s[0] for c, s in zip(self.convs, self.slabs)):
             self._build()  # a parameter was re-homed

@@ -78,17 +78,23 @@ class FlatAdam:
 
 
 class LBFGS(torch.optim.Optimizer):
-    """torch.optim.LBFGS (torch 2.10 semantics, no line search) on libstx vector
-    kernels, for StyleNetwork.train_gatys (stransfer/network.py:411-458:
+    """torch.optim.LBFGS (torch 2.10 semantics, no line search) on libstx, for
+    StyleNetwork.train_gatys (stransfer/network.py:411-458:
     `optim.LBFGS([input_img.requires_grad_()])` with the defaults lr=1, max_iter=20,
     max_eval=25, tolerance_grad=1e-7, tolerance_change=1e-9, history_size=100).
 
-    Every vector operation (dot products, the two-loop recursion, the parameter
-    update) is a HIP kernel (stx_vec_reduce / stx_vec_axpby); the 0-d quantities
-    torch keeps as device tensors (ys, rho_i, alpha_i, H_diag, the step size t) stay
-    in one device scalar array, so the recursion runs without host round trips.
-    The host reads back exactly the values torch's control flow branches on
-    (ys > 1e-10, g.d, max|g|, max|t d|, the closure's loss)."""
+    The direction is torch's two-loop recursion in its compact form (lbfgs.hip:
+    stx_lbfgs_direction): the pair update, the history dots, an fp64 m x m solve, the
+    combination d = -H g, g.d and x += t d are a fixed launch sequence whatever the
+    history length, with the history ring, R, Y^T Y, H_diag, t and torch's n_iter in
+    a device state block.  The host reads back exactly the values torch's control
+    flow branches on: after the closure (loss, max|g|) and after the direction (g.d,
+    max|t d|) -- two small reads per iteration, as torch's own `.item()`-style tests.
+    vgg.GatysLBFGS runs the same control flow (`run`) with the direction, the VGG
+    closure and the gradient statistics captured as one hipGraph per iteration (one
+    host read per iteration)."""
+
+    NSCAL = 16
 
     def __init__(self, params, lr=1, max_iter=20, max_eval=None, tolerance_grad=1e-7,
                  tolerance_change=1e-9, history_size=100, line_search_fn=None):
@@ -103,49 +109,53 @@ class LBFGS(torch.optim.Optimizer):
         if len(self.param_groups) != 1 or len(self.param_groups[0]["params"]) != 1:
             raise ValueError("LBFGS optimises one tensor (the image), as the reference")
         self._p = self.param_groups[0]["params"][0]
-        self._hist = history_size
-        # scalar array: 0 ys, 1 yy, 2 H_diag, 3 t, 4 gtd, 5 reduction tmp, 6 coef,
-        # 7 lr, 8 zero, 9 one; rho_k at 16+k, alpha_k at 16+hist+k (ring slots k)
-        self._S = None
+        self._hist = int(history_size)
+        self._buf = None
 
-    # -- kernels ----------------------------------------------------------------
-    def _axpby(self, y, x, a=1.0, a_dev=None, sgn=1.0, b=0.0):
+    # -- device buffers -------------------------------------------------------------
+    def _buffers(self, n, dev):
+        if self._buf is None:
+            from ._native import lib
+            L = lib()
+            m = self._hist
+            hb, sb, wb = L.stx_lbfgs_hist_bytes(n, m), L.stx_lbfgs_state_bytes(m), \
+                L.stx_lbfgs_ws(n, m)
+            if not (hb and sb and wb):
+                raise ValueError(f"LBFGS: history_size {m} outside 1..256")
+            npad = hb // (4 * 2 * (m + 1))
+            self._buf = dict(
+                n=n, hist=torch.zeros(hb // 4, device=dev, dtype=torch.float32),
+                state=torch.zeros(sb, device=dev, dtype=torch.uint8),
+                ws=torch.zeros(wb, device=dev, dtype=torch.uint8),
+                prev_g=torch.zeros(npad, device=dev, dtype=torch.float32),
+                scal=torch.zeros(self.NSCAL, device=dev, dtype=torch.float32),
+                loss=torch.zeros(1, device=dev, dtype=torch.float32))
+        return self._buf
+
+    def grad_stats(self, g, loss=None, clear=None):
+        """scal[0..2] = loss, max|g|, sum|g| of a fresh gradient (stx_lbfgs_grad_stats);
+        loss: a device scalar (None: scal[0] untouched)."""
         from ._native import check, lib
-        check(lib().stx_vec_axpby(y.data_ptr(), None if x is None else x.data_ptr(), y.numel(),
-                                  float(a), a_dev, float(sgn), float(b), ops._stream()),
-              "stx_vec_axpby")
+        b = self._buf
+        check(lib().stx_lbfgs_grad_stats(
+            g.data_ptr(), g.numel(), None if loss is None else loss.data_ptr(),
+            b["scal"].data_ptr(), None if clear is None else clear.data_ptr(),
+            0 if clear is None else clear.numel(), b["ws"].data_ptr(), b["ws"].numel(),
+            ops._stream()), "stx_lbfgs_grad_stats")
 
-    def _red(self, a, b, op, out, mul=None, add=None, sgn=1.0):
+    def direction(self, g):
+        """One torch loop iteration up to the next closure (stx_lbfgs_direction)."""
         from ._native import check, lib
-        L = lib()
-        wp, wn = ops.WS.get(L.stx_vec_ws(), a.device)
-        check(L.stx_vec_reduce(a.data_ptr(), None if b is None else b.data_ptr(), a.numel(), op,
-                               out, mul, add, float(sgn), wp, wn, ops._stream()),
-              "stx_vec_reduce")
+        b = self._buf
+        grp = self.param_groups[0]
+        check(lib().stx_lbfgs_direction(
+            self._p.data.view(-1).data_ptr(), g.data_ptr(), b["prev_g"].data_ptr(),
+            b["hist"].data_ptr(), b["n"], self._hist, float(grp["lr"]),
+            float(grp["tolerance_change"]), b["state"].data_ptr(), b["scal"].data_ptr(),
+            b["ws"].data_ptr(), b["ws"].numel(), ops._stream()), "stx_lbfgs_direction")
 
-    def _sc(self, op, i, j, k):
-        from ._native import check, lib
-        check(lib().stx_scalar_op(self._S.data_ptr(), op, i, j, k, ops._stream()),
-              "stx_scalar_op")
-
-    def _sp(self, i):
-        """device pointer of scalar slot i"""
-        return self._S.data_ptr() + 4 * i
-
-    def _host(self, i):
-        return float(self._S[i])
-
-    def _hosts(self, *idx):
-        """Several scalar slots in one device->host read."""
-        return self._S[list(idx)].tolist()
-
-    def _loss_slot(self, loss, i=10):
-        """Park the closure's loss in slot i (device copy, no sync); returns a thunk
-        for python-number losses, which have no device value."""
-        if torch.is_tensor(loss):
-            self._S[i:i + 1].copy_(loss.detach().reshape(1))
-            return None
-        return float(loss)
+    def _scal(self, *idx):
+        return self._buf["scal"][list(idx)].tolist()  # one device->host read
 
     def _grad(self):
         g = self._p.grad
@@ -155,123 +165,83 @@ class LBFGS(torch.optim.Optimizer):
             g = g.contiguous()
         return g.view(-1)
 
+    def _eval(self, closure):
+        """closure() -> (returned loss, host loss, max|g|): one host read."""
+        with torch.enable_grad():
+            ret = closure()
+        g = self._grad()
+        if torch.is_tensor(ret):
+            self._buf["loss"].copy_(ret.detach().reshape(1))
+            self.grad_stats(g, self._buf["loss"])
+            loss, gmax = self._scal(0, 1)
+        else:
+            self.grad_stats(g)
+            loss, gmax = float(ret), self._scal(1)[0]
+        return ret, loss, gmax, g
+
     @torch.no_grad()
     def step(self, closure):
         if closure is None:
             raise RuntimeError("LBFGS needs a closure")
-        group = self.param_groups[0]
-        lr, max_iter, max_eval = group["lr"], group["max_iter"], group["max_eval"]
-        tol_grad, tol_change = group["tolerance_grad"], group["tolerance_change"]
-        H = self._hist
         p = self._p
-        dev = p.device
-        if self._S is None:
-            self._S = torch.zeros(16 + 2 * H, device=dev, dtype=torch.float32)
-            self._S[7] = float(lr)
-            self._S[9] = 1.0
-        st = self.state[p]
+        if not p.is_contiguous():
+            raise RuntimeError("LBFGS: the parameter must be contiguous")
+        self._buffers(p.numel(), p.device)
+
+        def evaluate():
+            return self._eval(closure)
+
+        def move(g):
+            self.direction(g)
+            increment_version(p)
+            gtd, t, smax, flag = self._scal(3, 4, 5, 6)
+            return gtd, t, smax, bool(flag)
+        return self.run(evaluate, move)
+
+    def run(self, evaluate, move, first=None, on_eval=None):
+        """torch.optim.LBFGS.step's control flow (no line search).
+        evaluate() -> (returned loss, host loss, max|g|, g): a closure evaluation.
+        move(g) -> (g.d, t, max|t d|, stopped): the direction and x += t d (not applied
+        when stopped, i.e. g.d > -tolerance_change).
+        first: an evaluation already made at the current point (GatysLBFGS) or None.
+        on_eval(loss): called for every evaluation torch counts (host loss)."""
+        grp = self.param_groups[0]
+        max_iter, max_eval = grp["max_iter"], grp["max_eval"]
+        tol_grad, tol_change = grp["tolerance_grad"], grp["tolerance_change"]
+        st = self.state[self._p]
         st.setdefault("func_evals", 0)
         st.setdefault("n_iter", 0)
-        with torch.enable_grad():
-            orig_loss = closure()
-        hl = self._loss_slot(orig_loss)
+        orig_loss, loss, gmax, g = first if first is not None else evaluate()
+        if on_eval is not None:
+            on_eval(loss)
         current_evals = 1
         st["func_evals"] += 1
-        g = self._grad()
-        n = g.numel()
-        self._red(g, None, 2, self._sp(11))
-        loss, gmax = self._hosts(10, 11)                  # one sync: loss, max|g|
-        loss = loss if hl is None else hl
         if gmax <= tol_grad:
             return orig_loss
-        d = st.get("d")
-        prev_g = st.get("prev_flat_grad")
         prev_loss = st.get("prev_loss")
-        dirs, stps, slots = st.get("old_dirs"), st.get("old_stps"), st.get("slots")
-        t_host = st.get("t_host")
         n_iter = 0
         while n_iter < max_iter:
             n_iter += 1
             st["n_iter"] += 1
-            if st["n_iter"] == 1:
-                d = torch.empty(n, device=dev, dtype=torch.float32)
-                self._axpby(d, g, -1.0)
-                dirs, stps, slots = [], [], []
-                self._sc(3, 9, 8, 2)  # H_diag = 1
-            else:
-                y = torch.empty_like(g)
-                s = torch.empty_like(g)
-                self._axpby(y, g)
-                self._axpby(y, prev_g, -1.0, b=1.0)          # y = g - prev_g
-                self._axpby(s, d, 1.0, self._sp(3))           # s = d * t
-                self._red(y, s, 0, self._sp(0))               # ys
-                if self._host(0) > 1e-10:
-                    if len(dirs) == H:
-                        dirs.pop(0)
-                        stps.pop(0)
-                        k = slots.pop(0)
-                    else:
-                        k = len(slots)
-                    dirs.append(y)
-                    stps.append(s)
-                    slots.append(k)
-                    self._sc(4, 0, -1, 16 + k)                 # rho_k = 1 / ys
-                    self._red(y, y, 0, self._sp(1))           # yy
-                    self._sc(0, 0, 1, 2)                       # H_diag = ys / yy
-                # two-loop recursion, all scalars on the device
-                q = torch.empty_like(g)
-                self._axpby(q, g, -1.0)
-                for i in range(len(dirs) - 1, -1, -1):
-                    k = slots[i]
-                    self._red(stps[i], q, 0, self._sp(16 + H + k), mul=self._sp(16 + k))
-                    self._axpby(q, dirs[i], 1.0, self._sp(16 + H + k), sgn=-1.0, b=1.0)
-                d = torch.empty_like(g)
-                self._axpby(d, q, 1.0, self._sp(2))           # d = r = q * H_diag
-                for i in range(len(dirs)):
-                    k = slots[i]
-                    # coef = alpha_i - rho_i * (dirs_i . r)
-                    self._red(dirs[i], d, 0, self._sp(6), mul=self._sp(16 + k),
-                              add=self._sp(16 + H + k), sgn=-1.0)
-                    self._axpby(d, stps[i], 1.0, self._sp(6), b=1.0)
-            if prev_g is None:
-                prev_g = torch.empty_like(g)
-            self._axpby(prev_g, g)
             prev_loss = loss
-            if st["n_iter"] == 1:
-                self._red(g, None, 1, self._sp(5))             # sum |g|
-                self._sc(5, 5, 9, 3)                           # t = min(1, 1/sum|g|)
-                self._sc(1, 3, 7, 3)                           # t *= lr
-            else:
-                self._sc(3, 7, 8, 3)                           # t = lr
-            self._red(g, d, 0, self._sp(4))                    # gtd
-            t_host, gtd = self._hosts(3, 4)                    # one sync: t, g.d
-            if gtd > -tol_change:
+            gtd, t, smax, stopped = move(g)
+            if stopped:   # gtd > -tolerance_change: torch breaks before moving x
                 break
-            ls_evals = 0
-            self._axpby(p.data.view(-1), d, 1.0, self._sp(3), b=1.0)   # x += t d
-            increment_version(p)
             opt_cond = False
-            self._red(d, None, 2, self._sp(12))                # max|d| (for the last test)
-            dmax = None
+            ls_evals = 0
             if n_iter != max_iter:
-                with torch.enable_grad():
-                    hl = self._loss_slot(closure())
-                g = self._grad()
-                self._red(g, None, 2, self._sp(11))
-                loss, gmax, dmax = self._hosts(10, 11, 12)     # one sync: loss, max|g|, max|d|
-                loss = loss if hl is None else hl
+                _, loss, gmax, g = evaluate()
+                if on_eval is not None:
+                    on_eval(loss)
                 opt_cond = gmax <= tol_grad
                 ls_evals = 1
             current_evals += ls_evals
             st["func_evals"] += ls_evals
             if n_iter == max_iter or current_evals >= max_eval or opt_cond:
                 break
-            if dmax is None:
-                dmax = self._host(12)
-            if abs(t_host) * dmax <= tol_change:               # max|d * t|
+            if smax <= tol_change:             # max|d * t|
                 break
             if abs(loss - prev_loss) < tol_change:
                 break
-        st.update(d=d, prev_flat_grad=prev_g, prev_loss=prev_loss, old_dirs=dirs,
-                  old_stps=stps, slots=slots, t_host=t_host)
+        st["prev_loss"] = prev_loss
         return orig_loss

@@ -60,6 +60,7 @@ class FastStTrainer:
         self.sw, self.cw, self.tv = float(style_weight), float(content_weight), float(tv_factor)
         self.world = int(world_size)
         self.pg = process_group
+        self.exchanges = 0  # flat-gradient all-reduces issued
         self.flat, self.flat_grad = flatten_parameters(itn, self.device)
         self.params = list(itn.parameters())
         if self.world > 1:
@@ -122,8 +123,11 @@ class FastStTrainer:
         return total.detach()
 
     def _exchange(self):
-        if self.world > 1:
+        # an explicit process group forces the exchange even at world 1 (the RCCL path
+        # exercised on one GPU: a 1-rank SUM is the identity)
+        if self.world > 1 or self.pg is not None:
             dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
+            self.exchanges += 1
 
     def step(self, batch: torch.Tensor) -> torch.Tensor:
         batch = batch.to(self.device, torch.float32).contiguous()
@@ -155,6 +159,9 @@ class FastStTrainer:
         with torch.cuda.graph(g_up, pool=g_fb.pool(), capture_error_mode="thread_local"):
             self.opt.step()
         ptrs = self._param_ptrs()
+        # every older graph refuses to replay (pointer check below): the slabs of
+        # earlier generations are dead
+        self.slabs.release_retired()
 
         def replay():
             if self._param_ptrs() != ptrs:

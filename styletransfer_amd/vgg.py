@@ -484,3 +484,119 @@ class GatysEngine:
     def losses(self):
         """[style x5, content, feature] of the last forward (device tensor)."""
         return loss_values(self.st)
+
+
+class GatysLBFGS:
+    """StyleNetwork.train_gatys (stransfer/network.py:411-458) as hipGraph replays:
+    torch.optim.LBFGS (lr 1, max_iter 20, max_eval 25, tolerance_grad 1e-7,
+    tolerance_change 1e-9, history 100) over the image with the closure
+
+        zero_grad; net(x, content); (style_weight*style + content_weight*content).backward()
+
+    Two graphs: `eval` (closure + gradient statistics) for the evaluation that opens an
+    outer step, and `iter` (stx_lbfgs_direction -- pair update, compact two-loop
+    direction, x += t d -- then the closure and the statistics) for every loop
+    iteration; optim.LBFGS.run drives them with torch's control flow and one host read
+    per iteration.  Every closure evaluation the graphs make is one torch makes too:
+    torch's last iteration of an outer step (n_iter == max_iter) moves x without
+    evaluating, and the next step opens with a closure at that point -- the `iter`
+    graph's evaluation, reused.  The one exception is an iteration that stops on
+    g.d > -tolerance_change: x does not move and its (identical) re-evaluation is
+    discarded."""
+
+    def __init__(self, feat: VGGFeatures, style_image, content_image, style_weight=100_000,
+                 content_weight=1, targets=None, init=None, **lbfgs_kw):
+        from .optim import LBFGS
+        dev = feat.device
+        self.feat = feat
+        if targets is None:
+            targets = feat.style_targets(style_image.to(dev, torch.float32))
+        self.targets = [t.reshape(t.shape[-2:]).contiguous() for t in targets]
+        self.content = content_image.to(dev, torch.float32).contiguous()
+        self.c4 = content_target(feat, self.content).clone()
+        src = self.content if init is None else init.to(dev, torch.float32)
+        self.x = src.clone().contiguous()
+        self.grad = torch.zeros_like(self.x)
+        self.sw, self.cw = float(style_weight), float(content_weight)
+        self.total = torch.zeros((), device=dev, dtype=torch.float32)
+        self.st = LossState()
+        self.scratch = {}
+        self.opt = LBFGS([self.x], **lbfgs_kw)
+        self.opt._buffers(self.x.numel(), dev)
+        self.g_eval = self.g_iter = None
+        self._at_x = None  # the latest evaluation, made at the current x
+        self.closure_runs = 0  # closure evaluations actually executed (graph replays)
+
+    def _closure(self):
+        loss_forward(self.feat, self.targets, self.x, self.c4, self.st,
+                     folded_weights=(self.sw, self.cw), total=self.total)
+        loss_backward(self.feat, self.st, dx=self.grad, feature_grad=False,
+                      scratch=self.scratch)
+        # the statistics launch also zeroes the amax groups for the next forward
+        self.opt.grad_stats(self.grad.view(-1), self.total.view(1), clear=self.st.amax)
+        self.st.amax_cleared = True
+
+    def capture(self):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._closure()  # allocates every buffer (x unchanged: no optimiser state)
+        torch.cuda.current_stream().wait_stream(s)
+        self.g_eval = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_eval):
+            self._closure()
+        self.g_iter = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_iter, pool=self.g_eval.pool()):
+            self.opt.direction(self.grad.view(-1))
+            self._closure()
+        return self
+
+    def _read(self):
+        loss, gmax, gtd, t, smax, flag = self.opt._scal(0, 1, 3, 4, 5, 6)
+        return loss, gmax, gtd, t, smax, flag
+
+    def step(self, on_eval=None):
+        """One outer optimizer.step(closure); returns its opening loss (host float).
+        on_eval(loss): called with the loss of every evaluation torch counts."""
+        if self.g_iter is None:
+            self.capture()
+
+        def evaluate():
+            self.g_eval.replay()
+            self.closure_runs += 1
+            loss, gmax = self.opt._scal(0, 1)
+            self._at_x = (loss, loss, gmax, self.grad.view(-1))
+            return self._at_x
+
+        pending = []
+
+        def move(g):
+            self.g_iter.replay()
+            self.closure_runs += 1
+            loss, gmax, gtd, t, smax, flag = self._read()
+            self._at_x = (loss, loss, gmax, self.grad.view(-1))
+            pending.append(self._at_x)
+            return gtd, t, smax, bool(flag)
+
+        def evaluate_after_move():
+            return pending.pop() if pending else evaluate()
+
+        first, self._at_x = self._at_x, None
+        ret = self.opt.run(evaluate_after_move, move, first=first, on_eval=on_eval)
+        if self._at_x is None:  # (no evaluation or move ran: gradient already tiny)
+            self._at_x = first
+        return ret
+
+    @property
+    def func_evals(self):
+        return self.opt.state[self.x].get("func_evals", 0)
+
+    def history(self):
+        """(committed pairs, torch n_iter) from the device state."""
+        pairs, n_iter = self.opt._scal(8, 9)
+        return int(pairs), int(n_iter)
+
+    def run(self, steps):
+        for _ in range(steps):
+            self.step()
+        return self.x

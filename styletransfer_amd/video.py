@@ -66,6 +66,8 @@ def iterate_raw_frames(source, max_frames=90 * 24) -> Iterator[np.ndarray]:
         f = np.ascontiguousarray(f, dtype=np.uint8)
         if f.ndim == 3 and f.shape[2] == 4:
             f = np.ascontiguousarray(f[:, :, :3])  # RGBA frame: .convert("RGB") drops alpha
+        elif f.ndim == 2:
+            f = np.repeat(f[:, :, None], 3, axis=2)  # grayscale: PIL "L" -> "RGB" copies
         yield f
 
 

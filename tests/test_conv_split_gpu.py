@@ -165,6 +165,24 @@ def test_split_conv_fused_epilogue(dev):
     assert rel(o1, o2) < 2e-6
 
 
+@pytest.mark.parametrize("mode", [N.STX_IN_RELU, N.STX_IN_RELU_POOL2, N.STX_IN_UPSAMPLE2])
+def test_split_conv_phase2_needs_raw_input(dev, mode):
+    """The fused Gram-backward phase exists only for raw-input data gradients: any
+    other loader mode on the split path is rejected, not silently dropped."""
+    n, c, h, w = 1, 64, 16, 36
+    hv, wv = {N.STX_IN_RELU: (h, w), N.STX_IN_RELU_POOL2: (h // 2, w // 2),
+              N.STX_IN_UPSAMPLE2: (2 * h, 2 * w)}[mode]
+    z = rnd(n, c, hv, wv, dev=dev, seed=91, scale=2, shift=-1)
+    dy = rnd(n, c, h, w, dev=dev, seed=92, scale=2, shift=-1)
+    wgt = rnd(c, c, 3, 3, dev=dev, seed=93, scale=0.2, shift=-0.1)
+    _, coef = ops.style_loss(z, rnd(c, c, dev=dev, seed=94))
+    wtT = ops.conv_weight_prep(wgt, transpose=True)
+    w16 = ops.conv_weight_prep16(wgt, transpose=True)
+    with pytest.raises(N.NativeError, match="raw-input"):
+        ops.conv2d(dy, wtT, c, c, 3, in_mode=mode, p2_z=z, p2_coef=coef, wt16=w16)
+        torch.cuda.synchronize()
+
+
 def test_amax(dev):
     x = rnd(3, 5, 7, 11, dev=dev, seed=7, scale=4, shift=-2)
     x.view(-1)[123] = -9.5

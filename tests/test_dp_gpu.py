@@ -96,3 +96,23 @@ def test_no_grad_forward_sees_trained_weights(runs):
     (Conv2d caches its slabs per weight version; the HIP Adam bumps the versions)."""
     for r in runs:
         assert torch.equal(r["y_after"], r["y_fresh"])
+
+
+def test_rccl_world1_exchange(tmp_path):
+    """the north star's one collective through RCCL itself.  A rank with
+    the torchrun environment at world 1 initialises the "nccl" (= RCCL) process group
+    as bench.py does and trains 3 steps with FastStTrainer(process_group=pg): the
+    exchange runs (counted), eagerly between the two graph replays; the parameters are
+    bit-identical to a group-less trainer's (a 1-rank SUM is the identity) and librccl
+    is mapped into the process."""
+    w = os.path.join(HERE, "rccl_worker.py")
+    p = subprocess.run([sys.executable, w, str(tmp_path), _port()], timeout=150,
+                       capture_output=True, text=True)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    r = torch.load(os.path.join(tmp_path, "rccl.pt"), weights_only=True)
+    assert r["backend"] == "nccl"
+    assert r["rccl_mapped"]
+    # eager step + the capture's warm-up step + one replay; none without a group
+    assert r["rccl_exchanges"] == 3 and r["plain_exchanges"] == 0
+    assert torch.equal(r["rccl_flat"], r["plain_flat"])
+    assert torch.equal(r["rccl_grad"], r["plain_grad"])

@@ -64,6 +64,34 @@ def test_pool_sum_contract_rejected():
     assert rc == 1001 and b"pool_sum" in cp.stx_last_error_string()
 
 
+def test_phase2_contract_rejected():
+    """The fused Gram-backward phase (p2_z) on the split path needs a raw-input data
+    gradient; any other loader mode is refused before a launch, not dropped."""
+    from styletransfer_amd import _native as N
+    import ctypes as C
+    L = N.lib()
+    for mode, (hv, wv) in ((N.STX_IN_RELU, (64, 64)), (N.STX_IN_RELU_POOL2, (32, 32)),
+                           (N.STX_IN_UPSAMPLE2, (128, 128))):
+        p = N.ConvParams(x=16, y=32, n=1, cin=64, h=64, w=64, cout=64, ks=3, stride=1, pad=1,
+                         in_mode=mode, hv=hv, wv=wv, ho=hv, wo=wv, cin_pad=64, cout_pad=64,
+                         wt16=48, w_amax=64, in_amax=80, p2_z=96, p2_wt=112, p2_c=64,
+                         p2_amax=128)
+        rc = L.stx_conv2d(C.byref(p), None)
+        assert rc == 1001 and b"raw-input" in L.stx_last_error_string(), mode
+
+
+def test_grayscale_frames_expand_to_rgb():
+    """iterate_raw_frames: 2-D (grayscale) frames become HxWx3 like PIL's L -> RGB."""
+    from PIL import Image
+    from styletransfer_amd import video
+    arr = (np.arange(2 * 5 * 7) % 251).astype(np.uint8).reshape(2, 5, 7)
+    out = list(video.iterate_raw_frames(arr))
+    assert len(out) == 2
+    for f, g in zip(out, arr):
+        assert f.shape == (5, 7, 3)
+        assert np.array_equal(f, np.asarray(Image.fromarray(g).convert("RGB")))
+
+
 def test_image_loader_matches_reference():
     from styletransfer_amd import img_utils
     d = np.load(os.path.join(GOLDEN, "images.npz"))

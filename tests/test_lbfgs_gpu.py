@@ -4,6 +4,7 @@ StyleNetwork.train_gatys runs `optim.LBFGS` with its defaults
 (stransfer/network.py:435); our LBFGS restates torch's algorithm on libstx vector
 kernels.  Same closure, same inputs: trajectories must agree to reduction-order
 rounding (dot products are summed in a different order)."""
+import numpy as np
 import pytest
 import torch
 
@@ -22,9 +23,12 @@ def quad_problem(dev, n=4096, seed=0):
     return m, b, x0
 
 
-@pytest.mark.parametrize("history", [100, 3])
-def test_lbfgs_matches_torch_on_quadratic(dev, history):
-    m, b, x0 = quad_problem(dev)
+@pytest.mark.parametrize("history,n", [(100, 4096), (3, 4096), (1, 4096), (100, 4093),
+                                       (5, 2500)])
+def test_lbfgs_matches_torch_on_quadratic(dev, history, n):
+    """history 1 / 3 / 5 evict from the ring within the 4 steps; n = 4093 / 2500 are not
+    multiples of the 1024-element history chunk (padded slots, ragged tail)."""
+    m, b, x0 = quad_problem(dev, n)
     xs = []
     for cls in (torch.optim.LBFGS, stx_optim.LBFGS):
         x = x0.clone().view(1, -1).requires_grad_()
@@ -79,3 +83,47 @@ def test_lbfgs_gatys(dev):
     # by test_lbfgs_matches_torch_on_quadratic, and train_gatys against the reference's
     # own L-BFGS run in fp64 three-way form by test_train_gatys_lbfgs_reference.
     assert abs(finals[0] - finals[1]) <= 1e-2 * abs(finals[0]), finals
+
+
+def test_gatys_lbfgs_engine_matches_torch_control_flow(dev):
+    """vgg.GatysLBFGS (graph replays, one host read per iteration, the opening
+    evaluation of a step reused from the previous iteration's graph) against
+    torch.optim.LBFGS driving the SAME closure (the engine's eager loss evaluation):
+    identical evaluation counts per outer step and the same losses up to the
+    direction's rounding (compact form vs torch's two-loop recursion)."""
+    from styletransfer_amd import vgg as V
+    H = 64
+    s = torch.from_numpy(W.synthetic_image(31, (1, 3, H, H))).to(dev)
+    c = torch.from_numpy(W.synthetic_image(32, (1, 3, H, H))).to(dev)
+    feat = V.VGGFeatures(V.load_vgg19_weights(), dev)
+    # torch's optimiser over the engine's eager closure
+    ref = V.GatysLBFGS(feat, s, c)
+    x = ref.x
+    opt = torch.optim.LBFGS([x])
+    ref_losses, ref_evals = [], []
+
+    def closure():
+        ref._closure()
+        x.grad = ref.grad
+        ref_losses.append(float(ref.total))
+        return ref.total.clone()
+
+    for _ in range(4):
+        opt.step(closure)
+        ref_evals.append(opt.state[x]["func_evals"])
+    eng = V.GatysLBFGS(feat, s, c)
+    losses, evals = [], []
+    for _ in range(4):
+        eng.step(on_eval=losses.append)
+        evals.append(eng.func_evals)
+    assert evals == ref_evals, (evals, ref_evals)
+    assert len(losses) == len(ref_losses)
+    got, want = np.array(losses), np.array(ref_losses)
+    err = np.abs(got - want) / np.abs(want)
+    assert err[:6].max() < 1e-4, err[:6]
+    assert err.max() < 5e-2, err.max()
+    # every graph evaluation is one torch makes (the last step's closing evaluation is the
+    # next step's opening one), but for stops on g.d (none expected here)
+    assert eng.closure_runs <= eng.func_evals + 1, (eng.closure_runs, eng.func_evals)
+    pairs, n_iter = eng.history()
+    assert n_iter == opt.state[x]["n_iter"] and 0 < pairs <= 100

@@ -288,14 +288,20 @@ def test_itn_forward_backward_golden(itn_case, dev, monkeypatch):
             # |g| ~ 1e-14; fp32 rounding noise ~1e-5 in the reference)
             assert np.linalg.norm(gp) < 1e-6 * norms.max(), i
             continue
-        if i in flipped:
-            continue
         e64 = rel(proj32(gp), f64["grad64_proj"][i, 1:])
         r32 = float(f64["ref32_err"][i])
+        if i in flipped:
+            # upstream of a flip: a loose bound only (the forced-branch tests hold these
+            # parameters to fp32-class error)
+            assert e64 <= max(2.5 * r32, 3e-2), (i, e64, r32)
+            continue
         errs.append((e64, r32, i))
         assert e64 <= max(2.5 * r32, 1e-5), (i, e64, r32)
     print("ITN grad error vs fp64 downstream of every flip (hip, fp32-ref, param):",
           sorted(errs)[-3:], "flip-affected params:", len(flipped))
+    # the tight check must have covered something: every parameter a flip cannot reach
+    # (the ITN's last layers at least: conv22's weight sits downstream of every branch)
+    assert len(errs) >= 1 and (len(params) - 2) in [i for _, _, i in errs] + list(flipped)
     with torch.no_grad():
         assert rel(net(batch[:1]), d["y_single"]) < 1e-4
 
