@@ -111,6 +111,9 @@ def parse():
                     help="timed outer L-BFGS steps of the train_gatys leg (0 = skip)")
     ap.add_argument("--lbfgs-fill", type=int, default=20,
                     help="untimed outer L-BFGS steps at most, to fill the 100-pair history")
+    ap.add_argument("--loader-images", type=int, default=256,
+                    help="synthetic 640x480 JPEGs of the COCO loader leg (0 = skip)")
+    ap.add_argument("--loader-epochs", type=int, default=3)
     ap.add_argument("--skip-fast", action="store_true")
     ap.add_argument("--fast-only", action="store_true", help="profiling: fast_st leg only")
     ap.add_argument("--skip-cpu", action="store_true")
@@ -268,6 +271,39 @@ def gatys_lbfgs_leg(args, world, rank, dev):
                 dt=dt, steps=args.lbfgs_steps, evals=evals, closure_runs=runs,
                 fill_steps=fill, pairs_at_start=pairs0, pairs_at_end=pairs1, n_iter=n_iter,
                 loss=float(eng.total))
+
+
+def coco_loader_leg(args, dev, fast_rate=None):
+    """the fast_st input pipeline (dataset.get_coco_loader with GPU
+    conditioning: worker processes decode + pack JPEG batches, the pinned batch is
+    uploaded and centre-cropped / Pillow-exact-resized / normalised on a side stream,
+    the consumer's stream waits on an event) over synthetic 640x480 JPEGs at the
+    per-GPU batch of 8; images/s of conditioned [8, 3, 256, 256] batches in HBM."""
+    import shutil
+    import tempfile
+    from styletransfer_amd import dataset
+    tmp = tempfile.mkdtemp(prefix="stx_coco_")
+    try:
+        n = args.loader_images
+        dataset.write_synthetic_jpegs(tmp, n, seed=7)
+        _, train = dataset.get_coco_loader(batch_size=args.fast_batch, test_split=0.0, path=tmp,
+                                           gpu_conditioning=True)
+        workers = train.loader.num_workers
+        for _ in train:  # warm-up epoch: workers started, pinned/host caches filled
+            pass
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        count = 0
+        for _ in range(args.loader_epochs):
+            for b in train:
+                count += b.shape[0]
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        return dict(rate=count / dt, images=count, s=dt, workers=workers, files=n,
+                    jpeg_kb=round(sum(os.path.getsize(os.path.join(tmp, f))
+                                      for f in os.listdir(tmp)) / n / 1024, 1))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def fast_st_leg(args, world, rank, dev, B=None, steps=None):
@@ -512,6 +548,9 @@ def main():
     if not args.skip_infer:
         vid = video_leg(args, world, rank, dev)
         conv = convert_leg(args, world, rank, dev)
+    ld = None
+    if world == 1 and args.loader_images > 0 and not args.skip_infer:
+        ld = coco_loader_leg(args, dev)
     cpu = None
     if rank == 0 and world == 1 and not args.skip_cpu:
         cpu = cpu_baseline(args)
@@ -635,6 +674,15 @@ def main():
                 "tflops": round(FAST_ST_GFLOP_PER_IMAGE * fs64["rate"] / 1e3, 3),
                 "graph": fs64["graph"], "note": "config-4 global batch 64 on one GPU (the "
                 "1-GPU point of the strong-scaling view; the weak-scaling legs keep 8/GPU)"}
+        if ld:
+            res["coco_loader"] = {
+                "value": round(ld["rate"], 1), "unit": "images/s", "batch": args.fast_batch,
+                "workers": ld["workers"], "images": ld["images"], "seconds": round(ld["s"], 3),
+                "jpeg": f"{ld['files']} synthetic 640x480 JPEGs, {ld['jpeg_kb']} KB avg",
+                "vs_fast_st_step_rate": round(ld["rate"] / fs["rate"], 3) if fs else None,
+                "note": "dataset.get_coco_loader(gpu_conditioning=True): decode workers -> "
+                        "pinned packed batch -> side-stream upload + GPU crop/resize/normalise "
+                        "(bit-identical to the PIL path); per rank, fed by this rank's CPU share"}
         if vid:
             res["video_st"] = {
                 "value": round(vid["rate"], 2), "unit": "frames/s",

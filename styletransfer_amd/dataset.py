@@ -61,25 +61,103 @@ def _list_collate(batch):
     return list(batch)
 
 
-class GpuConditionedLoader:
-    """Wraps a DataLoader of decoded uint8 images (CocoDataset(decode_only=True),
-    list collate) and yields each batch conditioned on the GPU as [B, 1, 3, S, S]
-    -- the shape static_train squeezes (stransfer/network.py:688)."""
+def _pack_collate(batch):
+    """Decoded HxWx3 uint8 images -> (one packed uint8 tensor, int32 [B, 2] shapes):
+    runs in the loader's worker, so a batch crosses to the main process as one
+    shared-memory tensor (and is pinned there by the DataLoader's pin thread)."""
+    arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in batch]
+    packed = torch.empty(sum(a.nbytes for a in arrs), dtype=torch.uint8)
+    pk = packed.numpy()
+    o = 0
+    for a in arrs:
+        pk[o:o + a.nbytes] = a.reshape(-1)
+        o += a.nbytes
+    shapes = torch.tensor([a.shape[:2] for a in arrs], dtype=torch.int32).reshape(-1, 2)
+    return packed, shapes
 
-    def __init__(self, loader, size=None, device=None):
+
+def default_workers():
+    """Decode workers for the GPU-conditioned loader: the CPUs this process may use
+    (affinity, cgroup quota) minus one for the training loop, at most 16."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(0, min(16, n - 1))
+
+
+class GpuConditionedLoader:
+    """Wraps a DataLoader of packed decoded uint8 batches (CocoDataset(decode_only=True),
+    _pack_collate; its workers decode the JPEGs) and yields each batch conditioned on
+    the GPU as [B, 1, 3, S, S] -- the shape static_train squeezes
+    (stransfer/network.py:688).  Pipelined: batch k+depth's upload (pinned -> device)
+    and conditioning kernels run on a side stream while the consumer works on batch k;
+    the consumer's stream waits on the batch's event, never the host."""
+
+    def __init__(self, loader, size=None, device=None, depth=2):
         self.loader = loader
         self.batch_sampler = getattr(loader, "batch_sampler", None)
         self.cond = img_utils.ImageConditioner(size, device)
+        self.depth = max(1, int(depth))
 
     def __len__(self):
         return len(self.loader)
 
+    def _submit(self, item, side):
+        packed, shapes = item
+        cond, dev = self.cond, self.cond.device
+        metas, coef, max_rows, tmp_bytes, src_bytes = cond._plan(
+            [tuple(hw) for hw in shapes.tolist()])
+        B, S = shapes.shape[0], cond.size
+        if packed.numel() != src_bytes:
+            raise ValueError("packed batch size does not match its shapes")
+        mb = bytes(metas)
+        head = torch.empty(len(mb) + coef.nbytes, dtype=torch.uint8).pin_memory()
+        hv = head.numpy()
+        hv[:len(mb)] = np.frombuffer(mb, np.uint8)
+        hv[len(mb):] = coef.view(np.uint8).reshape(-1)
+        with torch.cuda.stream(side):
+            src = packed.to(dev, non_blocking=True)
+            hd = head.to(dev, non_blocking=True)
+            tmp = torch.empty(max(tmp_bytes, 16), dtype=torch.uint8, device=dev)
+            out = torch.empty((B, 3, S, S), dtype=torch.float32, device=dev)
+            cond._launch(src, hd[:len(mb)], B, max_rows, hd[len(mb):].view(torch.int32), out,
+                         tmp)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        return out, ev
+
     def __iter__(self):
-        for imgs in self.loader:
-            yield self.cond(imgs).unsqueeze(1)
+        from collections import deque
+        dev = self.cond.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        it = iter(self.loader)
+        pending = deque()
+        for item in it:
+            pending.append(self._submit(item, side))
+            if len(pending) >= self.depth:
+                break
+        while pending:
+            out, ev = pending.popleft()
+            main = torch.cuda.current_stream(dev)
+            main.wait_event(ev)
+            out.record_stream(main)
+            nxt = next(it, None)
+            if nxt is not None:
+                pending.append(self._submit(nxt, side))
+            yield out.unsqueeze(1)
 
 
-def _train_loader(ds, batch_size, shard, shuffle=True, seed=0, num_workers=0, collate=None):
+def _train_loader(ds, batch_size, shard, shuffle=True, seed=0, num_workers=0, collate=None,
+                  pin_memory=False, prefetch_factor=None):
     """DataLoader over `ds` whose batches are this rank's shard of each global batch
     of `batch_size` (distributed.ShardedBatchSampler); at world 1 a plain batch."""
     from .distributed import Shard, ShardedBatchSampler
@@ -87,16 +165,23 @@ def _train_loader(ds, batch_size, shard, shuffle=True, seed=0, num_workers=0, co
     sampler = ShardedBatchSampler(len(ds), batch_size, shard.rank, shard.world,
                                   shuffle=shuffle, seed=seed)
     kw = {"collate_fn": collate} if collate is not None else {}
-    return DataLoader(ds, batch_sampler=sampler, num_workers=num_workers, **kw)
+    if num_workers > 0:
+        kw["persistent_workers"] = True
+        if prefetch_factor:
+            kw["prefetch_factor"] = prefetch_factor
+    return DataLoader(ds, batch_sampler=sampler, num_workers=num_workers, pin_memory=pin_memory,
+                      **kw)
 
 
 def get_coco_loader(batch_size=4, test_split=0.10, test_limit=None, path=None, shard=None,
-                    gpu_conditioning=None, num_workers=0):
+                    gpu_conditioning=None, num_workers=None):
     """(test_loader, train_loader) over local COCO images (stransfer/dataset.py:314-360).
     `batch_size` is the global batch; with a data-parallel `shard` each rank's train
     loader yields its batch_size/world slice of every global batch.  With
-    gpu_conditioning (default: when a GPU is present) the workers only decode and
-    the crop/resize/normalisation of each batch runs on the GPU (identical output)."""
+    gpu_conditioning (default: when a GPU is present) the workers only decode (and pack
+    the batch), the upload and the crop/resize/normalisation run on the GPU on a side
+    stream, pipelined with the consumer (identical output); num_workers defaults to
+    default_workers() there and to 0 (the reference's DataLoader) on the PIL path."""
     path = path or os.path.join(constants.PROJECT_ROOT_PATH, IMAGE_FOLDER_PATH)
     if not os.path.isdir(path) or not os.listdir(path):
         raise FileNotFoundError(
@@ -110,18 +195,41 @@ def get_coco_loader(batch_size=4, test_split=0.10, test_limit=None, path=None, s
     if gpu_conditioning is None:
         gpu_conditioning = constants.DEVICE.type == "cuda"
     if gpu_conditioning:
+        nw = default_workers() if num_workers is None else num_workers
+        pin = torch.cuda.is_available()
         test = GpuConditionedLoader(DataLoader(CocoDataset(test_imgs, path=path, decode_only=True),
                                                batch_size=batch_size, shuffle=False,
-                                               collate_fn=_list_collate, num_workers=num_workers))
+                                               collate_fn=_pack_collate, num_workers=min(nw, 2),
+                                               pin_memory=pin))
         train = GpuConditionedLoader(_train_loader(
             CocoDataset(train_imgs, path=path, decode_only=True), batch_size, shard,
-            num_workers=num_workers, collate=_list_collate))
+            num_workers=nw, collate=_pack_collate, pin_memory=pin,
+            prefetch_factor=4 if nw > 0 else None))
         return test, train
+    num_workers = num_workers or 0
     test = DataLoader(CocoDataset(test_imgs, path=path), batch_size=batch_size, shuffle=False,
                       num_workers=num_workers)
     train = _train_loader(CocoDataset(train_imgs, path=path), batch_size, shard,
                           num_workers=num_workers)
     return test, train
+
+
+def write_synthetic_jpegs(path, n, h=480, w=640, seed=0, quality=90):
+    """n seeded JPEGs of COCO's typical size (640x480) under `path`: smooth colour
+    fields plus sensor-like noise, so the files compress like photographs (~120 KB
+    at quality 90) and decode at a photograph's cost.  For loader throughput runs."""
+    os.makedirs(path, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float32)
+    noise = rng.normal(0, 12, (h + 64, w + 64, 3)).astype(np.float32)
+    for k in range(n):
+        oy, ox = rng.integers(0, 64, 2)
+        f = rng.uniform(12, 40, 4)
+        base = np.stack([np.sin(x / f[0]) * 60 + np.cos(y / f[1]) * 60 + 128,
+                         np.sin((x + y) / f[2]) * 90 + 128,
+                         (x * y / (f[3] * 10)) % 255], 2)
+        img = np.clip(base + noise[oy:oy + h, ox:ox + w], 0, 255).astype(np.uint8)
+        Image.fromarray(img).save(os.path.join(path, f"{k:06d}.jpg"), quality=quality)
 
 
 class SyntheticImageDataset(Dataset):
