@@ -72,6 +72,14 @@ __device__ __forceinline__ float read_amax(const float* __restrict__ g) {
   return __uint_as_float(m);
 }
 
+// e with |a| < 2^e (frexp), clamped so 2^(15-e) and 2^(ex+ew-30) stay normal floats
+// (the power-of-two scales of the fp16 hi/lo split operands)
+__device__ __forceinline__ int amax_exp(float a) {
+  int e = 0;
+  frexpf(a, &e);
+  return min(max(e, -60), 60);
+}
+
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ inline int rup(int a, int b) { return cdiv(a, b) * b; }
 

@@ -38,12 +38,6 @@ namespace stx {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-// e with |a| < 2^e (frexp), clamped so 2^(15-e) and 2^(ex+ew-30) stay normal floats
-__device__ __forceinline__ int amax_exp(float a) {
-  int e = 0;
-  frexpf(a, &e);
-  return min(max(e, -60), 60);
-}
 
 // Split Gram-backward phase: acc (the de-scaled, masked main result) gets
 //   + s2 * sum_c A[n][c][co] * z2[n][c][pixel]
@@ -1009,7 +1003,13 @@ __global__ void __launch_bounds__(256) weight_prep_batch_kernel(WprepJobs b) {
                        b.gin[j], b.gout[j], i0, step);
 }
 
+int conv16_pc(const stx_conv_params& p, hipStream_t st);  // conv16pc.hip (-1: not covered)
+
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st) {
+  if (p.stride == 1) {
+    const int rc = conv16_pc(p, st);  // producer / consumer waves, persistent blocks
+    if (rc >= 0) return rc;
+  }
   switch (p.stride == 2 ? LM_S2 : p.in_mode) {
     case STX_IN_RAW: return dispatch16_tw<STX_IN_RAW>(p, st);
     case STX_IN_RELU: return dispatch16_tw<STX_IN_RELU>(p, st);

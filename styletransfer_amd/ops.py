@@ -419,10 +419,13 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
     return out
 
 
-def conv_gram_tiles(cin, cout, ho, wo):
-    """Gram partials per image of a split 3x3 stride-1 conv with a fused Gram
-    (stx_conv_gram_tiles; 0: not fusable)."""
-    p = ConvParams(cin=cin, cout=cout, ks=3, stride=1, pad=1, ho=ho, wo=wo, wt16=2)
+def conv_gram_tiles(cin, cout, ho, wo, n=1, in_mode=N.STX_IN_RAW):
+    """Gram partials per image of a split 3x3 stride-1 conv with a fused Gram over a
+    batch of n (stx_conv_gram_tiles; 0: not fusable).  The count depends on the launch
+    (one per 64 x 4 tile, or one per persistent block of the producer/consumer kernel),
+    so n and the loader mode must be the ones of the conv call."""
+    p = ConvParams(cin=cin, cout=cout, ks=3, stride=1, pad=1, ho=ho, wo=wo, wt16=2, n=n,
+                   in_mode=in_mode)
     return lib().stx_conv_gram_tiles(C.byref(p))
 
 

@@ -111,13 +111,13 @@ class VGGFeatures:
         return (l + 1 < len(IN_MODES) and IN_MODES[l + 1] == N.STX_IN_RELU_POOL2
                 and self.wt16[l] is not None and self.wt16[l + 1] is not None and wo > 32)
 
-    def gram_tiles(self, l, ho, wo):
-        """Fused Gram partials per image conv l can emit (0: not fusable)."""
+    def gram_tiles(self, l, ho, wo, n=1):
+        """Fused Gram partials per image conv l emits in a batch of n (0: not fusable)."""
         cout, cin = VGG_CONV_SHAPES[l]
         # conv1_1 (3 input channels) runs on convfew.hip's split kernel without a slab
         if (cin >= 16 and self.wt16[l] is None) or os.environ.get("STX_GRAM_FUSE", "1") == "0":
             return 0
-        return ops.conv_gram_tiles(cin, cout, ho, wo)
+        return ops.conv_gram_tiles(cin, cout, ho, wo, n=n, in_mode=IN_MODES[l])
 
     def forward(self, x, upto=5, outs=None, amax=None, pools=None, on_layer=None, grams=None):
         """[Z1..Z_upto] (pre-ReLU conv outputs).  amax: device [>=5] slots, zeroed by
@@ -237,7 +237,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     # conv layers whose Gram partials come out of the conv epilogue (no re-read of Z)
     hs = [H, H, H // 2, H // 2, H // 4]
     for l in range(5):
-        nt = feat.gram_tiles(l, hs[l], hs[l] * W // H) if split else 0
+        nt = feat.gram_tiles(l, hs[l], hs[l] * W // H, n=B) if split else 0
         if nt == 0:
             st.grams[l] = None
         elif st.grams[l] is None or st.grams[l].numel() != B * nt * 4096:

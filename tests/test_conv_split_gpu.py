@@ -50,6 +50,12 @@ CASES = [
     (2, 128, 128, 18, 70, N.STX_IN_RAW),
     (2, 64, 256, 32, 64, N.STX_IN_RAW),
     (2, 128, 128, 64, 64, N.STX_IN_RAW),     # ITN residual conv shape
+    # producer/consumer kernel (conv16pc.hip: >= 2 tiles per CU), every loader mode
+    (2, 64, 64, 256, 256, N.STX_IN_RELU),
+    (4, 64, 128, 128, 128, N.STX_IN_RAW),
+    (4, 64, 128, 256, 256, N.STX_IN_RELU_POOL2),
+    (8, 128, 64, 64, 64, N.STX_IN_UPSAMPLE2),
+    (3, 48, 70, 150, 170, N.STX_IN_RELU),    # ragged tiles, 3 chunks, cout % 64 != 0
 ]
 
 
@@ -125,9 +131,11 @@ def test_split_conv_dgrad(dev, case):
     assert rel(dx, ref) < TOL64
 
 
-def test_split_conv_dilate(dev):
-    """stride-2 data gradient as a stride-1 conv over the zero-dilated input."""
-    n, cin, cout, h, w = 2, 32, 64, 33, 30
+@pytest.mark.parametrize("case", [(2, 32, 64, 33, 30), (8, 32, 64, 128, 128)])
+def test_split_conv_dilate(dev, case):
+    """stride-2 data gradient as a stride-1 conv over the zero-dilated input (the
+    second case on the producer/consumer kernel)."""
+    n, cin, cout, h, w = case
     x = rnd(n, cin, h, w, dev=dev, seed=14).double().cpu().requires_grad_()
     wgt = rnd(cout, cin, 3, 3, dev=dev, seed=15, scale=0.2, shift=-0.1)
     y = F.conv2d(x, wgt.double().cpu(), stride=2, padding=1)
@@ -165,6 +173,32 @@ def test_split_conv_fused_epilogue(dev):
     assert rel(o1, o2) < 2e-6
 
 
+@pytest.mark.parametrize("shape", [(1, 64, 512, 512), (1, 128, 256, 256), (2, 64, 160, 300),
+                                   (4, 64, 128, 128)])
+@pytest.mark.parametrize("scaled", [False, True])
+def test_split_conv_fused_epilogue_pc(dev, shape, scaled):
+    """The Gram-backward data gradient at the VGG shapes (conv1_2^T at 512^2, conv2_2^T at
+    256^2 with two 64-cout blocks, ragged tiles, a batch of 4) on the producer/consumer
+    kernel: dZ = [Z > 0] conv^T(dY) + s2 A.Z against the fp32-MFMA kernel's fused
+    epilogue, and out_amax is the exact max|dZ|."""
+    n, c, h, w = shape
+    z = rnd(n, c, h, w, dev=dev, seed=191, scale=2, shift=-1)
+    dy = rnd(n, c, h, w, dev=dev, seed=192, scale=2e-3, shift=-1e-3)
+    wgt = rnd(c, c, 3, 3, dev=dev, seed=193, scale=0.2, shift=-0.1)
+    t = rnd(c, c, dev=dev, seed=194)
+    _, coef = ops.style_loss(z, t, weight=2.0)
+    s2 = torch.tensor(0.375, device=dev) if scaled else None
+    wtT = ops.conv_weight_prep(wgt, transpose=True)
+    w16 = ops.conv_weight_prep16(wgt, transpose=True)
+    am = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    out = ops.conv2d(dy, wtT, c, c, 3, mask=z, p2_z=z, p2_coef=coef, p2_scale=s2, wt16=w16,
+                     out_amax=am)
+    out32 = ops.conv2d(dy, wtT, c, c, 3, mask=z, p2_z=z, p2_coef=coef, p2_scale=s2)
+    torch.cuda.synchronize()
+    assert rel(out, out32) < 2e-6, rel(out, out32)
+    assert float(am.max()) == float(out.abs().max())
+
+
 @pytest.mark.parametrize("mode", [N.STX_IN_RELU, N.STX_IN_RELU_POOL2, N.STX_IN_UPSAMPLE2])
 def test_split_conv_phase2_needs_raw_input(dev, mode):
     """The fused Gram-backward phase exists only for raw-input data gradients: any
@@ -194,7 +228,9 @@ def test_amax(dev):
     assert g.numel() == N.STX_AMAX_SLOTS and float(g.max()) == 3.25
 
 
-@pytest.mark.parametrize("shape", [(2, 64, 64, 20, 70), (1, 128, 128, 17, 99)])
+@pytest.mark.parametrize("shape", [(2, 64, 64, 20, 70), (1, 128, 128, 17, 99),
+                                   # producer/consumer kernel, ragged last row pair
+                                   (2, 64, 64, 255, 258), (2, 64, 128, 128, 130)])
 def test_split_conv_pool_out(dev, shape):
     """Fused VGG ReLU+MaxPool2d output (floor mode, odd sizes) beside y; bit-exact
     against pooling the kernel's own y."""
@@ -248,6 +284,11 @@ def test_split_gram(dev, shape):
                                   (2, 64, 38, 72, N.STX_IN_RELU, False),
                                   (1, 32, 30, 100, N.STX_IN_RAW, False),
                                   (1, 64, 256, 256, N.STX_IN_RELU, True),
+                                  # producer/consumer kernel (>= 2 tiles per CU): Gatys
+                                  # conv1_2 at 512^2, and a batch of 2 at 256^2
+                                  (1, 64, 512, 512, N.STX_IN_RELU, True),
+                                  (2, 64, 256, 256, N.STX_IN_RELU, False),
+                                  (3, 64, 200, 260, N.STX_IN_RAW, True),
                                   # 3 input channels (conv1_1, convfew.hip): 64 x 8 tiles
                                   (1, 3, 64, 128, N.STX_IN_RAW, False),
                                   (2, 3, 30, 70, N.STX_IN_RAW, False)])
@@ -262,8 +303,10 @@ def test_fused_gram_partials(dev, case):
     bias = rnd(cout, dev=dev, seed=93, scale=0.2, shift=-0.1)
     wt = ops.conv_weight_prep(wgt)
     w16 = ops.conv_weight_prep16(wgt)
-    nt = ops.conv_gram_tiles(cin, cout, h, w)
-    assert nt == -(-w // 64) * -(-h // (8 if cin == 3 else 4))
+    nt = ops.conv_gram_tiles(cin, cout, h, w, n=n, in_mode=mode)
+    tiles = -(-w // 64) * -(-h // (8 if cin == 3 else 4))
+    # one partial per tile, or per persistent block (conv16pc.hip: whole images per block)
+    assert nt == tiles or (cin != 3 and tiles % nt == 0 and nt < tiles), (nt, tiles)
     parts = torch.full((n * nt * 4096,), float("nan"), device=dev)
     kw = {}
     if pool:
@@ -455,7 +498,9 @@ def test_weight_prep16_pair(dev, shape):
     assert float(am.max()) == float(am1.max()) == float(w.abs().max())
 
 
-@pytest.mark.parametrize("case", [(2, 64, 128, 32, 48), (1, 32, 64, 64, 64), (2, 64, 128, 17, 40)])
+@pytest.mark.parametrize("case", [(2, 64, 128, 32, 48), (1, 32, 64, 64, 64), (2, 64, 128, 17, 40),
+                                  # producer/consumer kernel (the ITN up-conv at B8)
+                                  (8, 32, 64, 128, 128)])
 def test_split_dgrad_upsample_sum(dev, case):
     """UpsampleConvLayer backward (stransfer/network.py:583-605): the data gradient of a
     conv over the nearest-x2 upsampled input with the 2x2 sums fused into its epilogue
