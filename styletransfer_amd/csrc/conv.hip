@@ -549,7 +549,6 @@ static int dispatch_tw(const stx_conv_params& p, hipStream_t st) {
 }
 
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st);  // conv16.hip
-int conv16_pc_gram_parts(const stx_conv_params& p);          // conv16pc.hip
 int conv2d_fewin(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
 int fewin_gram_tiles(const stx_conv_params& p);              // convfew.hip
 int conv2d_fewout(const stx_conv_params& p, hipStream_t st);  // convfew.hip (-1: not covered)
@@ -596,12 +595,7 @@ extern "C" int stx_conv_gram_tiles(const stx_conv_params* pp) {
                   p.stride == 1 && p.cin >= 16 && p.cout == 64 && p.wo > 32 &&
                   p.wt_batch_stride == 0 && !p.mask && !p.aux && !p.accumulate &&
                   !p.acc_scale && !p.up_dp && !p.p2_z && !p.relu_out;
-  if (ok) {
-    // the producer/consumer kernel: one partial per block (a block's tiles lie in one
-    // image); otherwise one per 64 x 4 tile
-    const int pc = conv16_pc_gram_parts(p);
-    return pc > 0 ? pc : cdiv(p.wo, 64) * cdiv(p.ho, 4);
-  }
+  if (ok) return cdiv(p.wo, 64) * cdiv(p.ho, 4);
   return fewin_gram_tiles(p);  // 3 input channels (VGG conv1_1): 64 x 8 tiles
 }
 

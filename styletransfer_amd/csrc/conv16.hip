@@ -1003,13 +1003,7 @@ __global__ void __launch_bounds__(256) weight_prep_batch_kernel(WprepJobs b) {
                        b.gin[j], b.gout[j], i0, step);
 }
 
-int conv16_pc(const stx_conv_params& p, hipStream_t st);  // conv16pc.hip (-1: not covered)
-
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st) {
-  if (p.stride == 1) {
-    const int rc = conv16_pc(p, st);  // producer / consumer waves, persistent blocks
-    if (rc >= 0) return rc;
-  }
   switch (p.stride == 2 ? LM_S2 : p.in_mode) {
     case STX_IN_RAW: return dispatch16_tw<STX_IN_RAW>(p, st);
     case STX_IN_RELU: return dispatch16_tw<STX_IN_RELU>(p, st);

@@ -177,47 +177,52 @@ lb_commit_kernel(LbHdr* __restrict__ hdr, char* __restrict__ st, float* __restri
 }
 
 // K3: per pair k (chronological) and block: s_k.g, y_k.g, s_k.y_new, y_k.y_new over the
-// block's 1024 elements.  Wave w takes the pairs k = w (mod 4), two at a time (their
-// eight 16-B loads in flight together); partials [k][q][block]
+// block's 1024 elements (each lane 4 float4 of the chunk, 256 elements apart).  Wave w takes
+// the pairs k = w (mod 4), each over the WHOLE chunk; partials [k][q][block]
 __global__ void __launch_bounds__(LB_NT)
 lb_dots_kernel(const float* __restrict__ g, const float* __restrict__ hist, long long n,
                long long np, int m1, const LbHdr* __restrict__ hdr, float* __restrict__ parts) {
   const int count = hdr->count;
   if (count == 0) return;
   const int nb = (int)gridDim.x;
-  const long long e = (long long)blockIdx.x * LB_CHUNK + 4 * threadIdx.x;
-  const f32x4 gv = ld4g(g, e, n);
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  const f32x4 yn = hdr->accepted
-                       ? *reinterpret_cast<const f32x4*>(hist + (size_t)(m1 + hdr->order[count - 1]) * np + e)
-                       : zero;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long e0 = (long long)blockIdx.x * LB_CHUNK + 4 * lane;
+  const bool acc = hdr->accepted;
+  const float* __restrict__ ynp = hist + (size_t)(m1 + hdr->order[count - 1]) * np;
+  f32x4 gv[4], yn[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long long e = e0 + 256 * u;
+    gv[u] = ld4g(g, e, n);
+    yn[u] = acc ? *reinterpret_cast<const f32x4*>(ynp + e) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   auto dot4 = [](f32x4 a, f32x4 b) {
     return fmaf(a[3], b[3], fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0])));
   };
-  auto emit = [&](int k, f32x4 sv, f32x4 yv) {
-    float d[4] = {dot4(sv, gv), dot4(yv, gv), dot4(sv, yn), dot4(yv, yn)};
+  for (int k = w; k < count; k += 4) {
+    const int sl = hdr->order[k];
+    const float* __restrict__ sp = hist + (size_t)sl * np;
+    const float* __restrict__ yp = hist + (size_t)(m1 + sl) * np;
+    f32x4 sv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sv[u] = *reinterpret_cast<const f32x4*>(sp + e0 + 256 * u);
+      yv[u] = *reinterpret_cast<const f32x4*>(yp + e0 + 256 * u);
+    }
+    float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      d[0] += dot4(sv[u], gv[u]);
+      d[1] += dot4(yv[u], gv[u]);
+      d[2] += dot4(sv[u], yn[u]);
+      d[3] += dot4(yv[u], yn[u]);
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) d[q] = wave_sum(d[q]);
     if (lane == 0) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) parts[((size_t)k * 4 + q) * nb + blockIdx.x] = d[q];
     }
-  };
-  int k = w;
-  for (; k + 4 < count; k += 8) {
-    const int s0 = hdr->order[k], s1 = hdr->order[k + 4];
-    const f32x4 sv0 = *reinterpret_cast<const f32x4*>(hist + (size_t)s0 * np + e);
-    const f32x4 yv0 = *reinterpret_cast<const f32x4*>(hist + (size_t)(m1 + s0) * np + e);
-    const f32x4 sv1 = *reinterpret_cast<const f32x4*>(hist + (size_t)s1 * np + e);
-    const f32x4 yv1 = *reinterpret_cast<const f32x4*>(hist + (size_t)(m1 + s1) * np + e);
-    emit(k, sv0, yv0);
-    emit(k + 4, sv1, yv1);
-  }
-  if (k < count) {
-    const int s0 = hdr->order[k];
-    emit(k, *reinterpret_cast<const f32x4*>(hist + (size_t)s0 * np + e),
-         *reinterpret_cast<const f32x4*>(hist + (size_t)(m1 + s0) * np + e));
   }
 }
 

@@ -50,7 +50,7 @@ CASES = [
     (2, 128, 128, 18, 70, N.STX_IN_RAW),
     (2, 64, 256, 32, 64, N.STX_IN_RAW),
     (2, 128, 128, 64, 64, N.STX_IN_RAW),     # ITN residual conv shape
-    # producer/consumer kernel (conv16pc.hip: >= 2 tiles per CU), every loader mode
+    # full-chip grids (many tiles per CU), every loader mode
     (2, 64, 64, 256, 256, N.STX_IN_RELU),
     (4, 64, 128, 128, 128, N.STX_IN_RAW),
     (4, 64, 128, 256, 256, N.STX_IN_RELU_POOL2),
@@ -176,10 +176,9 @@ def test_split_conv_fused_epilogue(dev):
 @pytest.mark.parametrize("shape", [(1, 64, 512, 512), (1, 128, 256, 256), (2, 64, 160, 300),
                                    (4, 64, 128, 128)])
 @pytest.mark.parametrize("scaled", [False, True])
-def test_split_conv_fused_epilogue_pc(dev, shape, scaled):
+def test_split_conv_fused_epilogue_large(dev, shape, scaled):
     """The Gram-backward data gradient at the VGG shapes (conv1_2^T at 512^2, conv2_2^T at
-    256^2 with two 64-cout blocks, ragged tiles, a batch of 4) on the producer/consumer
-    kernel: dZ = [Z > 0] conv^T(dY) + s2 A.Z against the fp32-MFMA kernel's fused
+    256^2 with two 64-cout blocks, ragged tiles, a batch of 4): dZ = [Z > 0] conv^T(dY) + s2 A.Z against the fp32-MFMA kernel's fused
     epilogue, and out_amax is the exact max|dZ|."""
     n, c, h, w = shape
     z = rnd(n, c, h, w, dev=dev, seed=191, scale=2, shift=-1)
@@ -229,7 +228,7 @@ def test_amax(dev):
 
 
 @pytest.mark.parametrize("shape", [(2, 64, 64, 20, 70), (1, 128, 128, 17, 99),
-                                   # producer/consumer kernel, ragged last row pair
+                                   # full-chip grids, ragged last row pair
                                    (2, 64, 64, 255, 258), (2, 64, 128, 128, 130)])
 def test_split_conv_pool_out(dev, shape):
     """Fused VGG ReLU+MaxPool2d output (floor mode, odd sizes) beside y; bit-exact
@@ -284,8 +283,7 @@ def test_split_gram(dev, shape):
                                   (2, 64, 38, 72, N.STX_IN_RELU, False),
                                   (1, 32, 30, 100, N.STX_IN_RAW, False),
                                   (1, 64, 256, 256, N.STX_IN_RELU, True),
-                                  # producer/consumer kernel (>= 2 tiles per CU): Gatys
-                                  # conv1_2 at 512^2, and a batch of 2 at 256^2
+                                  # Gatys conv1_2 at 512^2, and a batch of 2 at 256^2
                                   (1, 64, 512, 512, N.STX_IN_RELU, True),
                                   (2, 64, 256, 256, N.STX_IN_RELU, False),
                                   (3, 64, 200, 260, N.STX_IN_RAW, True),
@@ -305,8 +303,7 @@ def test_fused_gram_partials(dev, case):
     w16 = ops.conv_weight_prep16(wgt)
     nt = ops.conv_gram_tiles(cin, cout, h, w, n=n, in_mode=mode)
     tiles = -(-w // 64) * -(-h // (8 if cin == 3 else 4))
-    # one partial per tile, or per persistent block (conv16pc.hip: whole images per block)
-    assert nt == tiles or (cin != 3 and tiles % nt == 0 and nt < tiles), (nt, tiles)
+    assert nt == tiles, (nt, tiles)  # one partial per output tile
     parts = torch.full((n * nt * 4096,), float("nan"), device=dev)
     kw = {}
     if pool:

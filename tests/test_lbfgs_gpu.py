@@ -27,24 +27,37 @@ def quad_problem(dev, n=4096, seed=0):
                                        (5, 2500)])
 def test_lbfgs_matches_torch_on_quadratic(dev, history, n):
     """history 1 / 3 / 5 evict from the ring within the 4 steps; n = 4093 / 2500 are not
-    multiples of the 1024-element history chunk (padded slots, ragged tail)."""
+    multiples of the 1024-element history chunk (padded slots, ragged tail).
+    The compact form and torch's two-loop recursion agree in exact arithmetic; in fp32
+    their roundings differ and 4 steps x 20 iterations amplify them (the CPU restatement
+    of the compact form lands 1e-7 .. 3e-5 from torch's CPU run; on the GPU both fp32 runs
+    land 1e-6 .. 2e-4 from fp64, case by case either one nearer), so the end point is held
+    against torch's fp64 run: within 5x torch fp32's own distance from it (floor 1e-4)."""
     m, b, x0 = quad_problem(dev, n)
     xs = []
-    for cls in (torch.optim.LBFGS, stx_optim.LBFGS):
-        x = x0.clone().view(1, -1).requires_grad_()
+    runs = ((torch.optim.LBFGS, dev, torch.float32), (stx_optim.LBFGS, dev, torch.float32),
+            (torch.optim.LBFGS, "cpu", torch.float64))
+    for cls, where, dt in runs:
+        mm, bb = m.to(where, dt), b.to(where, dt)
+        x = x0.clone().to(where, dt).view(1, -1).requires_grad_()
         opt = cls([x], history_size=history)
 
         def closure():
             opt.zero_grad()
-            f = 0.5 * ((m * x.view(-1) - b) ** 2).sum() + 0.1 * (x ** 4).sum()
+            f = 0.5 * ((mm * x.view(-1) - bb) ** 2).sum() + 0.1 * (x ** 4).sum()
             f.backward()
             return f
 
         for _ in range(4):
             opt.step(closure)
-        xs.append(x.detach().clone())
-    err = float((xs[0] - xs[1]).norm() / xs[0].norm())
-    assert err < 1e-4, err
+        xs.append(x.detach().double().cpu().clone())
+    ref32, ours, ref64 = xs
+    rel = lambda a, c: float((a - c).norm() / c.norm())  # noqa: E731
+    e_ours, e_ref = rel(ours, ref64), rel(ref32, ref64)
+    print(f"history {history} n {n}: ours vs fp64 {e_ours:.2e}, torch fp32 vs fp64 {e_ref:.2e}, "
+          f"ours vs torch fp32 {rel(ours, ref32):.2e}")
+    assert e_ours <= max(5 * e_ref, 1e-4), (e_ours, e_ref)
+    assert rel(ours, ref32) < 1e-3
 
 
 def test_lbfgs_gatys(dev):
