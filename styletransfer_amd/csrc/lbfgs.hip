@@ -12,7 +12,8 @@
 // is two passes over the history slabs and an m x m solve:
 //   dots     u = S^T g, w = Y^T g (and, for a newly accepted pair, S^T y_new, Y^T y_new:
 //            the new column of R and row of Y^T Y) -- one read of S and Y
-//   solve    r = R^-1 u; a = R^-T ((D + g Y^T Y) r - g w)   (one wave, fp64)
+//   solve    r = R^-1 u; a = R^-T ((D + g Y^T Y) r - g w)   (one block, fp64, R^-1 kept
+//            up to date: three matrix-vector products, no serial substitution)
 //   combine  d = -g g - S a + g Y r; s_next = t d; g.d; max|t d| -- one read of S and Y
 // so an iteration reads the 2m history vectors twice (torch: twice too, in 4m launches).
 //
@@ -40,7 +41,7 @@ struct LbHdr {
 
 struct LbLayout {
   int m1;
-  size_t sy, yy, dots, coef, total;
+  size_t sy, yy, ri, dots, coef, total;
   __host__ __device__ explicit LbLayout(int m) {
     m1 = m + 1;
     size_t o = (sizeof(LbHdr) + 255) & ~size_t(255);
@@ -48,6 +49,8 @@ struct LbLayout {
     o += sizeof(double) * m1 * m1;  // s_i . y_j by slot
     yy = o;
     o += sizeof(double) * m1 * m1;  // y_i . y_j by slot
+    ri = o;
+    o += sizeof(double) * m1 * m1;  // (R^-1)_ij by slot (upper triangle in chronological order)
     dots = o;
     o += sizeof(double) * 4 * m1;   // per chronological pair: s.g, y.g, s.yn, y.yn
     coef = o;
@@ -199,16 +202,22 @@ lb_dots_kernel(const float* __restrict__ g, const float* __restrict__ hist, long
   auto dot4 = [](f32x4 a, f32x4 b) {
     return fmaf(a[3], b[3], fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0])));
   };
-  for (int k = w; k < count; k += 4) {
-    const int sl = hdr->order[k];
+  // pair k+4's loads are issued before pair k's sums (unconditional: the index is clamped,
+  // so the wait before the sums covers exactly one pair's loads)
+  f32x4 sv[4], yv[4], sn[4], ynx[4];
+  auto load_pair = [&](int kk, f32x4 (&a)[4], f32x4 (&b)[4]) {
+    const int sl = hdr->order[min(kk, count - 1)];
     const float* __restrict__ sp = hist + (size_t)sl * np;
     const float* __restrict__ yp = hist + (size_t)(m1 + sl) * np;
-    f32x4 sv[4], yv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      sv[u] = *reinterpret_cast<const f32x4*>(sp + e0 + 256 * u);
-      yv[u] = *reinterpret_cast<const f32x4*>(yp + e0 + 256 * u);
+      a[u] = *reinterpret_cast<const f32x4*>(sp + e0 + 256 * u);
+      b[u] = *reinterpret_cast<const f32x4*>(yp + e0 + 256 * u);
     }
+  };
+  if (w < count) load_pair(w, sv, yv);
+  for (int k = w; k < count; k += 4) {
+    load_pair(k + 4, sn, ynx);
     float d[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -222,6 +231,11 @@ lb_dots_kernel(const float* __restrict__ g, const float* __restrict__ hist, long
     if (lane == 0) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) parts[((size_t)k * 4 + q) * nb + blockIdx.x] = d[q];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sv[u] = sn[u];
+      yv[u] = ynx[u];
     }
   }
 }
@@ -245,61 +259,94 @@ lb_dots_fin_kernel(const float* __restrict__ parts, int nb, const LbHdr* __restr
   if (threadIdx.x == 0) reinterpret_cast<double*>(st + L.dots)[b] = red[0];
 }
 
-// K4 (one wave, fp64): the new column of R / row of Y^T Y, then
-//   r = R^-1 u,  a = R^-T ((D + g Y^T Y) r - g w),  coefficients  s_k: -a_k,  y_k: g r_k
-// Lane l owns the chronological pairs l, l + 64, ... (up to 5 per lane).
-__global__ void __launch_bounds__(64)
+// K4 (one block, fp64): the new column of Y^T Y and of R^-1, then
+//   r = R^-1 u,  z = (D + g Y^T Y) r - g w,  a = R^-T z,  coefficients  s_k: -a_k,  y_k: g r_k
+// R^-1 is kept current instead of solving with R: dropping the oldest pair drops the
+// first row and column of both R and R^-1 (the inverse of an upper-triangular matrix's
+// trailing block is the trailing block of its inverse), and appending pair n (column
+// c_i = s_i.y_n, diagonal d = s_n.y_n) appends the column -R^-1 c / d and 1 / d.  Every
+// phase is a matrix-vector product: 8 neighbouring lanes per row (rows 128 apart per
+// pass), each lane a strided set of columns (independent loads), a fixed-order sum over
+// the 8 lanes.
+constexpr int LB_SOLVE_NT = 1024;
+constexpr int LB_RG = 8;  // lanes per row
+
+__device__ __forceinline__ double group_sum8(double v) {
+#pragma unroll
+  for (int o = 1; o < LB_RG; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(LB_SOLVE_NT)
 lb_solve_kernel(LbHdr* __restrict__ hdr, char* __restrict__ st, int m) {
   const LbLayout L(m);
   const int k = hdr->count;
   double* SY = reinterpret_cast<double*>(st + L.sy);
   double* YY = reinterpret_cast<double*>(st + L.yy);
+  double* RI = reinterpret_cast<double*>(st + L.ri);
   const double* dots = reinterpret_cast<const double*>(st + L.dots);
   float* coef = reinterpret_cast<float*>(st + L.coef);
-  const int m1 = L.m1, lane = threadIdx.x;
+  const int m1 = L.m1, sub = threadIdx.x % LB_RG, row0 = threadIdx.x / LB_RG;
+  constexpr int RPP = LB_SOLVE_NT / LB_RG;  // rows per pass
   __shared__ int slot[LB_MAXM + 1];
-  __shared__ double vec[LB_MAXM + 1], r[LB_MAXM + 1];
-  for (int i = lane; i < k; i += 64) slot[i] = hdr->order[i];
+  __shared__ double vu[LB_MAXM + 1], vc[LB_MAXM + 1], vr[LB_MAXM + 1], vz[LB_MAXM + 1];
+  for (int i = threadIdx.x; i < k; i += LB_SOLVE_NT) {
+    slot[i] = hdr->order[i];
+    vu[i] = dots[4 * i];
+    vc[i] = dots[4 * i + 2];
+  }
   __syncthreads();
   if (hdr->accepted && k > 0) {
     const int nw = slot[k - 1];
-    for (int i = lane; i < k; i += 64) {
+    const double dinv = 1.0 / SY[(size_t)nw * m1 + nw];
+    for (int i = threadIdx.x; i < k; i += LB_SOLVE_NT) {
       const int si = slot[i];
-      SY[(size_t)si * m1 + nw] = dots[4 * i + 2];
+      SY[(size_t)si * m1 + nw] = vc[i];
       YY[(size_t)si * m1 + nw] = dots[4 * i + 3];
       YY[(size_t)nw * m1 + si] = dots[4 * i + 3];
     }
+    // column k-1 of R^-1: rows i < k-1 from the old R^-1 (columns i .. k-2)
+    for (int i = row0; i < k - 1; i += RPP) {
+      const double* row = RI + (size_t)slot[i] * m1;
+      double acc = 0.0;
+      for (int j = i + sub; j < k - 1; j += LB_RG) acc = fma(row[slot[j]], vc[j], acc);
+      acc = group_sum8(acc);
+      if (sub == 0) RI[(size_t)slot[i] * m1 + nw] = -acc * dinv;
+    }
+    if (threadIdx.x == 0) RI[(size_t)nw * m1 + nw] = dinv;
   }
   __syncthreads();
   const double gam = (double)hdr->H_diag;
-  // back substitution r = R^-1 u (R upper triangular in chronological order)
-  for (int i = lane; i < k; i += 64) vec[i] = dots[4 * i];
-  __syncthreads();
-  for (int c = k - 1; c >= 0; --c) {
-    const double rc = vec[c] / SY[(size_t)slot[c] * m1 + slot[c]];
-    __syncthreads();
-    if (lane == 0) r[c] = rc;
-    for (int i = lane; i < c; i += 64) vec[i] -= SY[(size_t)slot[i] * m1 + slot[c]] * rc;
-    __syncthreads();
-  }
-  // z = (D + g Y^T Y) r - g w
-  for (int i = lane; i < k; i += 64) {
-    const int si = slot[i];
-    double z = SY[(size_t)si * m1 + si] * r[i] - gam * dots[4 * i + 1];
+  // r = R^-1 u
+  for (int i = row0; i < k; i += RPP) {
+    const double* row = RI + (size_t)slot[i] * m1;
     double acc = 0.0;
-    for (int j = 0; j < k; ++j) acc += YY[(size_t)si * m1 + slot[j]] * r[j];
-    vec[i] = z + gam * acc;
+    for (int j = i + sub; j < k; j += LB_RG) acc = fma(row[slot[j]], vu[j], acc);
+    acc = group_sum8(acc);
+    if (sub == 0) vr[i] = acc;
   }
   __syncthreads();
-  // forward substitution a = R^-T z
-  for (int c = 0; c < k; ++c) {
-    const double ac = vec[c] / SY[(size_t)slot[c] * m1 + slot[c]];
-    __syncthreads();
-    if (lane == 0) coef[c] = (float)(-ac);
-    for (int i = c + 1 + lane; i < k; i += 64) vec[i] -= SY[(size_t)slot[c] * m1 + slot[i]] * ac;
-    __syncthreads();
+  // z = (D + g Y^T Y) r - g w
+  for (int i = row0; i < k; i += RPP) {
+    const int si = slot[i];
+    const double* row = YY + (size_t)si * m1;
+    double acc = 0.0;
+    for (int j = sub; j < k; j += LB_RG) acc = fma(row[slot[j]], vr[j], acc);
+    acc = group_sum8(acc);
+    if (sub == 0) vz[i] = SY[(size_t)si * m1 + si] * vr[i] - gam * dots[4 * i + 1] + gam * acc;
   }
-  for (int i = lane; i < k; i += 64) coef[m1 + i] = (float)(gam * r[i]);
+  __syncthreads();
+  // a = R^-T z
+  for (int i = row0; i < k; i += RPP) {
+    const int si = slot[i];
+    double acc = 0.0;
+    for (int j = sub; j <= i; j += LB_RG) acc = fma(RI[(size_t)slot[j] * m1 + si], vz[j], acc);
+    acc = group_sum8(acc);
+    if (sub == 0) {
+      coef[i] = (float)(-acc);
+      coef[m1 + i] = (float)(gam * vr[i]);
+    }
+  }
 }
 
 // K5: d = -H_diag g + sum_k (cs_k s_k + cy_k y_k); s_next = t d into the free slot;
@@ -364,11 +411,14 @@ lb_combine_kernel(const float* __restrict__ g, float* __restrict__ hist, long lo
   }
 }
 
-// K6 (one block): g.d and max|t d|; flag = (g.d > -tolerance_change): torch breaks before
-// moving x
+// K6: g.d and max|t d| (every block sums the combine's partials in the same fixed order,
+// so all blocks agree bit for bit); flag = (g.d > -tolerance_change): torch breaks before
+// moving x; otherwise x += t d (= s_next).  Block 0 publishes the scalars.
 __global__ void __launch_bounds__(LB_NT)
-lb_finish_kernel(LbHdr* __restrict__ hdr, float* __restrict__ scal, const float* __restrict__ parts,
-                 int nb, float tol_change) {
+lb_finish_step_kernel(LbHdr* __restrict__ hdr, float* __restrict__ scal,
+                      const float* __restrict__ parts, int nb, float tol_change,
+                      float* __restrict__ x, const float* __restrict__ hist, long long n,
+                      long long np) {
   __shared__ float red[8];
   float gd = 0.f, dm = 0.f;
   for (int i = threadIdx.x; i < nb; i += LB_NT) {  // fixed order per thread
@@ -376,8 +426,9 @@ lb_finish_kernel(LbHdr* __restrict__ hdr, float* __restrict__ scal, const float*
     dm = nanmax(dm, parts[2 * i + 1]);
   }
   block_red2<true>(gd, dm, red);
-  if (threadIdx.x == 0) {
-    const int flag = gd > -tol_change;
+  const int flag = gd > -tol_change;
+  const int cand = hdr->cand;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     hdr->flag = flag;
     hdr->gtd = gd;
     hdr->dmax = dm;
@@ -386,14 +437,8 @@ lb_finish_kernel(LbHdr* __restrict__ hdr, float* __restrict__ scal, const float*
     scal[5] = dm;
     scal[6] = (float)flag;
   }
-}
-
-// K7: x += t d (= s_next), unless the iteration stopped on g.d
-__global__ void __launch_bounds__(LB_NT)
-lb_step_kernel(float* __restrict__ x, const float* __restrict__ hist, long long n, long long np,
-               const LbHdr* __restrict__ hdr) {
-  if (hdr->flag) return;
-  const float* __restrict__ s = hist + (size_t)hdr->cand * np;
+  if (flag) return;
+  const float* __restrict__ s = hist + (size_t)cand * np;
   const long long n4 = n >> 2;
   for (long long i = blockIdx.x * (long long)LB_NT + threadIdx.x; i < n4;
        i += (long long)gridDim.x * LB_NT)
@@ -403,7 +448,7 @@ lb_step_kernel(float* __restrict__ x, const float* __restrict__ hist, long long 
     x[i] += s[i];
 }
 
-// K8/K9: max|g| (NaN propagates, as torch's max) and sum|g| of a fresh gradient; the loss
+// K7/K8: max|g| (NaN propagates, as torch's max) and sum|g| of a fresh gradient; the loss
 // copied next to them (one host read); optionally zero `clear` (the Gatys engine's amax
 // groups, next written by the following forward)
 __global__ void __launch_bounds__(LB_NT)
@@ -515,11 +560,11 @@ extern "C" int stx_lbfgs_direction(float* x, const float* g, float* prev_g, floa
   hipLaunchKernelGGL(lb_commit_kernel, dim3(1), dim3(LB_NT), 0, st, hdr, sb, scal, p1, m, lr);
   hipLaunchKernelGGL(lb_dots_kernel, dim3(nb), dim3(LB_NT), 0, st, g, hist, n, np, m + 1, hdr, p3);
   hipLaunchKernelGGL(lb_dots_fin_kernel, dim3(4 * (m + 1)), dim3(LB_NT), 0, st, p3, nb, hdr, sb, m);
-  hipLaunchKernelGGL(lb_solve_kernel, dim3(1), dim3(64), 0, st, hdr, sb, m);
+  hipLaunchKernelGGL(lb_solve_kernel, dim3(1), dim3(LB_SOLVE_NT), 0, st, hdr, sb, m);
   hipLaunchKernelGGL(lb_combine_kernel, dim3(nb), dim3(LB_NT), 0, st, g, hist, n, np, hdr, sb, m,
                      p5);
-  hipLaunchKernelGGL(lb_finish_kernel, dim3(1), dim3(LB_NT), 0, st, hdr, scal, p5, nb, tol_change);
-  hipLaunchKernelGGL(lb_step_kernel, dim3(LB_G), dim3(LB_NT), 0, st, x, hist, n, np, hdr);
+  hipLaunchKernelGGL(lb_finish_step_kernel, dim3(LB_G), dim3(LB_NT), 0, st, hdr, scal, p5, nb,
+                     tol_change, x, hist, n, np);
   return check_launch("stx_lbfgs_direction");
 }
 

@@ -129,7 +129,9 @@ class LBFGS(torch.optim.Optimizer):
                 ws=torch.zeros(wb, device=dev, dtype=torch.uint8),
                 prev_g=torch.zeros(npad, device=dev, dtype=torch.float32),
                 scal=torch.zeros(self.NSCAL, device=dev, dtype=torch.float32),
-                loss=torch.zeros(1, device=dev, dtype=torch.float32))
+                loss=torch.zeros(1, device=dev, dtype=torch.float32),
+                # pinned mirror of scal: one D2H copy per read, no gather kernel
+                host=torch.zeros(self.NSCAL, dtype=torch.float32, pin_memory=True))
         return self._buf
 
     def grad_stats(self, g, loss=None, clear=None):
@@ -155,7 +157,17 @@ class LBFGS(torch.optim.Optimizer):
             b["ws"].data_ptr(), b["ws"].numel(), ops._stream()), "stx_lbfgs_direction")
 
     def _scal(self, *idx):
-        return self._buf["scal"][list(idx)].tolist()  # one device->host read
+        """scal[idx] on the host: one async copy into the pinned mirror + a stream sync."""
+        b = self._buf
+        b["host"].copy_(b["scal"], non_blocking=True)
+        return self._scal_host(*idx)
+
+    def _scal_host(self, *idx):
+        """scal[idx] from the pinned mirror once the current stream's work (which ends with
+        the mirror copy, e.g. a captured graph's last node) is done."""
+        torch.cuda.current_stream().synchronize()
+        h = self._buf["host"].tolist()
+        return [h[i] for i in idx]
 
     def _grad(self):
         g = self._p.grad

@@ -542,17 +542,21 @@ class GatysLBFGS:
         with torch.cuda.stream(s):
             self._closure()  # allocates every buffer (x unchanged: no optimiser state)
         torch.cuda.current_stream().wait_stream(s)
+        b = self.opt._buf
         self.g_eval = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_eval):
             self._closure()
+            b["host"].copy_(b["scal"], non_blocking=True)  # the scalars torch tests
         self.g_iter = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_iter, pool=self.g_eval.pool()):
             self.opt.direction(self.grad.view(-1))
             self._closure()
+            b["host"].copy_(b["scal"], non_blocking=True)
         return self
 
     def _read(self):
-        loss, gmax, gtd, t, smax, flag = self.opt._scal(0, 1, 3, 4, 5, 6)
+        # the graph's last node copied scal into the pinned mirror
+        loss, gmax, gtd, t, smax, flag = self.opt._scal_host(0, 1, 3, 4, 5, 6)
         return loss, gmax, gtd, t, smax, flag
 
     def step(self, on_eval=None):
@@ -564,7 +568,7 @@ class GatysLBFGS:
         def evaluate():
             self.g_eval.replay()
             self.closure_runs += 1
-            loss, gmax = self.opt._scal(0, 1)
+            loss, gmax = self.opt._scal_host(0, 1)
             self._at_x = (loss, loss, gmax, self.grad.view(-1))
             return self._at_x
 
