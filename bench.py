@@ -193,12 +193,19 @@ def gatys_leg(args, world, rank, dev):
     am_out = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
     pool = torch.empty_like(eng.st.pools[1])
     gparts = eng.st.grams[1]
-    gp = torch.empty_like(gparts) if gparts is not None else None
+    grouped = isinstance(gparts, tuple)  # (per-tile scratch + group sums, group counters)
+    if grouped:
+        gp = (torch.empty_like(gparts[0]), torch.zeros_like(gparts[1]))
+    else:
+        gp = torch.empty_like(gparts) if gparts is not None else None
 
-    def conv12(gram_part):
+    def conv12(g):
+        kw = {}
+        if g is not None:
+            kw = dict(gram_part=g[0], gram_cnt=g[1]) if grouped else dict(gram_part=g)
         return ops.conv2d(z1, feat.wt[1], 64, 64, 3, in_mode=N.STX_IN_RELU, bias=feat.b[1],
                           out=out, wt16=feat.wt16[1], in_amax=am, out_amax=am_out,
-                          pool_out=pool, gram_part=gram_part)
+                          pool_out=pool, **kw)
 
     fwd_ms = event_avg_ms(lambda: conv12(gp), reps=20)
     gf_conv = conv_gflop(64, 64, H, H)
@@ -212,13 +219,17 @@ def gatys_leg(args, world, rank, dev):
     if gp is not None:
         plain_ms = event_avg_ms(lambda: conv12(None), reps=20)
         conv12(gp)
-        nt = gp.numel() // 4096
+        if grouped:  # the finalize reads the group sums only
+            nt = gp[1].numel()
+            parts = gp[0][gp[0].numel() - nt * 4096:]
+        else:
+            nt, parts = gp.numel() // 4096, gp
         wsb = torch.empty(N.lib().stx_gram_ws(1, 64, H * H), device=dev, dtype=torch.uint8)
         tgt = eng.targets[1]
-        fin_ms = event_avg_ms(lambda: ops.style_loss_from_parts(gp, nt, 1, 64, H * H, tgt,
+        fin_ms = event_avg_ms(lambda: ops.style_loss_from_parts(parts, nt, 1, 64, H * H, tgt,
                                                                 defer_ws=wsb), reps=20)
         gram = dict(ms=max(fwd_ms - plain_ms, 0.0) + fin_ms, fused=True, epi_ms=fwd_ms - plain_ms,
-                    finalize_ms=fin_ms, conv_ms=plain_ms)
+                    finalize_ms=fin_ms, conv_ms=plain_ms, partials=nt, grouped=grouped)
     else:
         zam = V.slot(eng.st.amax, 2).clone()
         gram = dict(ms=event_avg_ms(lambda: ops.gram(z2, z_amax=zam), reps=20), fused=False)
@@ -623,13 +634,17 @@ def main():
             },
             "gram_roofline": {
                 "kernel": ("fused into conv1_2's epilogue (launch with gram_part minus launch "
-                           "without) + gram_finalize_kernel from the partials"
+                           "without; with gram_cnt the epilogue also sums each group of "
+                           f"{N.STX_GRAM_GROUP} tiles' partials in-launch) + gram_finalize_kernel "
+                           "from the partials it leaves"
                            if g["gram"]["fused"] else
                            "gram_partial_f16_kernel + gram_finalize_kernel")
                           + f" (StyleLoss.gram_matrix of conv1_2's output, C=64, HW={args.size}^2)",
                 "ms": round(g["gram"]["ms"], 4),
                 "parts_ms": {kk: round(v, 4) for kk, v in g["gram"].items()
                              if kk in ("epi_ms", "finalize_ms", "conv_ms")},
+                "finalize_partials": g["gram"].get("partials"),
+                "finalize_partial_mb": round(g["gram"].get("partials", 0) * 16384 / 1e6, 2),
                 "achieved_tflops_fp32eq": round(g["gram"]["gflop"] / g["gram"]["ms"], 2),
                 "mfma_bf16_peak_frac": round(3 * g["gram"]["gflop"] / g["gram"]["ms"]
                                              / PEAK_F16_MFMA_TFLOPS, 4),

@@ -121,7 +121,18 @@ typedef struct stx_conv_params {
    * ho / wo, plain epilogue only (no mask / aux / accumulate / acc_scale / up_dp / p2_z /
    * relu_out / gram_part / out_amax). */
   int pool_sum;
+  /* optional with gram_part: per-group arrival counters, n * stx_conv_gram_groups(p)
+   * uint32 words, zeroed once by the caller (every call leaves them zero again).  The
+   * partials of tiles g*STX_GRAM_GROUP .. g*STX_GRAM_GROUP+7 of image n form group g;
+   * the last block of a group to finish sums the group's partials in tile order and
+   * writes that sum to gram_part + (n_total * T + n * NG + g) * 4096 (NG =
+   * stx_conv_gram_groups(p)), so stx_style_loss_from_parts reads NG sums per image
+   * instead of T partials.  The per-tile slots then hold three of the four 32 x 32
+   * blocks only (scratch); the gram_part slab needs (T + NG) * 4096 floats per image. */
+  unsigned int* gram_cnt;
 } stx_conv_params;
+
+#define STX_GRAM_GROUP 8
 
 int stx_version(void);
 const char* stx_last_error_string(void);
@@ -174,6 +185,9 @@ int stx_amax(const float* x, long long n, float* out, void* stream);
 /* Gram partials per image a stx_conv2d call with these params writes through
  * gram_part (its 256-pixel output tiles), or 0 when the fused Gram does not apply. */
 int stx_conv_gram_tiles(const stx_conv_params* p);
+/* Gram group sums per image written with gram_cnt (ceil(T / STX_GRAM_GROUP)), 0 when
+ * the fused Gram does not apply. */
+int stx_conv_gram_groups(const stx_conv_params* p);
 
 /* Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_32x32x2_f32), fused input
  * transform (in_mode) and epilogue (bias, mask, aux, accumulate, relu). */

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("STX_LIB", os.path.join(_HERE, "libstx.so"))
 
 STX_IN_RAW, STX_IN_RELU, STX_IN_RELU_POOL2, STX_IN_UPSAMPLE2, STX_IN_DILATE2 = range(5)
 STX_AMAX_SLOTS = 32  # an "amax" is a group of 32 floats whose max is the value (stx.h)
+STX_GRAM_GROUP = 8  # fused Gram partials per in-kernel group sum (stx_conv_params.gram_cnt)
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -37,6 +38,7 @@ class ConvParams(C.Structure):
         ("up_dp", vp), ("up_z", vp),
         ("wt16", vp), ("w_amax", vp), ("in_amax", vp), ("out_amax", vp),
         ("pool_out", vp), ("p2_amax", vp), ("gram_part", vp), ("pool_sum", i32),
+        ("gram_cnt", vp),
     ]
 
 
@@ -89,6 +91,7 @@ SIGNATURES = {
     "stx_conv_weight_prep": (i32, [vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv2d": (i32, [C.POINTER(ConvParams), vp]),
     "stx_conv_gram_tiles": (i32, [C.POINTER(ConvParams)]),
+    "stx_conv_gram_groups": (i32, [C.POINTER(ConvParams)]),
     "stx_conv_weight16_bytes": (sz, [i32, i32, i32, i32]),
     "stx_conv_weight_prep16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv_weight_prep16_pair": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),

@@ -599,6 +599,11 @@ extern "C" int stx_conv_gram_tiles(const stx_conv_params* pp) {
   return fewin_gram_tiles(p);  // 3 input channels (VGG conv1_1): 64 x 8 tiles
 }
 
+extern "C" int stx_conv_gram_groups(const stx_conv_params* pp) {
+  const int t = stx_conv_gram_tiles(pp);
+  return t > 0 ? cdiv(t, STX_GRAM_GROUP) : 0;
+}
+
 extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   if (!pp) {
     set_error("stx_conv2d: null params");
@@ -662,6 +667,11 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
        p.gram_part || p.out_amax || p.wt_batch_stride)) {
     set_error("stx_conv2d: pool_sum needs pool_out on the split path (3x3 stride 1, wo > 32, "
               "even output dims) and the plain epilogue");
+    return STX_E_INVALID;
+  }
+  if (p.gram_cnt && (!p.gram_part || (reinterpret_cast<uintptr_t>(p.gram_part) & 15) ||
+                     (long long)stx_conv_gram_tiles(&p) * 16384 >= (1ll << 31))) {
+    set_error("stx_conv2d: gram_cnt needs a 16-byte aligned gram_part slab (< 2 GB per image)");
     return STX_E_INVALID;
   }
   if (p.gram_part && !stx_conv_gram_tiles(&p)) {

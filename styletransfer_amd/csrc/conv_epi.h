@@ -148,6 +148,70 @@ __device__ __forceinline__ void gram_store(float* out, const f32x16& g, int wave
   }
 }
 
+// Grouped partials (stx_conv_params.gram_cnt): the in-launch fixed-order reduction of
+// STX_GRAM_GROUP consecutive tiles' partials, so the loss finalize reads one 16 KB sum
+// per group instead of one partial per tile.  Called by all four waves (waves 0..2 hold
+// the blocks (0,0), (0,1), (1,1) in g).  Hand-off (cdna_hip_programming.md §6 G16, the
+// sc1 form): each wave stores its block TRANSPOSED with 16-B write-through (sc1) stores --
+// (0,0) and (1,1) are symmetric blocks, and (0,1) lands as its mirror (1,0), so no
+// 4-byte stores -- drains them (vmcnt(0)), the block barrier, then one lane's relaxed
+// agent-scope ticket add; the block that draws the group's last ticket resets the
+// counter and reads the group's partials with sc1 loads (no acquire fence: every load of
+// the handed-off bytes is sc1), sums them in tile order and writes the group sum
+// (plain stores: read by the next launch), mirroring (1,0) into (0,1).
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+
+__device__ __forceinline__ void gram_store_grouped(const stx_conv_params& p, int n, int tix,
+                                                   int ntl, const f32x16& g, int wave, int h,
+                                                   int l32, float* flag) {
+  constexpr int G = STX_GRAM_GROUP;
+  const int grp = tix / G, g0 = grp * G, gs = min(G, ntl - g0), ng = cdiv(ntl, G);
+  const auto rs = make_srd(p.gram_part + (size_t)n * ntl * 4096, (uint32_t)ntl * 16384u);
+  if (wave < 3) {
+    const int I = wave == 2 ? 1 : 0, J = wave == 0 ? 0 : 1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = {g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]};
+      const uint32_t off =
+          (uint32_t)((tix * 64 + J * 32 + l32) * 64 + I * 32 + 8 * q + 4 * h) * 4u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, off, 0, 16);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gu32_t* cnt = (gu32_t*)(p.gram_cnt + (size_t)n * ng + grp);
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = t == (unsigned)(gs - 1);
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last ? 1.f : 0.f;
+  }
+  __syncthreads();
+  if (*flag == 0.f) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float* gsum = p.gram_part + ((size_t)p.n * ntl + (size_t)n * ng + grp) * 4096;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {  // stored blocks (0,0), (1,0), (1,1): 256 float4 each
+    const int f = threadIdx.x, rr = f >> 3, c4 = f & 7;
+    const int row = (k == 0 ? 0 : 32) + rr, col = (k == 2 ? 32 : 0) + 4 * c4;
+    f32x4 v[G];
+#pragma unroll
+    for (int m = 0; m < G; ++m) {
+      const uint32_t off = (uint32_t)(((g0 + min(m, gs - 1)) * 64 + row) * 64 + col) * 4u;
+      v[m] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+    }
+    f32x4 s = v[0];
+#pragma unroll
+    for (int m = 1; m < G; ++m)
+      if (m < gs) s += v[m];
+    *reinterpret_cast<f32x4*>(gsum + row * 64 + col) = s;
+    if (k == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gsum[(col + e) * 64 + row] = s[e];
+    }
+  }
+}
+
 // conv16's 64 x 256 tile: acc holds y; lane_ok[j] marks pixels inside the image
 template <int NI>
 __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
@@ -171,18 +235,21 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
         gram_put(H, GP::HP, ch, wave * 64 + j * 32 + l32, lane_ok[j] ? acc[i][j][r] * sx : 0.f);
       }
   __syncthreads();
-  if (wave < 3) {
-    f32x16 g;
+  f32x16 g;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) g[q] = 0.f;
+  for (int q = 0; q < 16; ++q) g[q] = 0.f;
+  if (wave < 3) {
     gram_mma<16>(H, GP::HP, wave, h, l32, g);
     const float inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
 #pragma unroll
     for (int q = 0; q < 16; ++q) g[q] *= inv2;
-    const int tix = t.tile >= 0 ? t.tile : (int)blockIdx.x;
-    const int ntl = t.tile >= 0 ? t.ntiles : (int)gridDim.x;
-    float* out = p.gram_part + ((size_t)blockIdx.z * ntl + tix) * 4096;
-    gram_store(out, g, wave, h, l32);
+  }
+  const int tix = t.tile >= 0 ? t.tile : (int)blockIdx.x;
+  const int ntl = t.tile >= 0 ? t.ntiles : (int)gridDim.x;
+  if (p.gram_cnt) {  // (red's block maxima were read before the barrier above)
+    gram_store_grouped(p, blockIdx.z, tix, ntl, g, wave, h, l32, red);
+  } else if (wave < 3) {
+    gram_store(p.gram_part + ((size_t)blockIdx.z * ntl + tix) * 4096, g, wave, h, l32);
   }
 }
 

@@ -341,9 +341,13 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
       }
     }
   }
-  if constexpr (GRAM) if (gram && wave < 3)
-    gram_store(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, g, wave, h,
-               l32);
+  if constexpr (GRAM) if (gram) {
+    if (p.gram_cnt)
+      gram_store_grouped(p, blockIdx.z, blockIdx.x, gridDim.x, g, wave, h, l32, gred);
+    else if (wave < 3)
+      gram_store(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, g, wave,
+                 h, l32);
+  }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
@@ -361,7 +365,6 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
 //    from registers, at its own power-of-two scale (no barrier per N-block); the four
 //    waves' partials are summed once per block through LDS in a fixed order.
 // wo % 4 == 0 (whole 16-B groups); otherwise the lane-per-pixel kernel above runs.
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 template <int MT>
 __global__ void __launch_bounds__(256, 2) conv_fewin16t_kernel(stx_conv_params p, int tiles_x) {
@@ -567,17 +570,23 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16t_kernel(stx_conv_params p
     for (int b3 = 0; b3 < 3; ++b3)
       *reinterpret_cast<f32x16*>(&gsum[((wave * 3 + b3) * 64 + lane) * 16]) = g[b3];
     __syncthreads();
+    f32x16 s;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s[q] = 0.f;
     if (wave < 3) {
-      f32x16 s = *reinterpret_cast<const f32x16*>(&gsum[((0 * 3 + wave) * 64 + lane) * 16]);
+      s = *reinterpret_cast<const f32x16*>(&gsum[((0 * 3 + wave) * 64 + lane) * 16]);
 #pragma unroll
       for (int w = 1; w < 4; ++w) {
         const f32x16 o = *reinterpret_cast<const f32x16*>(&gsum[((w * 3 + wave) * 64 + lane) * 16]);
 #pragma unroll
         for (int q = 0; q < 16; ++q) s[q] += o[q];
       }
+    }
+    if (p.gram_cnt)  // (gsum's first word becomes the reducer flag after the helper's barrier)
+      gram_store_grouped(p, blockIdx.z, blockIdx.x, gridDim.x, s, wave, h, l32, gsum);
+    else if (wave < 3)
       gram_store(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, s, wave, h,
                  l32);
-    }
   }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }

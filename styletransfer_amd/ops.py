@@ -347,7 +347,8 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
            out=None, mask=None, aux=None, aux_scale=0.0, acc_scale=None, accumulate=False,
            relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
            p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
-           pool_out=None, p2_amax=None, split_1x1=False, gram_part=None, pool_sum=False):
+           pool_out=None, p2_amax=None, split_1x1=False, gram_part=None, pool_sum=False,
+           gram_cnt=None):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
     up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
@@ -413,20 +414,33 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
     if gram_part is not None:
         _req(gram_part, "gram_part")
         nt = lib().stx_conv_gram_tiles(C.byref(p))
-        assert nt > 0 and gram_part.numel() >= n * nt * 4096, (nt, gram_part.numel())
+        ng = lib().stx_conv_gram_groups(C.byref(p)) if gram_cnt is not None else 0
+        assert nt > 0 and gram_part.numel() >= n * (nt + ng) * 4096, (nt, ng, gram_part.numel())
         p.gram_part = gram_part.data_ptr()
+        if gram_cnt is not None:
+            assert gram_cnt.is_cuda and gram_cnt.dtype == torch.int32 and \
+                gram_cnt.numel() >= n * ng, (gram_cnt.dtype, gram_cnt.numel(), n * ng)
+            p.gram_cnt = gram_cnt.data_ptr()
     check(lib().stx_conv2d(C.byref(p), _stream()), "stx_conv2d")
     return out
 
 
 def conv_gram_tiles(cin, cout, ho, wo, n=1, in_mode=N.STX_IN_RAW):
-    """Gram partials per image of a split 3x3 stride-1 conv with a fused Gram over a
-    batch of n (stx_conv_gram_tiles; 0: not fusable).  The count depends on the launch
-    (one per 64 x 4 tile, or one per persistent block of the producer/consumer kernel),
-    so n and the loader mode must be the ones of the conv call."""
+    """Gram partials per image (one per output tile) of a split 3x3 stride-1 conv with a
+    fused Gram over a batch of n (stx_conv_gram_tiles; 0: not fusable)."""
     p = ConvParams(cin=cin, cout=cout, ks=3, stride=1, pad=1, ho=ho, wo=wo, wt16=2, n=n,
                    in_mode=in_mode)
     return lib().stx_conv_gram_tiles(C.byref(p))
+
+
+def conv_gram_groups(cin, cout, ho, wo, n=1, in_mode=N.STX_IN_RAW):
+    """In-kernel group sums per image of the fused Gram with gram_cnt
+    (stx_conv_gram_groups: ceil(tiles / STX_GRAM_GROUP); 0: not fusable).  The slab then
+    holds n * (tiles + groups) * 4096 floats: the per-tile scratch, then the group sums
+    (conv2d(gram_part=slab, gram_cnt=counters); style_loss_from_parts on the sums)."""
+    p = ConvParams(cin=cin, cout=cout, ks=3, stride=1, pad=1, ho=ho, wo=wo, wt16=2, n=n,
+                   in_mode=in_mode)
+    return lib().stx_conv_gram_groups(C.byref(p))
 
 
 def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, dw=None,

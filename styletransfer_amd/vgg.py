@@ -119,13 +119,25 @@ class VGGFeatures:
             return 0
         return ops.conv_gram_tiles(cin, cout, ho, wo, n=n, in_mode=IN_MODES[l])
 
+    def gram_groups(self, l, ho, wo, n=1):
+        """In-kernel group sums per image of conv l's fused Gram (0: not grouped).  Off
+        unless STX_GRAM_GROUPED=1: the in-launch reduction (ticket counter + sc1 hand-off)
+        adds ~4.6 us to each producing conv, more than the smaller finalize saves (same-
+        process A/B: Gatys 512^2 695 -> 703 us, fast_st B8 4478 -> 4469 us)."""
+        if os.environ.get("STX_GRAM_GROUPED", "0") != "1" or not self.gram_tiles(l, ho, wo, n):
+            return 0
+        cout, cin = VGG_CONV_SHAPES[l]
+        return ops.conv_gram_groups(cin, cout, ho, wo, n=n, in_mode=IN_MODES[l])
+
     def forward(self, x, upto=5, outs=None, amax=None, pools=None, on_layer=None, grams=None):
         """[Z1..Z_upto] (pre-ReLU conv outputs).  amax: device [>=5] slots, zeroed by
         the caller; slot l+1 receives max|Z_l| (the next split conv's input scale);
         each slot is an amax group of N.STX_AMAX_SLOTS floats (slot(amax, k)).
         Where fuses_pool holds, conv l also writes P = maxpool(relu(Z_l)) (into
         pools[l] if given) and conv l+1 reads P directly.  grams[l] (if given and not
-        None): conv l writes its fused Gram partials there (gram_tiles)."""
+        None): conv l writes its fused Gram partials there (gram_tiles); a (slab,
+        counters) pair instead: the in-kernel group sums (gram_groups) after the per-tile
+        scratch."""
         zs, cur, pin = [], x, None
         for l in range(upto):
             cout, cin = VGG_CONV_SHAPES[l]
@@ -145,7 +157,10 @@ class VGGFeatures:
                     pools[l] = pin
                 kw["pool_out"] = pin
             if grams is not None and grams[l] is not None:
-                kw["gram_part"] = grams[l]
+                if isinstance(grams[l], tuple):
+                    kw["gram_part"], kw["gram_cnt"] = grams[l]
+                else:
+                    kw["gram_part"] = grams[l]
             cur = ops.conv2d(src, self.wt[l], cin, cout, 3, in_mode=mode, bias=self.b[l],
                              out=None if outs is None else outs[l], wt16=self.wt16[l], **kw)
             zs.append(cur)
@@ -238,9 +253,15 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     hs = [H, H, H // 2, H // 2, H // 4]
     for l in range(5):
         nt = feat.gram_tiles(l, hs[l], hs[l] * W // H, n=B) if split else 0
+        ng = feat.gram_groups(l, hs[l], hs[l] * W // H, n=B) if nt else 0
         if nt == 0:
             st.grams[l] = None
-        elif st.grams[l] is None or st.grams[l].numel() != B * nt * 4096:
+        elif ng:  # per-tile scratch + group sums, and the group arrival counters
+            if not isinstance(st.grams[l], tuple) or st.grams[l][0].numel() != B * (nt + ng) * 4096:
+                st.grams[l] = (torch.empty(B * (nt + ng) * 4096, device=dev, dtype=torch.float32),
+                               torch.zeros(B * ng, device=dev, dtype=torch.int32))
+        elif st.grams[l] is None or isinstance(st.grams[l], tuple) or \
+                st.grams[l].numel() != B * nt * 4096:
             st.grams[l] = torch.empty(B * nt * 4096, device=dev, dtype=torch.float32)
 
     fuse_content = os.environ.get("STX_CONTENT_FUSE", "1") != "0"
@@ -274,8 +295,12 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                     coef=st.coef[i], z_amax=slot(st.amax, l + 1), defer_ws=st.lws[i], fin=fin)
                 return
             if st.grams[l] is not None:
+                gp = st.grams[l]
+                if isinstance(gp, tuple):  # the group sums after the B * nt tile slots
+                    ng = gp[1].numel() // b_
+                    gp = gp[0][gp[0].numel() - b_ * ng * 4096:]
                 st.parts[i], st.coef[i] = ops.style_loss_from_parts(
-                    st.grams[l], st.grams[l].numel() // (b_ * 4096), b_, c_, z[0, 0].numel(),
+                    gp, gp.numel() // (b_ * 4096), b_, c_, z[0, 0].numel(),
                     targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
                     coef=st.coef[i], defer_ws=st.lws[i], fin=fin)
             else:

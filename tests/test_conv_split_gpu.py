@@ -332,6 +332,66 @@ def test_fused_gram_partials(dev, case):
     assert rel(a_f, a32) < 1e-5
 
 
+@pytest.mark.parametrize("case", [(1, 64, 512, 512, N.STX_IN_RELU, True),   # Gatys conv1_2
+                                  (8, 64, 256, 256, N.STX_IN_RELU, True),   # fast_st B8
+                                  (2, 64, 38, 72, N.STX_IN_RELU, False),    # 1 ragged group
+                                  (3, 64, 200, 260, N.STX_IN_RAW, True),    # 4 + 1 of 8 tiles
+                                  (1, 3, 512, 512, N.STX_IN_RAW, False),    # conv1_1 (convfew)
+                                  (2, 3, 30, 70, N.STX_IN_RAW, False)])
+def test_fused_gram_grouped(dev, case):
+    """In-launch group sums of the fused Gram partials (stx_conv_params.gram_cnt): the
+    last block of each group of STX_GRAM_GROUP tiles sums the group's partials (sc1
+    hand-off, ticket counter).  The group sums add up to the Gram (vs fp64), the conv
+    and pooled outputs equal the ungrouped launch bit for bit, the counters are zero
+    after every call, repeated calls give the same bits, and the style loss from the sums
+    equals the direct one."""
+    n, cin, h, w, mode, pool = case
+    cout, G = 64, N.STX_GRAM_GROUP
+    x = rnd(n, cin, h, w, dev=dev, seed=191, scale=2, shift=-1)
+    wgt = rnd(cout, cin, 3, 3, dev=dev, seed=192, scale=0.1, shift=-0.05)
+    bias = rnd(cout, dev=dev, seed=193, scale=0.2, shift=-0.1)
+    wt, w16 = ops.conv_weight_prep(wgt), ops.conv_weight_prep16(wgt)
+    nt = ops.conv_gram_tiles(cin, cout, h, w, n=n, in_mode=mode)
+    ng = ops.conv_gram_groups(cin, cout, h, w, n=n, in_mode=mode)
+    assert nt > 0 and ng == -(-nt // G), (nt, ng)
+    slab = torch.full((n * (nt + ng) * 4096,), float("nan"), device=dev)
+    cnt = torch.zeros(n * ng, device=dev, dtype=torch.int32)
+
+    def run(kw_gram):
+        kw = dict(kw_gram)
+        if pool:
+            kw["pool_out"] = torch.empty(n, cout, h // 2, w // 2, device=dev)
+        y = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=bias, wt16=w16, **kw)
+        return y, kw.get("pool_out")
+
+    y, p1 = run(dict(gram_part=slab, gram_cnt=cnt))
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
+    sums = slab[n * nt * 4096:].clone()
+    y2, p2 = run({})
+    assert torch.equal(y, y2)
+    if pool:
+        assert torch.equal(p1, p2)
+    assert torch.isfinite(sums).all()
+    g = sums.view(n, ng, 64, 64).double().sum(1).cpu() / (cout * h * w)
+    f = y.double().cpu().reshape(n, cout, h * w)
+    ref = torch.bmm(f, f.transpose(1, 2)) / (cout * h * w)
+    assert rel(g, ref) < TOL64, rel(g, ref)
+    for _ in range(3):  # the counters rearm: same bits on every call
+        run(dict(gram_part=slab, gram_cnt=cnt))
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
+    assert torch.equal(slab[n * nt * 4096:], sums)
+    t = rnd(cout, cout, dev=dev, seed=194, scale=0.02)
+    ws = torch.empty(N.lib().stx_gram_ws(n, cout, h * w), device=dev, dtype=torch.uint8)
+    lp, a_f = ops.style_loss_from_parts(sums, ng, n, cout, h * w, t, weight=3.0, defer_ws=ws)
+    lf = torch.zeros(1, device=dev)
+    ops.loss_finalize([lp], lf)
+    l32, a32 = ops.style_loss(y, t, weight=3.0)
+    assert rel(lf[0], l32) < 1e-5
+    assert rel(a_f, a32) < 1e-5
+
+
 @pytest.mark.parametrize("shape", [(1, 128, 256, 256), (2, 128, 24, 40), (1, 64, 32, 32),
                                    (1, 256, 16, 16), (3, 128, 8, 12)])
 def test_style_content_loss(dev, shape):
