@@ -398,19 +398,45 @@ def video_leg(args, world, rank, dev):
                 pcie=out["pcie"], conditioned=out["conditioned"], frame_hw=(FH, FW))
 
 
+def itn_forward_gflop(h, w):
+    """ImageTransformNet forward FLOPs per image (2*MAC; stransfer/network.py:520-611):
+    conv 3->32 9x9, 32->64 and 64->128 3x3 stride 2, 5 residual blocks of two 128->128 3x3
+    convs at h/4, nearest x2 + 128->64 and x2 + 64->32 3x3, 32->3 9x9."""
+    c = lambda ci, co, k, oh, ow: 2.0 * ci * co * k * k * oh * ow
+    return (c(3, 32, 9, h, w) + c(32, 64, 3, h // 2, w // 2) + c(64, 128, 3, h // 4, w // 4)
+            + 10 * c(128, 128, 3, h // 4, w // 4) + c(128, 64, 3, h // 2, w // 2)
+            + c(64, 32, 3, h, w) + c(32, 3, 9, h, w)) / 1e9
+
+
 def convert_leg(args, world, rank, dev):
-    """BASELINE config 3: fast_st convert-image, batch 32 at 256^2 (ITN forward)."""
+    """BASELINE config 3: fast_st convert-image, batch 32 at 256^2 (ITN forward), as one
+    hipGraph replay per batch (eager launches timed beside it)."""
     from styletransfer_amd import network
     B, H = 32, 256
     itn = network.ImageTransformNet(torch.rand([3, H, H]), batch_size=B).to(dev)
     itn.load_state_dict({k: torch.from_numpy(v) for k, v in W.itn_synthetic(4321)})
     x = torch.from_numpy(W.synthetic_image(6000 + rank, (B, 3, H, H))).to(dev)
+    n = max(3, args.steps // 5)
     with torch.no_grad():
         for _ in range(2):
             itn(x)
-        n = max(3, args.steps // 5)
-        dt = timed(lambda: itn(x), n, world, dev)
-    return dict(rate=world * B * n / dt, dt=dt, steps=n, batch=B)
+        dt_eager = timed(lambda: itn(x), n, world, dev)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            itn(x)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            y = itn(x)
+        g.replay()
+        dt = timed(g.replay, n, world, dev)
+        ref = itn(x)
+        torch.cuda.synchronize(dev)
+        same = bool(torch.equal(y, ref))
+    gf = itn_forward_gflop(H, H) * B
+    return dict(rate=world * B * n / dt, dt=dt, steps=n, batch=B, eager_rate=world * B * n / dt_eager,
+                gflop=gf, tflops=gf * n / dt / 1e3, graph_equals_eager=same)
 
 
 def _host_cpu():
@@ -728,8 +754,14 @@ def main():
             res["fast_st_convert"] = {
                 "value": round(conv["rate"], 2), "unit": "images/s", "batch": conv["batch"],
                 "ms_per_batch": round(1e3 * conv["dt"] / conv["steps"], 3),
-                "steps": conv["steps"], "note": "BASELINE config 3: ImageTransformNet "
-                "forward, batch 32 at 256x256, eager"}
+                "steps": conv["steps"], "eager_value": round(conv["eager_rate"], 2),
+                "gflop_per_batch": round(conv["gflop"], 2),
+                "tflops": round(conv["tflops"], 1),
+                "split_peak_frac": round(conv["tflops"] / PEAK_SPLIT_TFLOPS, 4),
+                "graph_equals_eager": conv["graph_equals_eager"],
+                "note": "BASELINE config 3: ImageTransformNet forward, batch 32 at 256x256, "
+                        "one hipGraph replay per batch (eager_value: the same launches issued "
+                        "eagerly); FLOPs 2*MAC of the convs, fraction of the 833 TF split peak"}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

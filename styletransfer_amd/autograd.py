@@ -173,13 +173,15 @@ class Conv2dFn(torch.autograd.Function):
             else:
                 raise NotImplementedError("in_mode backward")
         if ctx.needs_input_grad[1]:
+            # into the trainer's flat gradient: on the weight-gradient side stream
+            # (ops.SIDE, active inside a training step) next to the data gradients
             dw = _grad_into(w, lambda: ops.conv2d_wgrad(
                 x, dy, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
                 x_amax=ctx.x_amax, dy_amax=dy_amax),
-                lambda dst: ops.conv2d_wgrad(x, dy, cin, cout, ks, stride=stride, pad=pad,
-                                             in_mode=in_mode, dw=dst.view(w.shape),
-                                             accumulate=True, x_amax=ctx.x_amax,
-                                             dy_amax=dy_amax))
+                lambda dst: ops.SIDE.run(lambda: ops.conv2d_wgrad(
+                    x, dy, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
+                    dw=dst.view(w.shape), accumulate=True, x_amax=ctx.x_amax,
+                    dy_amax=dy_amax), x, dy, ctx.x_amax, dy_amax))
         if has_b and ctx.needs_input_grad[2]:
             b = ctx.b_ref
             db = _grad_into(b, lambda: ops.bias_grad(dy),

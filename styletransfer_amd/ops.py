@@ -73,6 +73,61 @@ class _Workspace:
 
 
 WS = _Workspace()
+WS_SIDE = _Workspace()  # the weight-gradient side stream's own scratch (SideStream)
+
+
+class SideStream:
+    """Weight gradients off the data-gradient chain.  In a training step's backward
+    (train.FastStTrainer / VideoTrainer between begin() and end()) every conv's dW --
+    which nothing in the backward reads -- runs on a side stream that waits for the
+    work issued so far (dy is ready), while the data gradients continue on the main
+    stream; end() joins the side stream back before the gradient exchange / Adam.  The
+    small B=8 grids of the ImageTransformNet (2 blocks per CU) leave room for a
+    concurrent kernel.  The side work has its own scratch (WS_SIDE) and keeps its
+    inputs referenced until the join (no cross-stream reuse of their memory, eager or
+    captured).  STX_WGRAD_SIDE=0 runs everything on the main stream."""
+
+    def __init__(self):
+        self.active = False
+        self.streams = {}
+        self.stream = None
+        self.keep = []
+
+    def begin(self, device):
+        import os
+        if os.environ.get("STX_WGRAD_SIDE", "1") == "0":
+            return
+        key = torch.device(device).index or 0
+        if key not in self.streams:
+            self.streams[key] = torch.cuda.Stream(device)
+        self.stream = self.streams[key]
+        self.active = True
+        self.keep = []
+
+    def on_side(self):
+        return self.active and torch.cuda.current_stream() == self.stream
+
+    def run(self, fn, *keep):
+        if not self.active:
+            return fn()
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            r = fn()
+        self.keep.extend(t for t in keep if t is not None)
+        return r
+
+    def end(self):
+        if self.active:
+            torch.cuda.current_stream().wait_stream(self.stream)
+            self.keep = []
+            self.active = False
+
+
+SIDE = SideStream()
+
+
+def _scratch():
+    return WS_SIDE if SIDE.on_side() else WS
 
 
 class AmaxArena:
@@ -465,7 +520,7 @@ def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW,
         if need9 and ho == h and wo == w:
             xa = x_amax if x_amax is not None else amax(x)
             da = dy_amax if dy_amax is not None else amax(dy)
-            wp, wn = WS.get(need9, x.device)
+            wp, wn = _scratch().get(need9, x.device)
             check(L.stx_conv2d_wgrad_few16(x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
                                            int(accumulate), n, cin, h, w, cout, ks, pad,
                                            xa.data_ptr(), da.data_ptr(), wp, wn, _stream()),
@@ -477,7 +532,7 @@ def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW,
             _req(dy, "dy")
             xa = x_amax if x_amax is not None else amax(x)
             da = dy_amax if dy_amax is not None else amax(dy)
-            wp, wn = WS.get(need16, x.device)
+            wp, wn = _scratch().get(need16, x.device)
             check(L.stx_conv2d_wgrad16(x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
                                        int(accumulate), n, cin, h, w, cout, in_mode, ho, wo,
                                        xa.data_ptr(), da.data_ptr(), wp, wn, _stream()),
@@ -490,14 +545,14 @@ def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW,
         if need16:
             xa = x_amax if x_amax is not None else amax(x)
             da = dy_amax if dy_amax is not None else amax(dy)
-            wp, wn = WS.get(need16, x.device)
+            wp, wn = _scratch().get(need16, x.device)
             check(L.stx_conv2d_wgrad16_s2(x.data_ptr(), dy.data_ptr(), dw.data_ptr(),
                                           int(accumulate), n, cin, h, w, cout, ho, wo,
                                           xa.data_ptr(), da.data_ptr(), wp, wn, _stream()),
                   "stx_conv2d_wgrad16_s2")
             return dw
     need = L.stx_conv2d_wgrad_ws(n, cin, cout, ks, stride, ho, wo)
-    wp, wn = WS.get(need, x.device)
+    wp, wn = _scratch().get(need, x.device)
     check(L.stx_conv2d_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), int(accumulate), n, cin,
                              h, w, cout, ks, stride, pad, in_mode, hv, wv, ho, wo, wp, wn,
                              _stream()), "stx_conv2d_wgrad")

@@ -112,12 +112,14 @@ class FastStTrainer:
         self.slabs.prep()
         ops.ARENA.begin(self.device)  # InstanceNorm outputs carry their max|.| to the convs
         ops.PGRADS.begin()            # one launch for all InstanceNorm parameter gradients
+        ops.SIDE.begin(self.device)   # weight gradients on a side stream
         try:
             y = self.itn(batch)
             total = self._total(batch, y)
             total.backward()
             ops.PGRADS.flush()
         finally:
+            ops.SIDE.end()
             ops.PGRADS.active = False
             ops.ARENA.end()
         return total.detach()
@@ -257,12 +259,14 @@ class VideoTrainer(FastStTrainer):
         self.slabs.prep()
         ops.ARENA.begin(self.device)
         ops.PGRADS.begin()
+        ops.SIDE.begin(self.device)
         try:
             y = self.itn(x6)
             total = self._video_total(batch, y, old_c, old_s)
             total.backward()
             ops.PGRADS.flush()
         finally:
+            ops.SIDE.end()
             ops.PGRADS.active = False
             ops.ARENA.end()
         self.old = (batch, y.detach())
