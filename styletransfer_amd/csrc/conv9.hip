@@ -104,9 +104,7 @@ struct In3 {
   static constexpr int LDS_A = 9 * 2 * 2 * 2 * 32 * 16; // [kw][s][P][h][co]
 };
 
-// DBG (profiling only, STX_CONV9_DBG): bit 0 skips the epilogue stores, bit 1 the MFMAs,
-// bit 2 the next tile's input loads
-template <int DBG = 0, int W = NWV>
+template <int W = NWV>
 __global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_params p, int tiles_x,
                                                                   int tiles_y) {
   using C = In3<W>;
@@ -145,7 +143,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_param
     }
   };
   int tile = first_tile();
-  if (!(DBG & 16) && tile < ntiles) load_b(tile);
+  if (tile < ntiles) load_b(tile);
 
   // weights, once: unit u = tid + NT k -> co = u % 32, h = (u / 32) % 2, s = (u / 64) % 2,
   // kw = u / 128; element e is pair q = 16 s + 8 h + e of W[co][ci][kh][kw]
@@ -183,11 +181,6 @@ __global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_param
     }
     __syncthreads();  // red[] is reused by the first tile's window max
   }
-  if (DBG & 8) {  // profiling: the prologue alone
-    if (bv[0][0] == 1234.5f && threadIdx.x == 0) p.y[0] = 0.f;
-    return;
-  }
-
   const size_t plane = (size_t)p.ho * p.wo;
   const uint32_t pb = (uint32_t)plane * 4u;
   float bias_r[16];
@@ -223,7 +216,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_param
     }
     __syncthreads();
     const int cur = tile;
-    if (!(DBG & 4) && tile + (int)gridDim.x < ntiles) load_b(tile + gridDim.x);  // in flight during the MFMAs
+    if (tile + (int)gridDim.x < ntiles) load_b(tile + gridDim.x);  // in flight during the MFMAs
 
     f32x16 acc[2];
 #pragma unroll
@@ -231,7 +224,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_param
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 #pragma unroll
-    for (int kw = 0; kw < ((DBG & 2) ? 1 : 9); ++kw)
+    for (int kw = 0; kw < 9; ++kw)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int base = ((kw * 2 + s) * 2) * 2;
@@ -266,7 +259,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_param
         // leaves the compiler unsure how many are pending, so the next tile's wait for
         // its prefetched loads becomes a wait for every store too)
         const bool ok = row_c + 4 * h < p.cout;
-        if constexpr (!(DBG & 1)) buf_st(ry, ok ? vo + (uint32_t)row_c * pb : BUF_OOB, v);
+        buf_st(ry, ok ? vo + (uint32_t)row_c * pb : BUF_OOB, v);
         vmax_u = max(vmax_u, (in && ok) ? (__float_as_uint(v) & 0x7fffffffu) : 0u);
       }
     }
@@ -292,7 +285,12 @@ static_assert(NB_ITEMS % NT == 0, "halo units per thread");
 static_assert(NWV * 27 * PST * 4 <= LDS_B, "P rows fit in the halo region");
 }  // namespace out3
 
-template <int DBG = 0>
+// The block walks steps s = (its tile i, chunk c) = (s / NCH, s % NCH); the halo loads of
+// step s + 2 are issued right after step s is staged (two register sets: a load has two
+// steps of MFMAs to land instead of one), unconditionally -- a step past the block's
+// last tile loads through an empty descriptor and stores out of range -- so the wait
+// before a set's staging covers exactly the older set's loads.
+template <int NCH>
 __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, int tiles_x,
                                                            int tiles_y) {
   using namespace out3;
@@ -304,7 +302,6 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
   const int tiles_img = tiles_x * tiles_y, ntiles = tiles_img * p.n;
   const int plane_in = p.h * p.w;
   const bool relu_in = p.in_mode == STX_IN_RELU;
-  const int nch = cdiv(p.cin, 16);  // 1 or 2
 
   // halo unit i = tid + NT k -> channel group cg = i / NPOS, position (row, col)
   uint32_t hpos[NB_R];
@@ -315,11 +312,18 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
     const int rr = pos / TWI, cc = pos - rr * TWI;
     hpos[k] = (uint32_t)(cg << 20 | rr << 10 | cc);
   }
-  float hv[NB_R][8];
-  auto load_h = [&](int tile, int c) {
+  const int tile0 = first_tile();
+  const int mine = tile0 < ntiles ? cdiv(ntiles - tile0, (int)gridDim.x) : 0;
+  const int nsteps = rup(mine * NCH, 2);  // whole pairs of steps (a padded step is inert)
+  float hv[2][NB_R][8];
+  auto load_h = [&](float (&hs)[NB_R][8], int step) {
+    const int it = step / NCH, c = step - it * NCH;
+    const int tile = tile0 + it * (int)gridDim.x;
+    const bool valid = it < mine;
     const int n = tile / tiles_img, t = tile - n * tiles_img;
     const int oy0 = (t / tiles_x) * TH, ox0 = (t % tiles_x) * TWO;
-    const auto rx = make_srd(p.x + (size_t)n * p.cin * plane_in, (uint32_t)(p.cin * plane_in) * 4u);
+    const auto rx = make_srd(p.x + (size_t)(valid ? n : 0) * p.cin * plane_in,
+                             valid ? (uint32_t)(p.cin * plane_in) * 4u : 0u);
 #pragma unroll
     for (int k = 0; k < NB_R; ++k) {
       const int cg = hpos[k] >> 20, rr = (hpos[k] >> 10) & 1023, cc = hpos[k] & 1023;
@@ -328,11 +332,11 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
       const uint32_t o = (uint32_t)(ch * plane_in + y * p.w + x) * 4u;
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        hv[k][e] = buf_ld(rx, (ok && ch + e < p.cin) ? o + (uint32_t)(e * plane_in) * 4u : BUF_OOB);
+        hs[k][e] = buf_ld(rx, (ok && ch + e < p.cin) ? o + (uint32_t)(e * plane_in) * 4u : BUF_OOB);
     }
   };
-  int tile = first_tile();
-  if (!(DBG & 16) && tile < ntiles) load_h(tile, 0);
+  load_h(hv[0], 0);
+  load_h(hv[1], 1);
 
   // weights of every chunk, once: unit u = tid + NT k -> chunk c = u / NA_ITEMS, (kh, h, m):
   // m = co * 9 + kw, element e = channel 16 c + 8 h + e: W[co][ci][kh][kw] = wt[(ci*81 + kh*9 + kw)][co]
@@ -350,7 +354,7 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int ci = 16 * c + 8 * hh + e;
-        const bool ok = c < nch && co < p.cout && ci < p.cin;
+        const bool ok = c < NCH && co < p.cout && ci < p.cin;
         const float w = p.wt[(size_t)(ok ? ci * 81 + kh * 9 + kw : 0) * p.cout_pad + (ok ? co : 0)];
         wv[k][e] = ok ? w : 0.f;
         mw = fmaxf(mw, fabsf(wv[k][e]));
@@ -373,55 +377,48 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
     }
   }
 
-  if (DBG & 8) {  // profiling: the prologue alone
-    __syncthreads();
-    if (hv[0][0] == 1234.5f && threadIdx.x == 0) p.y[0] = 0.f;
-    return;
-  }
   const size_t plane = (size_t)p.ho * p.wo;
   uint32_t vmax_u = 0u;
   const char* bb = lb + (wave * TWI + l32) * 16;  // (row wave + kh, column 32 j + l32)
   float* pw = reinterpret_cast<float*>(smem) + wave * 27 * PST;
-  for (; tile < ntiles; tile += gridDim.x) {
-    f32x16 acc[2];
+  f32x16 acc[2];
+  auto step = [&](float (&hs)[NB_R][8], int s, int c) {
+    if (c == 0) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-    for (int c = 0; c < nch; ++c) {
-      __syncthreads();  // the previous chunk's operand reads / P reads are done
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    }
+    __syncthreads();  // the previous step's operand reads / P reads are done
 #pragma unroll
-      for (int k = 0; k < NB_R; ++k) {
-        if (relu_in)
+    for (int k = 0; k < NB_R; ++k) {
+      if (relu_in)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) hv[k][e] = fmaxf(hv[k][e], 0.f);
-        f16x8 hi, lo;
-        split8(hv[k], sx, hi, lo);
-        const int i = tid + NT * k;
-        *reinterpret_cast<f16x8*>(lb + i * 16) = hi;
-        *reinterpret_cast<f16x8*>(lb + (NB_ITEMS + i) * 16) = lo;
-      }
-      __syncthreads();
-      // the next chunk (or the next tile's first) in flight during the MFMAs
-      if (DBG & 4) {
-      } else if (c + 1 < nch) load_h(tile, c + 1);
-      else if (tile + (int)gridDim.x < ntiles) load_h(tile + gridDim.x, 0);
-      const char* ac = la + c * 9 * 2 * 2 * 32 * 16;
+        for (int e = 0; e < 8; ++e) hs[k][e] = fmaxf(hs[k][e], 0.f);
+      f16x8 hi, lo;
+      split8(hs[k], sx, hi, lo);
+      const int i = tid + NT * k;
+      *reinterpret_cast<f16x8*>(lb + i * 16) = hi;
+      *reinterpret_cast<f16x8*>(lb + (NB_ITEMS + i) * 16) = lo;
+    }
+    __syncthreads();
+    load_h(hs, s + 2);  // in flight during this step's and the next step's MFMAs
+    const char* ac = la + c * 9 * 2 * 2 * 32 * 16;
 #pragma unroll
-      for (int kh = 0; kh < ((DBG & 2) ? 1 : 9); ++kh) {
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(ac + (((kh * 2 + 0) * 2 + h) * 32 + l32) * 16);
-        const f16x8 al = *reinterpret_cast<const f16x8*>(ac + (((kh * 2 + 1) * 2 + h) * 32 + l32) * 16);
+    for (int kh = 0; kh < 9; ++kh) {
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(ac + (((kh * 2 + 0) * 2 + h) * 32 + l32) * 16);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(ac + (((kh * 2 + 1) * 2 + h) * 32 + l32) * 16);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int off = ((h * NPOS) + kh * TWI + 32 * j) * 16;
-          const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + off);
-          const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + NB_ITEMS * 16 + off);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
-        }
+      for (int j = 0; j < 2; ++j) {
+        const int off = ((h * NPOS) + kh * TWI + 32 * j) * 16;
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(bb + off);
+        const f16x8 bl = *reinterpret_cast<const f16x8*>(bb + NB_ITEMS * 16 + off);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
       }
     }
+    if (c != NCH - 1) return;
     // P[(co, kw)][column] of this wave's row into LDS (rows < 27), then
     // y[co][x] = sum_kw P[co*9 + kw][x + kw]
     __syncthreads();  // every wave's halo reads are done
@@ -433,27 +430,35 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
         if (m < 27) pw[m * PST + 32 * j + l32] = acc[j][r] * descale;
       }
     __syncthreads();
-    const int n = tile / tiles_img, t = tile - n * tiles_img;
+    const int it = s / NCH;
+    const int tile = tile0 + it * (int)gridDim.x;
+    const bool tok = it < mine;
+    const int n = tok ? tile / tiles_img : 0, t = tile - n * tiles_img;
     const int oy = (t / tiles_x) * TH + wave, ox0 = (t % tiles_x) * TWO;
     // branch-free stores through a descriptor (see conv9_in3's epilogue): 3 x 64 lanes
-    // cover the 3 x 56 outputs, the rest store out of range
-    const auto ry = make_srd(p.y + (size_t)n * p.cout * plane, (uint32_t)(p.cout * plane) * 4u);
+    // cover the 3 x 56 outputs, the rest (and a padded step) store out of range
+    const auto ry = make_srd(p.y + (size_t)n * p.cout * plane,
+                             tok ? (uint32_t)(p.cout * plane) * 4u : 0u);
 #pragma unroll
-    for (int it = 0; it < 3; ++it) {
-      const int idx = lane + 64 * it;
+    for (int r3 = 0; r3 < 3; ++r3) {
+      const int idx = lane + 64 * r3;
       const int co = idx / TWO, x = idx - co * TWO, coc = min(co, p.cout - 1);
       float v = 0.f;
 #pragma unroll
       for (int kw = 0; kw < 9; ++kw) v += pw[(coc * 9 + kw) * PST + x + kw];
       const int ox = ox0 + x;
-      const bool ok = co < p.cout && oy < p.ho && ox < p.wo;
+      const bool ok = tok && co < p.cout && oy < p.ho && ox < p.wo;
       const uint32_t o = ok ? (uint32_t)((size_t)co * plane + (size_t)oy * p.wo + ox) * 4u : BUF_OOB;
       if (p.bias) v += p.bias[coc];
       if (p.accumulate) v += buf_ld(ry, o);
       if (p.relu_out) v = fmaxf(v, 0.f);
-      if constexpr (!(DBG & 1)) buf_st(ry, o, v);
+      buf_st(ry, o, v);
       vmax_u = max(vmax_u, ok ? (__float_as_uint(v) & 0x7fffffffu) : 0u);
     }
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(hv[0], s, NCH == 2 ? 0 : 0);
+    step(hv[1], s + 1, NCH == 2 ? 1 : 0);
   }
   if (p.out_amax) block_amax_out(p.out_amax, vmax_u, red);
 }
@@ -466,8 +471,6 @@ bool conv9_on() {
   return on;
 }
 
-#define CONV9_LAUNCH(KERN, grid, st, p, tx, ty) \
-  hipLaunchKernelGGL(KERN<0>, grid, dim3(NT), 0, st, p, tx, ty)
 
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -500,12 +503,17 @@ int conv2d_conv9(const stx_conv_params& p, hipStream_t st) {
   if (p.cin == 3 && p.cout >= 1 && p.cout <= 32 && !p.accumulate) {
     // (4-wave blocks, two per CU, measured the same: 58.5 vs 58.2 us at B8 256^2)
     const int tx = cdiv(p.wo, In3<8>::TW), ty = cdiv(p.ho, In3<8>::TH);
-    CONV9_LAUNCH(conv9_in3_kernel, dim3(persistent_grid(tx * ty * p.n, 1)), st, p, tx, ty);
+    hipLaunchKernelGGL(conv9_in3_kernel<>, dim3(persistent_grid(tx * ty * p.n, 1)), dim3(NT), 0,
+                       st, p, tx, ty);
     return check_launch("stx_conv2d(conv9 3->32)");
   }
   if (p.cout >= 1 && p.cout <= 3 && p.cin >= 1 && p.cin <= 32 && p.in_amax) {
     const int tx = cdiv(p.wo, out3::TWO), ty = cdiv(p.ho, out3::TH);
-    CONV9_LAUNCH(conv9_out3_kernel, dim3(persistent_grid(tx * ty * p.n, 1)), st, p, tx, ty);
+    const dim3 grid(persistent_grid(tx * ty * p.n, 1));
+    if (p.cin > 16)
+      hipLaunchKernelGGL(conv9_out3_kernel<2>, grid, dim3(NT), 0, st, p, tx, ty);
+    else
+      hipLaunchKernelGGL(conv9_out3_kernel<1>, grid, dim3(NT), 0, st, p, tx, ty);
     return check_launch("stx_conv2d(conv9 32->3)");
   }
   return -1;
