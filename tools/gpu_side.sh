@@ -2,7 +2,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 tag=${1:-side}
-timeout -k 10 500 python -u -m pytest tests/test_conv9_gpu.py tests/test_itn_masks_gpu.py tests/test_dp_gpu.py tests/test_video_gpu.py tests/test_parity_gpu.py tests/test_workflows_gpu.py -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/${tag}_t.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_side_stream_gpu.py tests/test_conv9_gpu.py tests/test_itn_masks_gpu.py tests/test_dp_gpu.py tests/test_video_gpu.py tests/test_parity_gpu.py tests/test_workflows_gpu.py -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/${tag}_t.log 2>&1
 rc=$?; tail -2 gpurun_out/${tag}_t.log; grep -E "^(FAILED|ERROR)|^E  " gpurun_out/${tag}_t.log | head -20
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python tools/ab_engine.py "STX_WGRAD_SIDE=0" "STX_WGRAD_SIDE=1" --rounds 7 --no-gatys > gpurun_out/${tag}_ab.log 2>&1; tail -3 gpurun_out/${tag}_ab.log
