@@ -85,7 +85,7 @@ class SideStream:
     small B=8 grids of the ImageTransformNet (2 blocks per CU) leave room for a
     concurrent kernel.  The side work has its own scratch (WS_SIDE) and keeps its
     inputs referenced until the join (no cross-stream reuse of their memory, eager or
-    captured).  STX_WGRAD_SIDE=0 runs everything on the main stream."""
+    captured).  Opt-in (STX_WGRAD_SIDE=1) until measured."""
 
     def __init__(self):
         self.active = False
@@ -95,7 +95,7 @@ class SideStream:
 
     def begin(self, device):
         import os
-        if os.environ.get("STX_WGRAD_SIDE", "1") == "0":
+        if os.environ.get("STX_WGRAD_SIDE", "0") != "1":
             return
         key = torch.device(device).index or 0
         if key not in self.streams:

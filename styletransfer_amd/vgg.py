@@ -267,8 +267,9 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     fuse_content = os.environ.get("STX_CONTENT_FUSE", "1") != "0"
     # the five taps' Gram finalizes in one launch after the forward (STX_FIN_BATCH=0: one
     # finalize launch per tap, right after its partials)
-    fin = ops.FinalizeBatch() if (os.environ.get("STX_FIN_BATCH", "1") != "0" and not overlap) \
-        else None
+    # (with the loss stream the jobs are recorded on the side stream's calls and the one
+    # finalize launch runs on main after the join)
+    fin = ops.FinalizeBatch() if os.environ.get("STX_FIN_BATCH", "1") != "0" else None
 
     def on_layer(l, z):
         # the style loss of layer l (and the content/feature losses at conv2_2) run on

@@ -7,3 +7,4 @@ rc=$?; tail -2 gpurun_out/${tag}_t.log; grep -E "^(FAILED|ERROR)|^E  " gpurun_ou
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python tools/ab_engine.py "STX_WGRAD_SIDE=0" "STX_WGRAD_SIDE=1" --rounds 7 --no-gatys > gpurun_out/${tag}_ab.log 2>&1; tail -3 gpurun_out/${tag}_ab.log
 timeout -k 10 120 python tools/bench_conv9.py > gpurun_out/${tag}_c9.log 2>&1; tail -5 gpurun_out/${tag}_c9.log
+timeout -k 10 400 python tools/ab_engine.py "STX_LOSS_STREAM=0" "STX_LOSS_STREAM=1" --rounds 7 > gpurun_out/${tag}_ls.log 2>&1; tail -4 gpurun_out/${tag}_ls.log
