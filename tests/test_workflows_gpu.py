@@ -213,6 +213,10 @@ def test_fast_st_cli_train_then_convert(dev, project_root):
     with torch.no_grad():
         want = np.asarray(img_utils.to_pil(itn(x)))
     diff = np.abs(got.astype(np.int32) - want.astype(np.int32))
+    # the reference's byte conversion clamps to [0, 255] before * 255 (img_utils.imshow,
+    # stransfer/img_utils.py:104-110), so values just above 1 wrap modulo 256: a one-unit
+    # rounding difference there reads as 255 -- compare on the byte circle
+    diff = np.minimum(diff, 256 - diff)
     print(f"convert-image vs oracle: max |diff| {diff.max()}, > 0: {(diff > 0).mean():.2e}")
     assert diff.max() <= 1 and (diff > 0).mean() < 1e-2
 
