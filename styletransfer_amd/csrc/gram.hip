@@ -579,64 +579,55 @@ static bool gram_tri_on(int c, int hw) {
 // result is bit-reproducible.  (16-element x 16-lane blocks reading 64-B segments
 // left the reduction latency-bound: 11.8 us for the 16.8 MB of C=64 @ 512^2 partials.)
 constexpr int FEL = 64, FKL = 64, FNT = FEL / 4 * FKL;  // elements, split-lanes, threads
-constexpr int FSUB = GT * GT / FEL;   // blocks per tile
-// block (bx, by) of a finalize over grid (ntu * FSUB, b)
-__device__ __forceinline__ void gram_finalize_body(
+constexpr int FSUB = GT * GT / FEL;   // 64-element sub-tiles per tile (loss partials)
+// Few partials per tile (the 128 / 256-channel taps at small HW and large batch: a handful
+// of splits) would leave most of a block's 64 split-lanes idle and pay the 64-deep LDS
+// sum per element anyway, in thousands of blocks: such a block takes G = 2 or 4 sub-tiles
+// with 64 / G split-lanes each (G from nsplit, so every caller of a tap picks the same
+// order and the same bits).
+__host__ __device__ inline int fin_groups(int nsplit) { return nsplit <= 16 ? 4 : nsplit <= 32 ? 2 : 1; }
+__host__ __device__ inline int fin_blocks_per_tile(int nsplit) { return FSUB / fin_groups(nsplit); }
+
+// block (bx, by) of a finalize over grid (ntu * fin_blocks_per_tile(nsplit), b)
+template <int G>
+__device__ __forceinline__ void gram_finalize_body_g(
     const float* __restrict__ ws, int c, int nsplit, float scale, float* __restrict__ g_out,
     const float* __restrict__ target, long long t_bstride, float* __restrict__ coef, int cpad,
-    float cA, float alpha, float* __restrict__ loss_parts, const float* __restrict__ mse_parts,
-    int mse_nparts, double mse_n, float* __restrict__ mse_out, int bx, int by) {
-  __shared__ float part[FKL][FEL + 1];
-  __shared__ float red[FNT / 64];
-  // block (0, 0) also finalizes the content / feature MSE partials of a fused content
-  // pass (gram_tri_f16_kernel<128, true>): the launch a separate mse2 finalize would take
-  if (mse_out && bx == 0 && by == 0) {
-    float s = 0.f, sr = 0.f;
-    for (int i = threadIdx.x; i < mse_nparts; i += FNT) {
-      s += mse_parts[2 * i];
-      sr += mse_parts[2 * i + 1];
-    }
-    s = block_sum<FNT>(s, red);
-    sr = block_sum<FNT>(sr, red);
-    if (threadIdx.x == 0) {
-      const float mr = (float)(sr / mse_n);
-      mse_out[0] = (float)(s / mse_n);
-      mse_out[1] = (float)((double)(mr * mr) / mse_n);
-      mse_out[2] = mr;
-    }
-  }
+    float cA, float alpha, float* __restrict__ loss_parts, int bx, int by, float* part) {
+  constexpr int KL = FKL / G, GT_ = FNT / G;  // split-lanes and threads per sub-tile
   const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
-  const int tile = bx / FSUB, sub = bx % FSUB;
+  const int tile = bx / (FSUB / G), r = threadIdx.x / GT_, sub = (bx % (FSUB / G)) * G + r;
   int I, J;
   tile_ij(tile, nt, I, J);
   const int b = by;
   const float* src = ws + ((size_t)b * ntu + tile) * nsplit * (GT * GT) + sub * FEL;
-  const int q4 = threadIdx.x % (FEL / 4), kl = threadIdx.x / (FEL / 4);
+  const int t2 = threadIdx.x % GT_, q4 = t2 % (FEL / 4), kl = t2 / (FEL / 4);
+  float* pr = part + (size_t)r * KL * (FEL + 1);  // this sub-tile's [KL][FEL + 1]
   {
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
     const f32x4* p4 = reinterpret_cast<const f32x4*>(src) + q4;
     constexpr int ST = GT * GT / 4;  // float4s per partial
     int k = kl;
-    for (; k + 3 * FKL < nsplit; k += 4 * FKL) {
-      const f32x4 a0 = p4[(size_t)(k + 0 * FKL) * ST], a1 = p4[(size_t)(k + 1 * FKL) * ST];
-      const f32x4 a2 = p4[(size_t)(k + 2 * FKL) * ST], a3 = p4[(size_t)(k + 3 * FKL) * ST];
+    for (; k + 3 * KL < nsplit; k += 4 * KL) {
+      const f32x4 a0 = p4[(size_t)(k + 0 * KL) * ST], a1 = p4[(size_t)(k + 1 * KL) * ST];
+      const f32x4 a2 = p4[(size_t)(k + 2 * KL) * ST], a3 = p4[(size_t)(k + 3 * KL) * ST];
       s0 += a0;
       s1 += a1;
       s2 += a2;
       s3 += a3;
     }
-    for (; k < nsplit; k += FKL) s0 += p4[(size_t)k * ST];
+    for (; k < nsplit; k += KL) s0 += p4[(size_t)k * ST];
     const f32x4 t = (s0 + s1) + (s2 + s3);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) part[kl][4 * q4 + i] = t[i];
+    for (int i = 0; i < 4; ++i) pr[kl * (FEL + 1) + 4 * q4 + i] = t[i];
   }
   __syncthreads();
   float sq = 0.f;
-  if (threadIdx.x < FEL) {
-    const int el = threadIdx.x, e = sub * FEL + el;
+  if (t2 < FEL) {  // one wave per sub-tile
+    const int el = t2, e = sub * FEL + el;
     float s = 0.f;
 #pragma unroll 8
-    for (int q = 0; q < FKL; ++q) s += part[q][el];
+    for (int q = 0; q < KL; ++q) s += pr[q * (FEL + 1) + el];
     const int gi = I * GT + e / GT, gj = J * GT + e % GT;
     if (gi < c && gj < c) {
       const float g = s * scale;
@@ -655,10 +646,49 @@ __device__ __forceinline__ void gram_finalize_body(
         }
       }
     }
+    if (target) {  // the sub-tile's loss partial: its one wave's sum
+      const float t = wave_sum(sq);
+      if (t2 == 0) loss_parts[(size_t)b * ntu * FSUB + (size_t)tile * FSUB + sub] = t;
+    }
   }
-  if (target) {
-    const float t = block_sum<FNT>(sq, red);
-    if (threadIdx.x == 0) loss_parts[(size_t)b * ntu * FSUB + bx] = t;
+}
+
+__device__ __forceinline__ void gram_finalize_body(
+    const float* __restrict__ ws, int c, int nsplit, float scale, float* __restrict__ g_out,
+    const float* __restrict__ target, long long t_bstride, float* __restrict__ coef, int cpad,
+    float cA, float alpha, float* __restrict__ loss_parts, const float* __restrict__ mse_parts,
+    int mse_nparts, double mse_n, float* __restrict__ mse_out, int bx, int by) {
+  __shared__ float part[FKL * (FEL + 1)];
+  __shared__ float red[FNT / 64];
+  // block (0, 0) also finalizes the content / feature MSE partials of a fused content
+  // pass (gram_tri_f16_kernel<128, true>): the launch a separate mse2 finalize would take
+  if (mse_out && bx == 0 && by == 0) {
+    float s = 0.f, sr = 0.f;
+    for (int i = threadIdx.x; i < mse_nparts; i += FNT) {
+      s += mse_parts[2 * i];
+      sr += mse_parts[2 * i + 1];
+    }
+    s = block_sum<FNT>(s, red);
+    sr = block_sum<FNT>(sr, red);
+    if (threadIdx.x == 0) {
+      const float mr = (float)(sr / mse_n);
+      mse_out[0] = (float)(s / mse_n);
+      mse_out[1] = (float)((double)(mr * mr) / mse_n);
+      mse_out[2] = mr;
+    }
+  }
+  switch (fin_groups(nsplit)) {
+    case 4:
+      gram_finalize_body_g<4>(ws, c, nsplit, scale, g_out, target, t_bstride, coef, cpad, cA,
+                              alpha, loss_parts, bx, by, part);
+      break;
+    case 2:
+      gram_finalize_body_g<2>(ws, c, nsplit, scale, g_out, target, t_bstride, coef, cpad, cA,
+                              alpha, loss_parts, bx, by, part);
+      break;
+    default:
+      gram_finalize_body_g<1>(ws, c, nsplit, scale, g_out, target, t_bstride, coef, cpad, cA,
+                              alpha, loss_parts, bx, by, part);
   }
 }
 
@@ -685,7 +715,7 @@ __global__ void __launch_bounds__(FNT) gram_finalize_batch_kernel(FinBatch fb) {
   while (j + 1 < fb.njobs && (int)blockIdx.x >= fb.blk0[j + 1]) ++j;
   const stx_gram_fin_job& q = fb.job[j];
   const int local = blockIdx.x - fb.blk0[j];
-  const int nt = cdiv(q.c, GT), nbx = nt * (nt + 1) / 2 * FSUB;
+  const int nt = cdiv(q.c, GT), nbx = nt * (nt + 1) / 2 * fin_blocks_per_tile(q.nsplit);
   gram_finalize_body(q.parts, q.c, q.nsplit, q.scale, q.g_out, q.target, q.t_bstride, q.coef,
                      q.cpad, q.cA, q.alpha, q.loss_parts, q.mse_parts, q.mse_nparts, q.mse_n,
                      q.mse_out, local % nbx, local / nbx);
@@ -874,7 +904,7 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
              parts, mse_fin ? mse_fin->parts : nullptr, mse_nparts, (double)b * c * hw,
              mse_fin ? mse_fin->out : nullptr, b);
   } else {
-    hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * FSUB, b), dim3(FNT), 0, st, slabs, c,
+    hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * fin_blocks_per_tile(nsplit), b), dim3(FNT), 0, st, slabs, c,
                        nsplit, scale, g_out, target, t_bstride, coef, cpad, cA, alpha, parts,
                        mse_fin ? mse_fin->parts : nullptr, mse_nparts, (double)b * c * hw,
                        mse_fin ? mse_fin->out : nullptr);
@@ -1085,7 +1115,7 @@ static int from_parts_impl(const float* gparts, int nparts, const float* target,
              0, 1.0, nullptr, b);
     return check_launch("stx_style_loss_from_parts_deferred");
   }
-  hipLaunchKernelGGL(gram_finalize_kernel, dim3(FSUB, b), dim3(FNT), 0, st, gparts, c, nparts,
+  hipLaunchKernelGGL(gram_finalize_kernel, dim3(fin_blocks_per_tile(nparts), b), dim3(FNT), 0, st, gparts, c, nparts,
                      (float)(1.0 / n), g_out, target,
                      target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts);
   if (loss)
@@ -1132,7 +1162,7 @@ extern "C" int stx_gram_finalize_batch(const stx_gram_fin_job* jobs, int njobs, 
     const int nt = cdiv(q.c, GT);
     fb.job[j] = q;
     fb.blk0[j] = blocks;
-    blocks += nt * (nt + 1) / 2 * FSUB * q.b;
+    blocks += nt * (nt + 1) / 2 * fin_blocks_per_tile(q.nsplit) * q.b;
   }
   fb.blk0[njobs] = blocks;
   fb.njobs = njobs;
