@@ -373,6 +373,191 @@ instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ 
   }
 }
 
+// Pipelined register variants for planes of exactly 4*NT*R4 floats (the ITN's 64^2
+// planes, 1024 of them at B = 8): a block walks PPB consecutive planes and issues the
+// next plane's loads before this plane's reductions and stores, so the chip's load and
+// store phases overlap instead of every block loading, reducing and storing in lockstep
+// (one-plane blocks all resident at once: 13 us for 34 MB).  Loads are unconditional
+// (exact plane size, compile-time residual / ReLU) so each wait covers one plane's loads.
+// Same arithmetic and reduction order per plane as the one-plane kernels (same bits).
+template <int NT, int R4, int PPB, bool RES>
+__global__ void __launch_bounds__(NT)
+instnorm_fwd_pipe_kernel(const float* __restrict__ x, const float* __restrict__ res,
+                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                         float* __restrict__ y, float* __restrict__ mean_out,
+                         float* __restrict__ rstd_out, int c, float eps, int relu,
+                         float* __restrict__ out_amax) {
+  constexpr int HW = 4 * NT * R4;
+  __shared__ float red[NT / 64];
+  const int p0 = blockIdx.x * PPB;
+  f32x4 xb[2][R4], rb[2][R4];
+  auto load = [&](int b, int plane) {
+    const f32x4* xp = reinterpret_cast<const f32x4*>(x + (size_t)plane * HW);
+#pragma unroll
+    for (int k = 0; k < R4; ++k) xb[b][k] = xp[threadIdx.x + k * NT];
+    if constexpr (RES) {
+      const f32x4* rp = reinterpret_cast<const f32x4*>(res + (size_t)plane * HW);
+#pragma unroll
+      for (int k = 0; k < R4; ++k) rb[b][k] = rp[threadIdx.x + k * NT];
+    }
+  };
+  uint32_t om = 0u;
+  load(0, p0);
+#pragma unroll
+  for (int j = 0; j < PPB; ++j) {
+    const int b = j & 1, plane = p0 + j;
+    if (j + 1 < PPB) load(b ^ 1, plane + 1);
+    f32x4 u[R4];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < R4; ++k) {
+      u[k] = xb[b][k];
+      if constexpr (RES) u[k] += rb[b][k];
+    }
+#pragma unroll
+    for (int k = 0; k < R4; ++k) s += (u[k][0] + u[k][1]) + (u[k][2] + u[k][3]);
+    const float mean = block_sum_nt<NT>(s, red) / (float)HW;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < R4; ++k) {
+      const f32x4 d = u[k] - mean;
+      q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+    }
+    const float var = block_sum_nt<NT>(q, red) / (float)HW;
+    const float rstd = 1.f / sqrtf(var + eps);
+    const int ch = plane % c;
+    const float gsc = gamma ? gamma[ch] * rstd : rstd;
+    const float sh = (beta ? beta[ch] : 0.f) - mean * gsc;
+    f32x4* yp = reinterpret_cast<f32x4*>(y + (size_t)plane * HW);
+#pragma unroll
+    for (int k = 0; k < R4; ++k) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = u[k][e] * gsc + sh;
+        if (relu) o[e] = fmaxf(o[e], 0.f);
+        om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
+      }
+      yp[threadIdx.x + k * NT] = o;
+    }
+    if (threadIdx.x == 0) {
+      if (mean_out) mean_out[plane] = mean;
+      if (rstd_out) rstd_out[plane] = rstd;
+    }
+  }
+  if (out_amax) {
+    uint32_t m = om;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = __uint_as_float(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t r = 0u;
+#pragma unroll
+      for (int i = 0; i < NT / 64; ++i) r = max(r, __float_as_uint(red[i]));
+      atomic_max_abs(out_amax + (blockIdx.x & (STX_AMAX_SLOTS - 1)), __uint_as_float(r));
+    }
+  }
+}
+
+template <int NT, int R4, int PPB, bool RELU, bool RES>
+__global__ void __launch_bounds__(NT)
+instnorm_bwd_pipe_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                         const float* __restrict__ x, const float* __restrict__ res,
+                         const float* __restrict__ gamma, const float* __restrict__ mean,
+                         const float* __restrict__ rstd, float* __restrict__ du,
+                         float* __restrict__ parts, int c, float* __restrict__ out_amax) {
+  constexpr int HW = 4 * NT * R4;
+  __shared__ float red[NT / 64];
+  const int p0 = blockIdx.x * PPB;
+  f32x4 db[2][R4], yb[2][R4], xb[2][R4], rb[2][R4];
+  auto load = [&](int b, int plane) {
+    const size_t base = (size_t)plane * HW;
+#pragma unroll
+    for (int k = 0; k < R4; ++k) {
+      const int i = threadIdx.x + k * NT;
+      db[b][k] = reinterpret_cast<const f32x4*>(dy + base)[i];
+      if constexpr (RELU) yb[b][k] = reinterpret_cast<const f32x4*>(y + base)[i];
+      xb[b][k] = reinterpret_cast<const f32x4*>(x + base)[i];
+      if constexpr (RES) rb[b][k] = reinterpret_cast<const f32x4*>(res + base)[i];
+    }
+  };
+  uint32_t om = 0u;
+  load(0, p0);
+#pragma unroll
+  for (int j = 0; j < PPB; ++j) {
+    const int b = j & 1, plane = p0 + j;
+    if (j + 1 < PPB) load(b ^ 1, plane + 1);
+    const float mu = mean[plane], rs = rstd[plane];
+    f32x4 g[R4], xh[R4];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int k = 0; k < R4; ++k) {
+      f32x4 u4 = xb[b][k];
+      if constexpr (RES) u4 += rb[b][k];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if constexpr (RELU) g[k][e] = !(yb[b][k][e] > 0.f) ? 0.f : db[b][k][e];
+        else g[k][e] = db[b][k][e];
+        xh[k][e] = (u4[e] - mu) * rs;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < R4; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sg += g[k][e];
+        sgx += g[k][e] * xh[k][e];
+      }
+    sg = block_sum_nt<NT>(sg, red);
+    sgx = block_sum_nt<NT>(sgx, red);
+    const float gm = gamma ? gamma[plane % c] : 1.f;
+    const float kk = gm * rs / (float)HW;
+    f32x4* dup = reinterpret_cast<f32x4*>(du + (size_t)plane * HW);
+    float sdu = 0.f;
+#pragma unroll
+    for (int k = 0; k < R4; ++k) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = kk * ((float)HW * g[k][e] - sg - xh[k][e] * sgx);
+        om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
+      }
+      dup[threadIdx.x + k * NT] = o;
+      sdu += (o[0] + o[1]) + (o[2] + o[3]);
+    }
+    sdu = block_sum_nt<NT>(sdu, red);
+    if (threadIdx.x == 0) {
+      parts[3 * plane] = sgx;
+      parts[3 * plane + 1] = sg;
+      parts[3 * plane + 2] = sdu;
+    }
+  }
+  if (out_amax) {
+    uint32_t m = om;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = __uint_as_float(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t r = 0u;
+#pragma unroll
+      for (int i = 0; i < NT / 64; ++i) r = max(r, __float_as_uint(red[i]));
+      atomic_max_abs(out_amax + (blockIdx.x & (STX_AMAX_SLOTS - 1)), __uint_as_float(r));
+    }
+  }
+}
+
+static int in_ppb() {  // planes per block of the pipelined 64^2 kernels (1: one-plane kernels)
+  static const int v = [] {
+    const char* e = getenv("STX_IN_PPB");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 // Large planes (the ITN's 256^2 layers: 64 K floats, 1024 threads x 16 float4): only g
 // stays in registers (64 VGPRs -- g and x-hat together would not fit 16 waves per CU);
 // the second pass re-reads u = x (+ res) instead of dy, y and u, one plane-read fewer
@@ -549,7 +734,21 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
   if (cfg == 1 && hw % 4 == 0 && hw <= 4 * 128 * 8)
     hipLaunchKernelGGL((instnorm_fwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, x, res,
                        gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
-  else if (cfg == 2 && hw % 4 == 0 && hw <= 4 * 512 * 2)
+  else if (cfg == 2 && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0 &&
+           ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) |
+             reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
+    const int ppb = in_ppb() >= 4 ? 4 : 2;
+    const dim3 grid(n * c / ppb);
+#define STX_IN_FWD_PIPE(P, R)                                                                   \
+  hipLaunchKernelGGL((instnorm_fwd_pipe_kernel<512, 2, P, R>), grid, dim3(512), 0, st, x, res, \
+                     gamma, beta, y, mean, rstd, c, eps, relu, out_amax)
+    if (ppb == 4) {
+      if (res) STX_IN_FWD_PIPE(4, true); else STX_IN_FWD_PIPE(4, false);
+    } else {
+      if (res) STX_IN_FWD_PIPE(2, true); else STX_IN_FWD_PIPE(2, false);
+    }
+#undef STX_IN_FWD_PIPE
+  } else if (cfg == 2 && hw % 4 == 0 && hw <= 4 * 512 * 2)
     hipLaunchKernelGGL((instnorm_fwd_reg_kernel<512, 2>), dim3(n * c), dim3(512), 0, st, x, res,
                        gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
   else if (hw % 4 == 0 && hw <= 4 * 256 * 4)
@@ -603,7 +802,21 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
   if (cfg == 1 && al && hw <= 4 * 128 * 8)
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, dy, y, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
-  else if (cfg == 2 && al && hw <= 4 * 512 * 2)
+  else if (cfg == 2 && al && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0) {
+    const int ppb = in_ppb() >= 4 ? 4 : 2;
+    const dim3 grid(n * c / ppb);
+#define STX_IN_BWD_PIPE(P, RL, R)                                                               \
+  hipLaunchKernelGGL((instnorm_bwd_pipe_kernel<512, 2, P, RL, R>), grid, dim3(512), 0, st, dy, y, \
+                     x, res, gamma, mean, rstd, du, (float*)ws, c, out_amax)
+    if (ppb == 4) {
+      if (relu) { if (res) STX_IN_BWD_PIPE(4, true, true); else STX_IN_BWD_PIPE(4, true, false); }
+      else { if (res) STX_IN_BWD_PIPE(4, false, true); else STX_IN_BWD_PIPE(4, false, false); }
+    } else {
+      if (relu) { if (res) STX_IN_BWD_PIPE(2, true, true); else STX_IN_BWD_PIPE(2, true, false); }
+      else { if (res) STX_IN_BWD_PIPE(2, false, true); else STX_IN_BWD_PIPE(2, false, false); }
+    }
+#undef STX_IN_BWD_PIPE
+  } else if (cfg == 2 && al && hw <= 4 * 512 * 2)
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<512, 2>), dim3(n * c), dim3(512), 0, st, dy, y, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else if (al && hw <= 4 * 256 * 4)

@@ -9,8 +9,8 @@ if [ -n "$T" ]; then
   [ $rc -eq 0 ] || exit $rc
 fi
 for i in 1 2; do
-  for v in new prev; do
-    if [ $v = prev ]; then L=$PWD/styletransfer_amd/libstx_prev.so; else L=$PWD/styletransfer_amd/libstx.so; fi
+  for v in new prev ${EXTRA_VARIANT:-}; do
+    if [ $v = prev ]; then L=$PWD/styletransfer_amd/libstx_prev.so; else L=$PWD/styletransfer_amd/libstx.so; fi; if [ $v = ppb2 ]; then export STX_IN_PPB=2; else unset STX_IN_PPB; fi
     STX_LIB=$L timeout -k 10 200 python bench.py --steps 50 --warmup 5 --skip-cpu --skip-infer --lbfgs-steps 0 --gatys-run-iters 0 --fast-b64-steps 0 > gpurun_out/${tag}_$v$i.json 2>gpurun_out/${tag}_$v$i.err || { tail -3 gpurun_out/${tag}_$v$i.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/${tag}_$v$i.json'));print('$v$i', 'gatys_ms', d['ms_per_step'], 'fast_ms', d['fast_st']['ms_per_step'])"
   done
