@@ -490,34 +490,40 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
 // whole restaging between them, and 36 KB of weights per chunk in one buffer).  Halo
 // buffers are sized to the exact item count (v1 pads to a multiple of 256).  Stride 1,
 // cin >= 16 only.
-template <int TW, int NI>
+// WM = 2: one 8-wave block for 128 couts (waves 4..7 the second 64), the halo of the
+// pixel tile staged once for both cout halves (the 128-channel layers)
+template <int TW, int NI, int WM = 1>
 struct C16v2 {
-  static constexpr int BM = 64, NPIX = 128 * NI, TH = NPIX / TW;
+  static constexpr int NT = 256 * WM;
+  static constexpr int BM = 64 * WM, NPIX = 128 * NI, TH = NPIX / TW;
   static constexpr int RH = TH + 2, RW = TW + 2, NPOS = RH * RW;
   static constexpr int NITEM = 2 * NPOS;               // (channel group, position) units
-  static constexpr int NIT = (NITEM + 255) / 256;      // items per thread
+  static constexpr int NIT = (NITEM + NT - 1) / NT;    // items per thread
   static constexpr int HB = 2 * NITEM * 16;            // one halo buffer: hi plane, lo plane
   static constexpr int WU = 3 * 4 * BM;                // weight units per step: [tap][P][cg][co]
-  static constexpr int NWU = WU / 256;
+  static constexpr int NWU = WU / NT;
   static constexpr int WB = WU * 16;                   // one weight buffer
   static constexpr int LDS_BYTES = 2 * HB + 2 * WB;
-  static_assert(WU % 256 == 0, "weight units per thread");
+  static_assert(WU % NT == 0, "weight units per thread");
   static_assert(16 * NPIX * 4 + 16 * BM * 4 <= LDS_BYTES, "phase-2 staging fits");
   static_assert(TW != 64 || NI != 2 || GramPlanes<256>::BYTES <= LDS_BYTES, "Gram planes fit");
 };
 
-template <int TW, int LM, int P2, int NI>
-__global__ void __launch_bounds__(256, (NI == 1 && TW <= 32) ? 3 : 2)
+template <int TW, int LM, int P2, int NI, int WM = 1>
+__global__ void __launch_bounds__(256 * WM, WM == 2 ? 1 : ((NI == 1 && TW <= 32) ? 3 : 2))
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
-  using C = C16v2<TW, NI>;
+  using C = C16v2<TW, NI, WM>;
+  constexpr int NT = C::NT;
   constexpr bool RP = TW == 64 && NI == 2;  // row-pair tiles (fused pool / unpool)
   static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
   static_assert(P2 != 2, "1x1 mode: v1 kernel");
+  static_assert(WM == 1 || (P2 == 0 && !RP), "WM = 2: plain epilogue only");
   constexpr int BM = C::BM;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // cout half, pixel column of the wave
   const int h = lane >> 5, l32 = lane & 31;
   const int co0 = blockIdx.y * BM;
   const int n = blockIdx.z;
@@ -551,7 +557,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   uint32_t woff[C::NWU];
 #pragma unroll
   for (int q = 0; q < C::NWU; ++q) {
-    const int u = tid + q * 256;
+    const int u = tid + q * NT;
     const int seg = u / BM, co = u - seg * BM;
     woff[q] = (uint32_t)((seg * cout64 + co0 + co) * 16);
   }
@@ -565,7 +571,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     const int vy0 = ty0 - 1, vx0 = tx0 - 1;
 #pragma unroll
     for (int r = 0; r < C::NIT; ++r) {
-      const int idx = tid + r * 256;
+      const int idx = tid + r * NT;
       const int cg = idx / C::NPOS, pos = idx - cg * C::NPOS;
       const int rr = pos / C::RW, cc = pos - rr * C::RW;
       const int vy = vy0 + rr, vx = vx0 + cc;
@@ -603,8 +609,8 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     }
   };
   auto st_halo = [&](int buf, int r) {
-    const int idx = tid + r * 256;
-    if (r + 1 < C::NIT || C::NITEM % 256 == 0 || idx < C::NITEM) {
+    const int idx = tid + r * NT;
+    if (r + 1 < C::NIT || C::NITEM % NT == 0 || idx < C::NITEM) {
       f16x8 hi, lo;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -632,7 +638,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     char* wbp = smem + 2 * C::HB + buf * C::WB;
 #pragma unroll
     for (int q = 0; q < C::NWU; ++q)
-      *reinterpret_cast<f32x4*>(wbp + (tid + q * 256) * 16) = wreg[q];
+      *reinterpret_cast<f32x4*>(wbp + (tid + q * NT) * 16) = wreg[q];
   };
 
   // per-lane operand bases (bytes) relative to buffer 0
@@ -640,10 +646,10 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     int ty, tx;
-    tile_pix<TW, RP, NI>(wave, j, l32, ty, tx);
+    tile_pix<TW, RP, NI>(wn, j, l32, ty, tx);
     boff[j] = (h * C::NPOS + ty * C::RW + tx) * 16;
   }
-  const int aoff = 2 * C::HB + (h * BM + l32) * 16;
+  const int aoff = 2 * C::HB + (h * BM + wm * 64 + l32) * 16;
 
   const int tile = first;
   halo_offsets(tile);
@@ -748,10 +754,12 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
       }
     }
 
-    EpiTile et{n, co0, ty0, tx0, 0, wave, h, l32};
+    EpiTile et{n, co0, ty0, tx0, wm, wn, h, l32};
     et.tile = tile;
     et.ntiles = ntiles;
-    if constexpr (P2 == 1) {
+    if constexpr (WM == 2) {
+      conv_epilogue_plain<TW, NI, RP>(acc, p, et, descale, smem);  // (eligibility: launch16v2)
+    } else if constexpr (P2 == 1) {
       conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, true>(acc, p, et, descale,
                                                        reinterpret_cast<float*>(smem),
                                                        reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
@@ -762,6 +770,25 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
                                                           reinterpret_cast<float*>(smem + 16 * C::NPIX * 4));
     }
   }
+}
+
+static int cus16() {  // compute units (the WM = 2 form pays only in a single round of blocks)
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+static bool wm2_on() {  // STX_V2_WM2=0: 64-cout blocks for every layer (A/B)
+  static const bool on = [] {
+    const char* e = getenv("STX_V2_WM2");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
 }
 
 template <int TW, int LM, int NI>
@@ -780,6 +807,19 @@ static int launch16v2(const stx_conv_params& p, hipStream_t st) {
     set_error("stx_conv2d: the fused Gram-backward phase needs a raw-input conv");
     return STX_E_INVALID;
   }
+  // 128-pixel tiles of a 128-channel layer through the plain epilogue, when the grid is at
+  // most one block per CU (the ImageTransformNet's residual convs at B = 8: 256 blocks): one
+  // 8-wave block per 128 couts, the tile's halo staged once for both cout halves (same-box
+  // A/B: fast_st 4607/4626 -> 4570/4592 us per step; Gatys' 512-block conv3_1 lost 5 us)
+  if constexpr (NI == 1)
+    if (wm2_on() && p.cout % 128 == 0 && (long long)ntiles * (p.cout / 128) * p.n <= cus16() &&
+        !p.mask && !p.accumulate && !p.acc_scale && !p.up_dp &&
+        !p.pool_out && !p.pool_sum && !p.gram_part && !(p.aux && p.relu_out)) {
+      dim3 g2(ntiles, p.cout / 128, p.n);
+      hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI, 2>), g2, dim3(512), 0, st, p,
+                         tiles_x, ntiles);
+      return check_launch("stx_conv2d(f16x3 v2, 128 couts)");
+    }
   hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI>), grid, dim3(256), 0, st, p,
                      tiles_x, ntiles);
   return check_launch("stx_conv2d(f16x3 v2)");

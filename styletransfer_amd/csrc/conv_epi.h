@@ -51,7 +51,7 @@ __device__ __forceinline__ void atomic_max_abs(float* slot, float m) {
 // ~12-15 ns each chip-wide (8192 of them stalled a 64 MB pass for 100 us; 1024 at a
 // conv's tail cost ~15 us)
 __device__ __forceinline__ void block_max_to(float* group, float m) {
-  __shared__ float red[4];
+  __shared__ float red[16];  // up to 1024-thread blocks
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float other = __shfl_xor(m, o, 64);
@@ -62,8 +62,7 @@ __device__ __forceinline__ void block_max_to(float* group, float m) {
   __syncthreads();
   if (tid == 0) {
     float r = red[0];
-#pragma unroll
-    for (int i = 1; i < 4; ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
     const int bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
     atomic_max_abs(group + (bid & (STX_AMAX_SLOTS - 1)), fabsf(r));
   }
