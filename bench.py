@@ -62,7 +62,7 @@ PEAK_HBM_GBS = 8000.0
 # WRITE_SIZE passes of tools/pmc_r3.sh over an eager Gatys iteration, calibrated on
 # kernels of known byte count: tools/pmc_r3_summary.py -> profiles/r4_pmc.json, the
 # passes over the current build)
-ROOFLINE_KERNEL = "conv3x3_f16x3_v2_kernel<64, 1, 0, 2>"
+ROOFLINE_KERNEL = "conv3x3_f16x3_v2_kernel<64, 1, 0, 2, 1>"
 ROOFLINE_MATCH = ROOFLINE_KERNEL
 PMC_FILE = os.path.join(REPO, "profiles", "r4_pmc.json")
 # algorithmic bytes of conv1_2 fwd @512^2 as the iteration launches it: Z1 in, Z2 and the
@@ -653,7 +653,7 @@ def main():
                 "iteration_tflops": round(GATYS_GFLOP.get(args.size, float("nan")) * g["rate"]
                                           / world / 1e3, 3),
                 "dominant_kernel": {
-                    "kernel": "conv3x3_f16x3_v2_kernel<64, 0, 1, 2> (conv1_2 data gradient "
+                    "kernel": "conv3x3_f16x3_v2_kernel<64, 0, 1, 2, 1> (conv1_2 data gradient "
                               f"@ {args.size}^2 with the fused Gram-backward phase: dZ1 = "
                               "[Z1 > 0] conv1_2^T(dZ2) + A1 Z1; the iteration's longest launch)",
                     "achieved": round(k["dg_tflops"], 3),

@@ -808,11 +808,13 @@ static int launch16v2(const stx_conv_params& p, hipStream_t st) {
     return STX_E_INVALID;
   }
   // 128-pixel tiles of a 128-channel layer through the plain epilogue, when the grid is at
-  // most one block per CU (the ImageTransformNet's residual convs at B = 8: 256 blocks): one
+  // most one block per CU and at least half the CUs (the ImageTransformNet's residual convs
+  // at B = 8: 256 blocks; at B = 1 the 64-cout form's 64 blocks beat 32): one
   // 8-wave block per 128 couts, the tile's halo staged once for both cout halves (same-box
   // A/B: fast_st 4607/4626 -> 4570/4592 us per step; Gatys' 512-block conv3_1 lost 5 us)
   if constexpr (NI == 1)
     if (wm2_on() && p.cout % 128 == 0 && (long long)ntiles * (p.cout / 128) * p.n <= cus16() &&
+        2LL * ntiles * (p.cout / 128) * p.n >= cus16() &&  // (tiny grids keep more blocks)
         !p.mask && !p.accumulate && !p.acc_scale && !p.up_dp &&
         !p.pool_out && !p.pool_sum && !p.gram_part && !(p.aux && p.relu_out)) {
       dim3 g2(ntiles, p.cout / 128, p.n);

@@ -735,6 +735,7 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
     hipLaunchKernelGGL((instnorm_fwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, x, res,
                        gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
   else if (cfg == 2 && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0 &&
+           n * c / in_ppb() >= 256 &&  // enough blocks to fill the chip (B = 8: 256)
            ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) |
              reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
     const int ppb = in_ppb() >= 4 ? 4 : 2;
@@ -802,7 +803,8 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
   if (cfg == 1 && al && hw <= 4 * 128 * 8)
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, dy, y, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
-  else if (cfg == 2 && al && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0) {
+  else if (cfg == 2 && al && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0 &&
+           n * c / in_ppb() >= 256) {
     const int ppb = in_ppb() >= 4 ? 4 : 2;
     const dim3 grid(n * c / ppb);
 #define STX_IN_BWD_PIPE(P, RL, R)                                                               \

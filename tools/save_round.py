@@ -28,7 +28,7 @@ open(f"profiles/{tag}_gatys512_iteration_breakdown.txt", "w").write(
 out = [f"rocprofv3 --kernel-trace of the bench's Gatys legs (profiles/{tag}_bench_kernel_stats.csv):",
        "per-dispatch durations by grid (blocks x, y, z)",
        "kernel                                              grid            n   mean_us  median_us"]
-for K in ("conv3x3_f16x3_v2_kernel<64, 1, 0, 2>", "conv3x3_f16x3_v2_kernel<64, 0, 1, 2>"):
+for K in ("conv3x3_f16x3_v2_kernel<64, 1, 0, 2, 1>", "conv3x3_f16x3_v2_kernel<64, 0, 1, 2, 1>"):
     by = {}
     for r in csv.DictReader(open(f"{G}/{tag}_prof/run_kernel_trace.csv")):
         if K in r["Kernel_Name"]:
