@@ -808,13 +808,14 @@ static int launch16v2(const stx_conv_params& p, hipStream_t st) {
     return STX_E_INVALID;
   }
   // 128-pixel tiles of a 128-channel layer through the plain epilogue, when the grid is at
-  // most one block per CU and at least half the CUs (the ImageTransformNet's residual convs
-  // at B = 8: 256 blocks; at B = 1 the 64-cout form's 64 blocks beat 32): one
+  // most one block per CU and fills (nearly) every CU (the ImageTransformNet's residual
+  // convs at B = 8: 256 blocks; a 128-block grid left half the CUs idle -- Gatys' conv3_1
+  // data gradient 39 -> 48 us -- and B = 1's 32 blocks lost to the 64-cout form's 64): one
   // 8-wave block per 128 couts, the tile's halo staged once for both cout halves (same-box
   // A/B: fast_st 4607/4626 -> 4570/4592 us per step; Gatys' 512-block conv3_1 lost 5 us)
   if constexpr (NI == 1)
     if (wm2_on() && p.cout % 128 == 0 && (long long)ntiles * (p.cout / 128) * p.n <= cus16() &&
-        2LL * ntiles * (p.cout / 128) * p.n >= cus16() &&  // (tiny grids keep more blocks)
+        10LL * ntiles * (p.cout / 128) * p.n >= 9LL * cus16() &&  // a (nearly) full round
         !p.mask && !p.accumulate && !p.acc_scale && !p.up_dp &&
         !p.pool_out && !p.pool_sum && !p.gram_part && !(p.aux && p.relu_out)) {
       dim3 g2(ntiles, p.cout / 128, p.n);
