@@ -130,6 +130,11 @@ typedef struct stx_conv_params {
    * instead of T partials.  The per-tile slots then hold three of the four 32 x 32
    * blocks only (scratch); the gram_part slab needs (T + NG) * 4096 floats per image. */
   unsigned int* gram_cnt;
+  /* optional with p2_z on the split path: device amax group >= max|s * A[n]| over every
+   * image n (stx_gram_fin_job.coef_amax of the finalize that wrote A, times |p2_scale|
+   * folded in by the kernel).  The Gram-backward phase then runs on the fp16 hi/lo
+   * split MFMA with this precomputed scale instead of the fp32 MFMA. */
+  const float* p2_wt_amax;
 } stx_conv_params;
 
 #define STX_GRAM_GROUP 8
@@ -328,6 +333,7 @@ typedef struct stx_gram_fin_job {
   double mse_n;
   float scale, cA, alpha;
   int c, nsplit, b, cpad, mse_nparts;
+  float* coef_amax;        /* optional amax group (zeroed): >= max|coef| over the batch */
 } stx_gram_fin_job;
 int stx_style_loss_deferred(const float* z, const float* target, float* coef, int b, int c,
                             int hw, int target_batched, float weight, float diag_alpha,

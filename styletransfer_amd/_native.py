@@ -38,7 +38,7 @@ class ConvParams(C.Structure):
         ("up_dp", vp), ("up_z", vp),
         ("wt16", vp), ("w_amax", vp), ("in_amax", vp), ("out_amax", vp),
         ("pool_out", vp), ("p2_amax", vp), ("gram_part", vp), ("pool_sum", i32),
-        ("gram_cnt", vp),
+        ("gram_cnt", vp), ("p2_wt_amax", vp),
     ]
 
 
@@ -77,7 +77,7 @@ class GramFinJob(C.Structure):
     _fields_ = [("parts", vp), ("g_out", vp), ("target", vp), ("coef", vp), ("loss_parts", vp),
                 ("mse_parts", vp), ("mse_out", vp), ("t_bstride", i64), ("mse_n", C.c_double),
                 ("scale", f32), ("cA", f32), ("alpha", f32), ("c", i32), ("nsplit", i32),
-                ("b", i32), ("cpad", i32), ("mse_nparts", i32)]
+                ("b", i32), ("cpad", i32), ("mse_nparts", i32), ("coef_amax", vp)]
 
 
 STX_FIN_MAX = 8

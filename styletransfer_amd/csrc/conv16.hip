@@ -226,6 +226,126 @@ __device__ __forceinline__ void phase2_f16(f32x16 (&acc)[2][2], const stx_conv_p
       for (int r = 0; r < 16; ++r) acc[i][j][r] *= down;
 }
 
+// Split Gram-backward phase of the v2 data-gradient conv (P2 = 3): acc -- already
+// de-scaled, *acc_scale, ReLU-masked and brought to the power-of-two scale S = 2^ls --
+// gets + S * s2 * A[n] . z2 on the fp16 hi/lo MFMA with every scale precomputed: z2 by
+// its amax group (p2_amax: sz = 2^(15 - ez)), A' = s2 * A by the batch max the Gram
+// finalize wrote (p2_wt_amax: sa = S / sz <= 2^(15 - ea)).  No in-kernel reductions: the
+// round-3 port of phase2_f16 paid two block-wide max passes and a re-read of A for its
+// scales, and lost to the fp32 MFMA.  Per 16-channel chunk: z2 -> LDS [P][cg][256 px]
+// (16-B units of 8 channels, hi / lo planes); A' straight from memory into each lane's
+// fragment registers (no LDS round trip); 3 MFMAs per 32 x 32 tile (the fp32 phase:
+// 8 x 32x32x2 f32, 5x the MFMA cycles); the next chunk's loads are in flight during the
+// MFMAs.
+template <int TW, bool RP>
+__device__ __forceinline__ void phase2_pre(f32x16 (&acc)[2][2], const stx_conv_params& p,
+                                           const EpiTile& t, int ls, int ez, char* smem) {
+  constexpr int NPIX = 256;
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, h = t.h, l32 = t.l32;
+  const size_t plane = (size_t)p.ho * p.wo;
+  const int C2 = p.p2_c;
+  const float s2 = p.p2_scale ? *p.p2_scale : 1.f;
+  const float sz = __builtin_ldexpf(1.f, 15 - ez);
+  const float sa = __builtin_ldexpf(s2, ls - (15 - ez));
+  char* lz = smem;                  // [P][cg][256 px] x 16 B = 16 KB
+  // z2: thread -> pixel quad (4 consecutive pixels of a tile row) x channel quad cq
+  const int q = tid & 63, cq = tid >> 6;
+  const int qp = 4 * q, qrow = qp / TW, qcol = qp - qrow * TW;
+  const int qy = t.ty0 + qrow, qx = t.tx0 + qcol;
+  const bool vec = (p.wo & 3) == 0;  // rows 16-B aligned: a quad is all in or all out
+  const uint32_t zq_off = (qy < p.ho && qx < p.wo) ? (uint32_t)(qy * p.wo + qx) * 4u : BUF_OOB;
+  const uint32_t pb = (uint32_t)plane * 4u;
+  const float* __restrict__ z2 = p.p2_z + (size_t)t.n * C2 * plane;
+  // A' fragments straight from memory (small, L2 resident): lane (h, l32) of tile i
+  // holds A[c0 + 8h + e][co0 + 32 i + l32], e < 8 (32 consecutive couts per load)
+  const auto ra = make_srd(p.p2_wt + (size_t)t.n * p.p2_wt_batch_stride,
+                           (uint32_t)C2 * (uint32_t)p.cout_pad * 4u);
+  const uint32_t a_off = (uint32_t)((8 * h) * p.cout_pad + t.co0 + l32) * 4u;
+  const uint32_t a_row = (uint32_t)p.cout_pad * 4u;
+  int bpix[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int ty, tx;
+    tile_pix<TW, RP, 2>(t.wn, j, l32, ty, tx);
+    bpix[j] = ty * TW + tx;
+  }
+  struct Stage {
+    f32x4 z[4];  // [channel e of the quad] x 4 pixels
+    float a[2][8];
+  };
+  auto fetch = [&](int c0, Stage& g) {
+    const auto rz = make_srd(z2 + (size_t)c0 * plane, (uint32_t)max(0, C2 - c0) * pb);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t o = zq_off + (uint32_t)(4 * cq + e) * pb;
+      if (vec) {
+        g.z[e] = buf_ld4(rz, o);
+      } else {  // ragged width: per-pixel loads, pixels past the row end read 0
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          g.z[e][k] = (qx + k < p.wo) ? buf_ld(rz, o + 4u * k) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)  // channels past C2 read 0 (descriptor range)
+        g.a[i][e] = buf_ld(ra, a_off + (uint32_t)(c0 + e) * a_row + (uint32_t)(128 * i));
+  };
+  auto stage = [&](const Stage& g) {
+    const int cg = cq >> 1, hf = cq & 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = g.z[e][k] * sz;
+        const _Float16 vh = (_Float16)v;
+        hi[e] = vh;
+        lo[e] = (_Float16)(v - (float)vh);
+      }
+      *reinterpret_cast<f16x4*>(lz + ((0 * 2 + cg) * NPIX + qp + k) * 16 + hf * 8) = hi;
+      *reinterpret_cast<f16x4*>(lz + ((1 * 2 + cg) * NPIX + qp + k) * 16 + hf * 8) = lo;
+    }
+  };
+  auto split_a = [&](const Stage& g, f16x8 (&fa)[2][2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = g.a[i][e] * sa;
+        const _Float16 vh = (_Float16)v;
+        fa[i][0][e] = vh;
+        fa[i][1][e] = (_Float16)(v - (float)vh);
+      }
+  };
+  Stage g;
+  fetch(0, g);
+  for (int c0 = 0; c0 < C2; c0 += 16) {
+    __syncthreads();  // the previous chunk's (or the main loop's) LDS reads done
+    stage(g);
+    f16x8 fa[2][2];
+    split_a(g, fa);
+    __syncthreads();
+    if (c0 + 16 < C2) fetch(c0 + 16, g);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f16x8 fb[2];
+#pragma unroll
+        for (int P = 0; P < 2; ++P)
+          fb[P] = *reinterpret_cast<const f16x8*>(lz + ((P * 2 + h) * NPIX + bpix[j]) * 16);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][0], fb[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][0], fb[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][1], fb[0], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // LDS handed back to the epilogue
+}
+
 // S = 2: the stride-2 downsampling convs (raw input, loader mode LM_S2): the tile's
 // input window is (2 TH + 1) x (2 TW + 1) and output pixel (ty, tx) reads its taps at
 // window position (2 ty + kh, 2 tx + kw)
@@ -759,6 +879,31 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     et.ntiles = ntiles;
     if constexpr (WM == 2) {
       conv_epilogue_plain<TW, NI, RP>(acc, p, et, descale, smem);  // (eligibility: launch16v2)
+    } else if constexpr (P2 == 3) {
+      // (eligibility: launch16v2 -- data gradient + mask + the phase, bias / out_amax only)
+      const int ez = amax_exp(read_amax(p.p2_amax));
+      const int ea = amax_exp(read_amax(p.p2_wt_amax) * fabsf(p.p2_scale ? *p.p2_scale : 1.f));
+      // |acc| < 9 cin16 2^(ex + ew) |acc_scale|: every split-operand product is below 2^30
+      // before the de-scale
+      const int eacc = ex + ew + (32 - __builtin_clz(9 * rup(p.cin, 16))) + 1 +
+                       amax_exp(p.acc_scale ? fabsf(*p.acc_scale) : 1.f);
+      const int ls = max(min(min(30 - ea - ez, 100 - eacc), 120), -100);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] *= descale;
+      epi_scale_mask<TW, RP, NI>(acc, p, et);
+      const float up = __builtin_ldexpf(1.f, ls);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] *= up;
+      phase2_pre<TW, RP>(acc, p, et, ls, ez, smem);
+      conv_epilogue_plain_body<TW, NI, RP, false>(acc, p, et, __builtin_ldexpf(1.f, -ls), smem);
     } else if constexpr (P2 == 1) {
       conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, true>(acc, p, et, descale,
                                                        reinterpret_cast<float*>(smem),
@@ -791,6 +936,14 @@ static bool wm2_on() {  // STX_V2_WM2=0: 64-cout blocks for every layer (A/B)
   return on;
 }
 
+static bool p2_split_on() {  // STX_P2_SPLIT=0: the fp32-MFMA phase even given p2_wt_amax (A/B)
+  static const bool on = [] {
+    const char* e = getenv("STX_P2_SPLIT");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 template <int TW, int LM, int NI>
 static int launch16v2(const stx_conv_params& p, hipStream_t st) {
   using C = C16v2<TW, NI>;
@@ -800,6 +953,12 @@ static int launch16v2(const stx_conv_params& p, hipStream_t st) {
   if (p.p2_z) {
     // the fused Gram-backward phase: 256-pixel tiles of a raw-input data gradient
     if constexpr (NI == 2 && LM == STX_IN_RAW) {
+      if (p.p2_wt_amax && p2_split_on() && !p.up_dp && !p.aux && !p.accumulate &&
+          !p.relu_out && !p.pool_out && !p.gram_part) {
+        hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 3, NI>), grid, dim3(256), 0, st, p,
+                           tiles_x, ntiles);
+        return check_launch("stx_conv2d(f16x3 v2 + split phase 2)");
+      }
       hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 1, NI>), grid, dim3(256), 0, st, p,
                          tiles_x, ntiles);
       return check_launch("stx_conv2d(f16x3 v2 + phase 2)");

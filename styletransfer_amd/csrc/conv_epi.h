@@ -389,6 +389,48 @@ __device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const 
   return true;
 }
 
+// acc *= acc_scale, then the ReLU mask (acc = 0 where mask <= 0): the order of the fp32
+// path, ahead of a fused Gram-backward phase
+template <int TW, bool ROWPAIR, int NI>
+__device__ __forceinline__ void epi_scale_mask(f32x16 (&acc)[2][NI], const stx_conv_params& p,
+                                               const EpiTile& t) {
+  const size_t plane = (size_t)p.ho * p.wo;
+  const int n = t.n, h = t.h, l32 = t.l32;
+  if (p.acc_scale) {
+    const float sc = *p.acc_scale;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
+  }
+  if (p.mask) {
+    // descriptor at this wave's first row: per-lane pixel offset + per-register row
+    // constant (no 64-bit address math); rows past cout / pixels past the image
+    // read 0 (their outputs are dropped by the final stores anyway)
+    const int co_m = t.co0 + t.wm * 64;
+    const uint32_t mpb = (uint32_t)plane * 4u;
+    const auto rm = make_srd(p.mask + ((size_t)n * p.cout + co_m) * plane,
+                             (uint32_t)max(0, p.cout - co_m) * mpb);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      int ty, tx;
+      tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
+      const int oy = t.ty0 + ty, ox = t.tx0 + tx;
+      const uint32_t mo = (oy < p.ho && ox < p.wo)
+                              ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t row = (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2));
+          if (!(buf_ld(rm, mo + row * mpb) > 0.f)) acc[i][j][r] = 0.f;
+        }
+    }
+  }
+}
+
 template <int BM, int TW, int NPIX, int CIS2, bool ROWPAIR = false, int NI = 2,
           bool HAS_P2 = true>
 // (NI: 32-pixel N-tiles per wave; ROWPAIR needs NI == 2)
@@ -410,39 +452,7 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][NI], const stx_co
   bool mask_done = false;
   if (HAS_P2 && p.p2_z) {
     // ---- fused second phase: acc = acc*(mask>0) + s2 * A[n] . z2 (1x1, no halo) ----
-    if (p.acc_scale) {
-      const float sc = *p.acc_scale;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
-    }
-    if (p.mask) {
-      // descriptor at this wave's first row: per-lane pixel offset + per-register row
-      // constant (no 64-bit address math); rows past cout / pixels past the image
-      // read 0 (their outputs are dropped by the final stores anyway)
-      const int co_m = t.co0 + t.wm * 64;
-      const uint32_t mpb = (uint32_t)plane * 4u;
-      const auto rm = make_srd(p.mask + ((size_t)n * p.cout + co_m) * plane,
-                               (uint32_t)max(0, p.cout - co_m) * mpb);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        int ty, tx;
-        tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
-        const int oy = t.ty0 + ty, ox = t.tx0 + tx;
-        const uint32_t mo = (oy < p.ho && ox < p.wo)
-                                ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const uint32_t row = (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2));
-            if (!(buf_ld(rm, mo + row * mpb) > 0.f)) acc[i][j][r] = 0.f;
-          }
-      }
-    }
+    epi_scale_mask<TW, ROWPAIR, NI>(acc, p, t);
     mask_done = true;
     const float s2 = p.p2_scale ? *p.p2_scale : 1.f;
     const float* __restrict__ z2 = p.p2_z + (size_t)n * p.p2_c * plane;

@@ -593,7 +593,8 @@ template <int G>
 __device__ __forceinline__ void gram_finalize_body_g(
     const float* __restrict__ ws, int c, int nsplit, float scale, float* __restrict__ g_out,
     const float* __restrict__ target, long long t_bstride, float* __restrict__ coef, int cpad,
-    float cA, float alpha, float* __restrict__ loss_parts, int bx, int by, float* part) {
+    float cA, float alpha, float* __restrict__ loss_parts, int bx, int by, float* part,
+    float* __restrict__ coef_amax) {
   constexpr int KL = FKL / G, GT_ = FNT / G;  // split-lanes and threads per sub-tile
   const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
   const int tile = bx / (FSUB / G), r = threadIdx.x / GT_, sub = (bx % (FSUB / G)) * G + r;
@@ -622,7 +623,7 @@ __device__ __forceinline__ void gram_finalize_body_g(
     for (int i = 0; i < 4; ++i) pr[kl * (FEL + 1) + 4 * q4 + i] = t[i];
   }
   __syncthreads();
-  float sq = 0.f;
+  float sq = 0.f, ma = 0.f;
   if (t2 < FEL) {  // one wave per sub-tile
     const int el = t2, e = sub * FEL + el;
     float s = 0.f;
@@ -641,14 +642,23 @@ __device__ __forceinline__ void gram_finalize_body_g(
         if (coef) {
           const float a = cA * d;
           float* cb = coef + (size_t)b * cpad * cpad;
-          cb[(size_t)gi * cpad + gj] = a + (gi == gj ? alpha : 0.f);
+          const float ad = a + (gi == gj ? alpha : 0.f);
+          cb[(size_t)gi * cpad + gj] = ad;
           if (I != J) cb[(size_t)gj * cpad + gi] = a;
+          ma = fmaxf(fabsf(ad), fabsf(a));
         }
       }
     }
     if (target) {  // the sub-tile's loss partial: its one wave's sum
       const float t = wave_sum(sq);
       if (t2 == 0) loss_parts[(size_t)b * ntu * FSUB + (size_t)tile * FSUB + sub] = t;
+    }
+    if (coef_amax) {  // max|A| of the batch for the split Gram-backward phase
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) ma = fmaxf(ma, __shfl_xor(ma, o, 64));
+      if (t2 == 0)  // |v| >= 0: the bit pattern orders like the value
+        atomicMax(reinterpret_cast<unsigned int*>(coef_amax + (bx & (STX_AMAX_SLOTS - 1))),
+                  __float_as_uint(ma));
     }
   }
 }
@@ -657,7 +667,8 @@ __device__ __forceinline__ void gram_finalize_body(
     const float* __restrict__ ws, int c, int nsplit, float scale, float* __restrict__ g_out,
     const float* __restrict__ target, long long t_bstride, float* __restrict__ coef, int cpad,
     float cA, float alpha, float* __restrict__ loss_parts, const float* __restrict__ mse_parts,
-    int mse_nparts, double mse_n, float* __restrict__ mse_out, int bx, int by) {
+    int mse_nparts, double mse_n, float* __restrict__ mse_out, int bx, int by,
+    float* __restrict__ coef_amax = nullptr) {
   __shared__ float part[FKL * (FEL + 1)];
   __shared__ float red[FNT / 64];
   // block (0, 0) also finalizes the content / feature MSE partials of a fused content
@@ -680,15 +691,15 @@ __device__ __forceinline__ void gram_finalize_body(
   switch (fin_groups(nsplit)) {
     case 4:
       gram_finalize_body_g<4>(ws, c, nsplit, scale, g_out, target, t_bstride, coef, cpad, cA,
-                              alpha, loss_parts, bx, by, part);
+                              alpha, loss_parts, bx, by, part, coef_amax);
       break;
     case 2:
       gram_finalize_body_g<2>(ws, c, nsplit, scale, g_out, target, t_bstride, coef, cpad, cA,
-                              alpha, loss_parts, bx, by, part);
+                              alpha, loss_parts, bx, by, part, coef_amax);
       break;
     default:
       gram_finalize_body_g<1>(ws, c, nsplit, scale, g_out, target, t_bstride, coef, cpad, cA,
-                              alpha, loss_parts, bx, by, part);
+                              alpha, loss_parts, bx, by, part, coef_amax);
   }
 }
 
@@ -718,7 +729,7 @@ __global__ void __launch_bounds__(FNT) gram_finalize_batch_kernel(FinBatch fb) {
   const int nt = cdiv(q.c, GT), nbx = nt * (nt + 1) / 2 * fin_blocks_per_tile(q.nsplit);
   gram_finalize_body(q.parts, q.c, q.nsplit, q.scale, q.g_out, q.target, q.t_bstride, q.coef,
                      q.cpad, q.cA, q.alpha, q.loss_parts, q.mse_parts, q.mse_nparts, q.mse_n,
-                     q.mse_out, local % nbx, local / nbx);
+                     q.mse_out, local % nbx, local / nbx, q.coef_amax);
 }
 
 // one wave: the fixed-order sum of n loss partials (4 lane-strided accumulators, then a

@@ -403,7 +403,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
            relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
            p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
            pool_out=None, p2_amax=None, split_1x1=False, gram_part=None, pool_sum=False,
-           gram_cnt=None):
+           gram_cnt=None, p2_wt_amax=None):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
     up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
@@ -414,7 +414,9 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
     gram_part [n * conv_gram_tiles(...) * 4096] receives the fused per-tile Gram
     partials of out (stx_conv_params.gram_part); pool_sum: pool_out receives the 2x2
     SUM of the output instead and the full-resolution output is not written (returned:
-    pool_out) -- the nearest-x2 upsampling backward fused into a data gradient."""
+    pool_out) -- the nearest-x2 upsampling backward fused into a data gradient.
+    p2_wt_amax: amax group >= max|p2_coef| over the batch (a FinalizeBatch job's
+    coef_amax): the split path's Gram-backward phase then runs on the fp16 split MFMA."""
     _req(x, "x")
     n, c, h, w = x.shape
     assert c == cin, (c, cin)
@@ -450,6 +452,8 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         p.wt16, p.w_amax, p.in_amax = wt16[0].data_ptr(), wt16[1].data_ptr(), in_amax.data_ptr()
         if p2_z is not None:
             p.p2_amax = (p2_amax if p2_amax is not None else amax(p2_z)).data_ptr()
+            if p2_wt_amax is not None:
+                p.p2_wt_amax = p2_wt_amax.data_ptr()
     elif split_1x1:
         # Gram backward as the split phase alone (per-image weights, include/stx.h)
         assert ks == 1 and wt_batch_stride and mask is None and p2_z is None

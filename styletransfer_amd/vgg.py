@@ -186,6 +186,7 @@ class LossState:
     alpha: float = 0.0
     amax: torch.Tensor = None                   # [16] max|.| slots of split-conv inputs
     amax_cleared: bool = False                  # amax already zeroed (by the engine's Adam)
+    coef_amax: list = None                      # per tap: amax group >= max|A| (or None)
     pools: list = field(default_factory=lambda: [None] * 5)  # fused relu+pool outputs
     lws: list = field(default_factory=lambda: [None] * 5)    # per-layer style-loss scratch
     parts: list = field(default_factory=lambda: [None] * 5)  # deferred loss partials
@@ -271,6 +272,31 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     # finalize launch runs on main after the join)
     fin = ops.FinalizeBatch() if os.environ.get("STX_FIN_BATCH", "1") != "0" else None
 
+    def tap_loss(i, l, z, b_, c_, fuse_mse):
+        if fuse_mse:  # style loss + content/feature/feature-mse in one pass over z
+            st.parts[i], st.coef[i] = ops.style_content_loss(
+                z, targets[i], c4, st.losses[5:8], weight=sw, diag_alpha=alpha,
+                coef=st.coef[i], z_amax=slot(st.amax, l + 1), defer_ws=st.lws[i], fin=fin)
+            return
+        if st.grams[l] is not None:
+            gp = st.grams[l]
+            if isinstance(gp, tuple):  # the group sums after the B * nt tile slots
+                ng = gp[1].numel() // b_
+                gp = gp[0][gp[0].numel() - b_ * ng * 4096:]
+            st.parts[i], st.coef[i] = ops.style_loss_from_parts(
+                gp, gp.numel() // (b_ * 4096), b_, c_, z[0, 0].numel(),
+                targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
+                coef=st.coef[i], defer_ws=st.lws[i], fin=fin)
+        else:
+            st.parts[i], st.coef[i] = ops.style_loss(
+                z, targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
+                coef=st.coef[i], z_amax=slot(st.amax, l + 1) if split else None,
+                defer_ws=st.lws[i], fin=fin)
+        if l == CONTENT_CONV:  # content, feature, feature-mse: one pass
+            ops.mse(z, c4, mode=2, out=st.losses[5:8])
+
+    st.coef_amax = [None] * 5
+
     def on_layer(l, z):
         # the style loss of layer l (and the content/feature losses at conv2_2) run on
         # the side stream while the next conv runs: memory-bound reductions under
@@ -290,27 +316,14 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                                                                              z[0, 0].numel())
             if st.lws[i] is None or st.lws[i].numel() < need:
                 st.lws[i] = torch.empty(need, device=dev, dtype=torch.uint8)
-            if fuse_mse:  # style loss + content/feature/feature-mse in one pass over z
-                st.parts[i], st.coef[i] = ops.style_content_loss(
-                    z, targets[i], c4, st.losses[5:8], weight=sw, diag_alpha=alpha,
-                    coef=st.coef[i], z_amax=slot(st.amax, l + 1), defer_ws=st.lws[i], fin=fin)
-                return
-            if st.grams[l] is not None:
-                gp = st.grams[l]
-                if isinstance(gp, tuple):  # the group sums after the B * nt tile slots
-                    ng = gp[1].numel() // b_
-                    gp = gp[0][gp[0].numel() - b_ * ng * 4096:]
-                st.parts[i], st.coef[i] = ops.style_loss_from_parts(
-                    gp, gp.numel() // (b_ * 4096), b_, c_, z[0, 0].numel(),
-                    targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
-                    coef=st.coef[i], defer_ws=st.lws[i], fin=fin)
-            else:
-                st.parts[i], st.coef[i] = ops.style_loss(
-                    z, targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
-                    coef=st.coef[i], z_amax=slot(st.amax, l + 1) if split else None,
-                    defer_ws=st.lws[i], fin=fin)
-            if l == CONTENT_CONV:  # content, feature, feature-mse: one pass
-                ops.mse(z, c4, mode=2, out=st.losses[5:8])
+            njobs = len(fin.jobs) if fin is not None else 0
+            tap_loss(i, l, z, b_, c_, fuse_mse)
+            if i in COEF_AMAX_SLOT and fin is not None and len(fin.jobs) == njobs + 1 and \
+                    os.environ.get("STX_P2_SPLIT", "1") != "0":
+                # the batched finalize also writes max|A| of the taps whose Gram backward
+                # runs inside a data-gradient conv: that phase's split-MFMA A scale
+                st.coef_amax[i] = slot(st.amax, COEF_AMAX_SLOT[i])
+                fin.jobs[-1].coef_amax = st.coef_amax[i].data_ptr()
 
     st.z = feat.forward(x, 5, st.z if st.z else None, amax=st.amax, pools=st.pools,
                         on_layer=on_layer, grams=st.grams)
@@ -336,6 +349,11 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
 
 
 _SIDE = {}
+
+
+# amax groups of LossState.amax: 0..5 forward, 6..10 backward split-conv inputs, 11 / 12
+# max|A| of the taps whose Gram backward is a data-gradient conv's second phase
+COEF_AMAX_SLOT = {0: 11, 2: 12}
 
 
 def slot(amax, k):
@@ -379,7 +397,7 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
 
     folded = st.folded
     s = (lambda i: None) if folded else (lambda i: g[i:i + 1])
-    am = st.amax  # slots 0..5: forward; 6..10: backward split-conv inputs
+    am = st.amax  # slots 0..5: forward; 6..10: backward split-conv inputs; COEF_AMAX_SLOT
     # conv3_1 output: dZ5 = A5 Z5
     sp = feat.wt16[1] is not None  # split kernels in use
     dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4),
@@ -400,9 +418,10 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
             ops.diff_scale(z[3], st.c4, 4.0 / (float(n) * float(n)), s1=g[6:7],
                            s2=st.fmean[1:2], relu=True, out=dz4, accumulate=True)
     # dZ3 = conv2_2^T(dZ4)*[Z3>0] + A3 Z3
+    ca = st.coef_amax if st.coef_amax else [None] * 5
     dz3 = feat.dgrad(3, dz4, buf("dz3", z[2].shape), mask=z[2], p2_z=z[2],
                      p2_coef=st.coef[2], p2_scale=s(2), in_amax=dz4_amax, out_amax=slot(am, 8),
-                     p2_amax=slot(am, 3))
+                     p2_amax=slot(am, 3), p2_wt_amax=ca[2])
     # -> grad wrt pool(relu Z2)
     n2 = (B, 64, z[1].shape[2] // 2, z[1].shape[3] // 2)
     dp1 = feat.dgrad(2, dz3, buf("dp1", n2), in_amax=slot(am, 8))
@@ -411,7 +430,7 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
     # dZ1 = conv1_2^T(dZ2)*[Z1>0] + A1 Z1
     dz1 = feat.dgrad(1, dz2, buf("dz1", z[0].shape), mask=z[0], p2_z=z[0],
                      p2_coef=st.coef[0], p2_scale=s(0), in_amax=slot(am, 9), p2_amax=slot(am, 1),
-                     out_amax=slot(am, 10) if sp else None)
+                     out_amax=slot(am, 10) if sp else None, p2_wt_amax=ca[0])
     # conv1_1 dgrad -> image (64 -> 3 GEMM + col2im; on the split MFMA given max|dZ1|)
     xs = (B, 3, z[0].shape[2], z[0].shape[3])
     if dx is None:

@@ -198,6 +198,46 @@ def test_split_conv_fused_epilogue_large(dev, shape, scaled):
     assert float(am.max()) == float(out.abs().max())
 
 
+@pytest.mark.parametrize("shape", [(1, 64, 512, 512), (1, 128, 256, 256), (2, 64, 160, 300),
+                                   (4, 64, 128, 128), (1, 64, 20, 34)])
+@pytest.mark.parametrize("scaled", [False, True])
+def test_split_phase2_precomputed_scale(dev, shape, scaled):
+    """The Gram-backward phase on the fp16 split MFMA with A's scale precomputed by the
+    batched Gram finalize (stx_gram_fin_job.coef_amax -> stx_conv_params.p2_wt_amax, the
+    Gatys dZ1 / dZ3 launches): the finalize's amax is max|A| exactly, and the data gradient
+    matches the fp32-MFMA phase (ragged width 34: the per-pixel z2 loads)."""
+    n, c, h, w = shape
+    z = rnd(n, c, h, w, dev=dev, seed=291, scale=2, shift=-1)
+    dy = rnd(n, c, h, w, dev=dev, seed=292, scale=2e-3, shift=-1e-3)
+    wgt = rnd(c, c, 3, 3, dev=dev, seed=293, scale=0.2, shift=-0.1)
+    t = rnd(n, c, c, dev=dev, seed=294)
+    ws = torch.empty(N.lib().stx_gram_ws(n, c, h * w), device=dev, dtype=torch.uint8)
+    fin = ops.FinalizeBatch()
+    _, coef = ops.style_loss(z, t, weight=2.0, diag_alpha=1e-3, defer_ws=ws, fin=fin)
+    ca = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    assert len(fin.jobs) == 1
+    fin.jobs[0].coef_amax = ca.data_ptr()
+    fin.flush()
+    torch.cuda.synchronize()
+    assert float(ca.max()) == float(coef.abs().max())
+    s2 = torch.tensor(-0.375, device=dev) if scaled else None
+    wtT = ops.conv_weight_prep(wgt, transpose=True)
+    w16 = ops.conv_weight_prep16(wgt, transpose=True)
+    am = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    out = ops.conv2d(dy, wtT, c, c, 3, mask=z, p2_z=z, p2_coef=coef, p2_scale=s2, wt16=w16,
+                     out_amax=am, p2_wt_amax=ca)
+    out32 = ops.conv2d(dy, wtT, c, c, 3, mask=z, p2_z=z, p2_coef=coef, p2_scale=s2)
+    # repeated launches give the same bits (a staging race showed up only as run-to-run
+    # differences in the last 16 couts of a tile, two blocks per CU)
+    reps = [ops.conv2d(dy, wtT, c, c, 3, mask=z, p2_z=z, p2_coef=coef, p2_scale=s2, wt16=w16,
+                       p2_wt_amax=ca) for _ in range(3)]
+    torch.cuda.synchronize()
+    assert rel(out, out32) < 2e-6, rel(out, out32)
+    assert float(am.max()) == float(out.abs().max())
+    for r in reps:
+        assert torch.equal(r, out)
+
+
 @pytest.mark.parametrize("mode", [N.STX_IN_RELU, N.STX_IN_RELU_POOL2, N.STX_IN_UPSAMPLE2])
 def test_split_conv_phase2_needs_raw_input(dev, mode):
     """The fused Gram-backward phase exists only for raw-input data gradients: any
