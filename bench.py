@@ -62,6 +62,7 @@ PEAK_HBM_GBS = 8000.0
 # WRITE_SIZE passes of tools/pmc_r3.sh over an eager Gatys iteration, calibrated on
 # kernels of known byte count: tools/pmc_r3_summary.py -> profiles/r4_pmc.json, the
 # passes over the current build)
+DG_KERNEL = "conv3x3_f16x3_v2_kernel<64, 0, {}, 2, 1>"
 ROOFLINE_KERNEL = "conv3x3_f16x3_v2_kernel<64, 1, 0, 2, 1>"
 ROOFLINE_MATCH = ROOFLINE_KERNEL
 PMC_FILE = os.path.join(REPO, "profiles", "r4_pmc.json")
@@ -242,13 +243,21 @@ def gatys_leg(args, world, rank, dev):
 
     dz2_am, z1_am = ops.amax(sc["dz2"]), ops.amax(st.z[0])
 
+    # (the split phase's A scale: the group the batched finalize wrote, when it did)
+    ca = st.coef_amax[0] if st.coef_amax else None
+
     def dgrad12():
         return feat.dgrad(1, sc["dz2"], dz1, mask=st.z[0], p2_z=st.z[0], p2_coef=st.coef[0],
-                          p2_scale=None, in_amax=dz2_am, out_amax=am_b, p2_amax=z1_am)
+                          p2_scale=None, in_amax=dz2_am, out_amax=am_b, p2_amax=z1_am,
+                          p2_wt_amax=ca)
     dg_ms = event_avg_ms(dgrad12, reps=20)
     dg_gf = gf_conv + 2.0 * 64 * 64 * H * H / 1e9
     loss = float(eng.total)
+    # the kernel instance that launch takes (conv16.hip launch16v2): P2 = 3 the split
+    # phase, 1 the fp32-MFMA phase
+    p2 = 1 if ca is None or os.environ.get("STX_P2_SPLIT", "1") == "0" else 3
     return dict(rate=rate, dt=dt, loss=loss, run=run, kernel=dict(fwd_ms=fwd_ms, gflop=gf,
+                                                         dg_kernel=DG_KERNEL.format(p2),
                                                          gflop_conv=gf_conv, tflops=achieved,
                                                          gram_fused=gp is not None,
                                                          dg_ms=dg_ms, dg_gflop=dg_gf,
@@ -653,7 +662,7 @@ def main():
                 "iteration_tflops": round(GATYS_GFLOP.get(args.size, float("nan")) * g["rate"]
                                           / world / 1e3, 3),
                 "dominant_kernel": {
-                    "kernel": "conv3x3_f16x3_v2_kernel<64, 0, 1, 2, 1> (conv1_2 data gradient "
+                    "kernel": k["dg_kernel"] + " (conv1_2 data gradient "
                               f"@ {args.size}^2 with the fused Gram-backward phase: dZ1 = "
                               "[Z1 > 0] conv1_2^T(dZ2) + A1 Z1; the iteration's longest launch)",
                     "achieved": round(k["dg_tflops"], 3),

@@ -28,13 +28,14 @@ open(f"profiles/{tag}_gatys512_iteration_breakdown.txt", "w").write(
 out = [f"rocprofv3 --kernel-trace of the bench's Gatys legs (profiles/{tag}_bench_kernel_stats.csv):",
        "per-dispatch durations by grid (blocks x, y, z)",
        "kernel                                              grid            n   mean_us  median_us"]
-for K in ("conv3x3_f16x3_v2_kernel<64, 1, 0, 2, 1>", "conv3x3_f16x3_v2_kernel<64, 0, 1, 2, 1>"):
+for K in ("conv3x3_f16x3_v2_kernel<64, 1, 0, 2, 1>", "conv3x3_f16x3_v2_kernel<64, 0, 3, 2, 1>",
+          "conv3x3_f16x3_v2_kernel<64, 0, 1, 2, 1>"):
     by = {}
     for r in csv.DictReader(open(f"{G}/{tag}_prof/run_kernel_trace.csv")):
         if K in r["Kernel_Name"]:
             g = tuple(int(r[f"Grid_Size_{a}"]) // int(r[f"Workgroup_Size_{a}"]) for a in "XYZ")
             by.setdefault(g, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    for g, v in sorted(by.items(), key=lambda kv: -len(kv[1])):
+    for g, v in sorted(by.items(), key=lambda kv: -len(kv[1])):  # (absent variants: no rows)
         out.append(f"{K:50s} {str(g):15s} {len(v):4d} {statistics.mean(v):8.2f} {statistics.median(v):10.2f}")
 open(f"profiles/{tag}_bench_roofline_kernel.txt", "w").write("\n".join(out) + "\n")
 print("\n".join(out))
