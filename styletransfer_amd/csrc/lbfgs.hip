@@ -179,64 +179,69 @@ lb_commit_kernel(LbHdr* __restrict__ hdr, char* __restrict__ st, float* __restri
   scal[10] = hdr->H_diag;
 }
 
-// K3: per pair k (chronological) and block: s_k.g, y_k.g, s_k.y_new, y_k.y_new over the
-// block's 1024 elements (each lane 4 float4 of the chunk, 256 elements apart).  Wave w takes
-// the pairs k = w (mod 4), each over the WHOLE chunk; partials [k][q][block]
+// K3: u = S^T g, w = Y^T g and the new pair's column (s_k . y_new, y_k . y_new) in one
+// read of the history.  The block's four waves walk the pairs in the same order,
+// each thread one float4 of the block's chunk (the combine pass's access pattern: every
+// pair's chunk read as one contiguous 4 KB per vector), four pairs' loads in flight; a
+// pair's four sums are packed into one wave reduction (xor 32 and 16 exchange halves of
+// the quantities, then one 16-lane tree: 7 lane exchanges instead of 24) and kept in
+// LDS, and after the last pair the block adds its waves' values in wave order (per-block
+// partials for lb_dots_fin_kernel).  Round 4: a wave per pair subset with 16 values per
+// lane and one 64-lane tree per quantity took 125.9 us at history 100, this form 118.5
 __global__ void __launch_bounds__(LB_NT)
 lb_dots_kernel(const float* __restrict__ g, const float* __restrict__ hist, long long n,
                long long np, int m1, const LbHdr* __restrict__ hdr, float* __restrict__ parts) {
   const int count = hdr->count;
   if (count == 0) return;
+  __shared__ float wp[LB_NT / 64][LB_MAXM + 1][4];
   const int nb = (int)gridDim.x;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long long e0 = (long long)blockIdx.x * LB_CHUNK + 4 * lane;
-  const bool acc = hdr->accepted;
-  const float* __restrict__ ynp = hist + (size_t)(m1 + hdr->order[count - 1]) * np;
-  f32x4 gv[4], yn[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const long long e = e0 + 256 * u;
-    gv[u] = ld4g(g, e, n);
-    yn[u] = acc ? *reinterpret_cast<const f32x4*>(ynp + e) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  const long long e = (long long)blockIdx.x * LB_CHUNK + 4 * threadIdx.x;
+  const f32x4 gv = ld4g(g, e, n);
+  const f32x4 yn = hdr->accepted
+                       ? *reinterpret_cast<const f32x4*>(hist + (size_t)(m1 + hdr->order[count - 1]) * np + e)
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
   auto dot4 = [](f32x4 a, f32x4 b) {
     return fmaf(a[3], b[3], fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0])));
   };
-  // pair k+4's loads are issued before pair k's sums (unconditional: the index is clamped,
-  // so the wait before the sums covers exactly one pair's loads)
-  f32x4 sv[4], yv[4], sn[4], ynx[4];
-  auto load_pair = [&](int kk, f32x4 (&a)[4], f32x4 (&b)[4]) {
+  constexpr int PF = 4;
+  f32x4 sv[PF], yv[PF];
+  auto load_pair = [&](int kk, f32x4& a, f32x4& b) {  // (clamped: unconditional loads)
     const int sl = hdr->order[min(kk, count - 1)];
-    const float* __restrict__ sp = hist + (size_t)sl * np;
-    const float* __restrict__ yp = hist + (size_t)(m1 + sl) * np;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a[u] = *reinterpret_cast<const f32x4*>(sp + e0 + 256 * u);
-      b[u] = *reinterpret_cast<const f32x4*>(yp + e0 + 256 * u);
-    }
+    a = *reinterpret_cast<const f32x4*>(hist + (size_t)sl * np + e);
+    b = *reinterpret_cast<const f32x4*>(hist + (size_t)(m1 + sl) * np + e);
   };
-  if (w < count) load_pair(w, sv, yv);
-  for (int k = w; k < count; k += 4) {
-    load_pair(k + 4, sn, ynx);
-    float d[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      d[0] += dot4(sv[u], gv[u]);
-      d[1] += dot4(yv[u], gv[u]);
-      d[2] += dot4(sv[u], yn[u]);
-      d[3] += dot4(yv[u], yn[u]);
+  for (int i = 0; i < PF; ++i) load_pair(i, sv[i], yv[i]);
+  const bool hi32 = lane >= 32, hi16 = (lane & 16) != 0;
+  for (int k0 = 0; k0 < count; k0 += PF) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int k = k0 + i;
+      if (k < count) {
+        const float d0 = dot4(sv[i], gv), d1 = dot4(yv[i], gv);
+        const float d2 = dot4(sv[i], yn), d3 = dot4(yv[i], yn);
+        load_pair(k + PF, sv[i], yv[i]);
+        // lanes < 32 keep quantities 0, 1; lanes >= 32 keep 2, 3
+        const float r0 = __shfl_xor(hi32 ? d0 : d2, 32, 64);
+        const float r1 = __shfl_xor(hi32 ? d1 : d3, 32, 64);
+        const float v0 = (hi32 ? d2 : d0) + r0, v1 = (hi32 ? d3 : d1) + r1;
+        // then lane bit 4 picks one of the two: quantity 2 * hi32 + hi16
+        const float r = __shfl_xor(hi16 ? v0 : v1, 16, 64);
+        float v = (hi16 ? v1 : v0) + r;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((lane & 15) == 0) wp[w][k][2 * hi32 + hi16] = v;
+      }
     }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4 * count; i += LB_NT) {
+    const int k = i >> 2, q = i & 3;
+    float t = wp[0][k][q];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] = wave_sum(d[q]);
-    if (lane == 0) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) parts[((size_t)k * 4 + q) * nb + blockIdx.x] = d[q];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      sv[u] = sn[u];
-      yv[u] = ynx[u];
-    }
+    for (int ww = 1; ww < LB_NT / 64; ++ww) t += wp[ww][k][q];
+    parts[((size_t)k * 4 + q) * nb + blockIdx.x] = t;
   }
 }
 
