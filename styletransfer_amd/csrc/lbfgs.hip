@@ -179,12 +179,42 @@ lb_commit_kernel(LbHdr* __restrict__ hdr, char* __restrict__ st, float* __restri
   scal[10] = hdr->H_diag;
 }
 
+// Lane exchanges without the LDS pipe (gfx950 v_permlane*_swap, DPP).  swap_sum<32>(a, c):
+// a + (a of lane + 32) in lanes < 32, (c of lane - 32) + c in lanes >= 32 -- the swap
+// trades the upper half of its first operand for the lower half of its second, and the
+// two results always hold the lane's own value and its partner's, in either order.
+// swap_sum<16>: the same between rows 0/1 and 2/3.
+template <int H>
+__device__ __forceinline__ float swap_sum(float a, float c) {
+  const auto r = H == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(c),
+                                                            false, false)
+                         : __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(c),
+                                                            false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// the sum of a 16-lane row in every lane of it: quad swaps, then the half-row and row
+// mirrors pair each lane with one of the other half (every lane adds the same two values)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
+}
+
 // K3: u = S^T g, w = Y^T g and the new pair's column (s_k . y_new, y_k . y_new) in one
 // read of the history.  The block's four waves walk the pairs in the same order,
 // each thread one float4 of the block's chunk (the combine pass's access pattern: every
 // pair's chunk read as one contiguous 4 KB per vector), four pairs' loads in flight; a
-// pair's four sums are packed into one wave reduction (xor 32 and 16 exchange halves of
-// the quantities, then one 16-lane tree: 7 lane exchanges instead of 24) and kept in
+// pair's four sums are packed into one wave reduction (the 32- and 16-lane swaps trade
+// halves of the quantities, then one 16-lane DPP tree: 7 register-only exchanges instead
+// of 24 LDS-pipe permutes) and kept in
 // LDS, and after the last pair the block adds its waves' values in wave order (per-block
 // partials for lb_dots_fin_kernel).  Round 4: a wave per pair subset with 16 values per
 // lane and one 64-lane tree per quantity took 125.9 us at history 100, this form 118.5
@@ -213,7 +243,6 @@ lb_dots_kernel(const float* __restrict__ g, const float* __restrict__ hist, long
   };
 #pragma unroll
   for (int i = 0; i < PF; ++i) load_pair(i, sv[i], yv[i]);
-  const bool hi32 = lane >= 32, hi16 = (lane & 16) != 0;
   for (int k0 = 0; k0 < count; k0 += PF) {
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
@@ -222,16 +251,11 @@ lb_dots_kernel(const float* __restrict__ g, const float* __restrict__ hist, long
         const float d0 = dot4(sv[i], gv), d1 = dot4(yv[i], gv);
         const float d2 = dot4(sv[i], yn), d3 = dot4(yv[i], yn);
         load_pair(k + PF, sv[i], yv[i]);
-        // lanes < 32 keep quantities 0, 1; lanes >= 32 keep 2, 3
-        const float r0 = __shfl_xor(hi32 ? d0 : d2, 32, 64);
-        const float r1 = __shfl_xor(hi32 ? d1 : d3, 32, 64);
-        const float v0 = (hi32 ? d2 : d0) + r0, v1 = (hi32 ? d3 : d1) + r1;
-        // then lane bit 4 picks one of the two: quantity 2 * hi32 + hi16
-        const float r = __shfl_xor(hi16 ? v0 : v1, 16, 64);
-        float v = (hi16 ? v1 : v0) + r;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if ((lane & 15) == 0) wp[w][k][2 * hi32 + hi16] = v;
+        // lanes < 32 end with quantities 0, 1, lanes >= 32 with 2, 3; then rows 0..3 with
+        // quantity 0..3; then the 16-lane tree
+        const float v0 = swap_sum<32>(d0, d2), v1 = swap_sum<32>(d1, d3);
+        const float v = row_sum16(swap_sum<16>(v0, v1));
+        if ((lane & 15) == 0) wp[w][k][lane >> 4] = v;
       }
     }
   }
