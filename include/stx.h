@@ -140,6 +140,11 @@ typedef struct stx_conv_params {
 #define STX_GRAM_GROUP 8
 
 int stx_version(void);
+/* sizeof and the offset of the last member of each ABI struct, in this order:
+ * stx_conv_params, stx_wprep_job, stx_loss_parts, stx_gram_fin_job, stx_in_pgrad_job,
+ * stx_image_meta -- 12 values, min(n, 12) written to out; returns 12.  Bindings check
+ * their struct mirrors against it. */
+int stx_abi_layout(long long* out, int n);
 const char* stx_last_error_string(void);
 
 /* Padded GEMM dims the conv kernels expect for a (cin, cout, ks) conv. */

@@ -86,6 +86,7 @@ STX_FIN_MAX = 8
 # name -> (restype, argtypes); every symbol include/stx.h declares
 SIGNATURES = {
     "stx_version": (i32, []),
+    "stx_abi_layout": (i32, [vp, i32]),
     "stx_last_error_string": (C.c_char_p, []),
     "stx_conv_weight_dims": (i32, [i32, i32, i32, C.POINTER(i32), C.POINTER(i32)]),
     "stx_conv_weight_prep": (i32, [vp, vp, i32, i32, i32, i32, vp]),

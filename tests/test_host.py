@@ -25,6 +25,21 @@ def test_library_exports_header_symbols():
     assert decl == set(N.SIGNATURES), decl ^ set(N.SIGNATURES)
 
 
+def test_struct_mirrors_match_the_library():
+    """Every ctypes mirror has the size and last-member offset the compiled library has
+    (stx_abi_layout): a member added to include/stx.h but not to _native.py, or the other
+    way round, fails here instead of shifting fields on the GPU."""
+    import ctypes as C
+    from styletransfer_amd import _native as N
+    out = (C.c_longlong * 12)()
+    assert N.lib().stx_abi_layout(C.cast(out, C.c_void_p), 12) == 12
+    mirrors = [(N.ConvParams, "p2_wt_amax"), (N.WprepJob, "pad_"), (N.LossParts, "k"),
+               (N.GramFinJob, "coef_amax"), (N.PGradJob, "pad_"), (N.ImageMeta, "tmp_offset")]
+    for i, (S, last) in enumerate(mirrors):
+        assert S._fields_[-1][0] == last, S
+        assert (C.sizeof(S), getattr(S, last).offset) == (out[2 * i], out[2 * i + 1]), S
+
+
 def test_host_queries_without_gpu():
     from styletransfer_amd import ops
     assert ops.conv_weight_dims(3, 64, 3) == (4, 64)
