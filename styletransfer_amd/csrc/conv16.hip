@@ -226,9 +226,10 @@ __device__ __forceinline__ void phase2_f16(f32x16 (&acc)[2][2], const stx_conv_p
       for (int r = 0; r < 16; ++r) acc[i][j][r] *= down;
 }
 
-// Split Gram-backward phase of the v2 data-gradient conv (P2 = 3): acc -- already
-// de-scaled, *acc_scale, ReLU-masked and brought to the power-of-two scale S = 2^ls --
-// gets + S * s2 * A[n] . z2 on the fp16 hi/lo MFMA with every scale precomputed: z2 by
+// Split Gram-backward phase of the v2 data-gradient conv (P2 = 3): acc -- de-scaled,
+// *acc_scale, ReLU-masked and brought to the power-of-two scale S = 2^ls by `prologue`,
+// which runs once chunk 0's loads are issued -- gets + S * s2 * A[n] . z2 on the fp16
+// hi/lo MFMA with every scale precomputed: z2 by
 // its amax group (p2_amax: sz = 2^(15 - ez)), A' = s2 * A by the batch max the Gram
 // finalize wrote (p2_wt_amax: sa = S / sz <= 2^(15 - ea)).  No in-kernel reductions: the
 // round-3 port of phase2_f16 paid two block-wide max passes and a re-read of A for its
@@ -237,9 +238,10 @@ __device__ __forceinline__ void phase2_f16(f32x16 (&acc)[2][2], const stx_conv_p
 // fragment registers (no LDS round trip); 3 MFMAs per 32 x 32 tile (the fp32 phase:
 // 8 x 32x32x2 f32, 5x the MFMA cycles); the next chunk's loads are in flight during the
 // MFMAs.
-template <int TW, bool RP>
+template <int TW, bool RP, class Prologue>
 __device__ __forceinline__ void phase2_pre(f32x16 (&acc)[2][2], const stx_conv_params& p,
-                                           const EpiTile& t, int ls, int ez, char* smem) {
+                                           const EpiTile& t, int ls, int ez, char* smem,
+                                           Prologue&& prologue) {
   constexpr int NPIX = 256;
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x, h = t.h, l32 = t.l32;
@@ -322,6 +324,7 @@ __device__ __forceinline__ void phase2_pre(f32x16 (&acc)[2][2], const stx_conv_p
   };
   Stage g;
   fetch(0, g);
+  prologue();  // the caller's scaling and mask, with chunk 0's loads in flight
   for (int c0 = 0; c0 < C2; c0 += 16) {
     __syncthreads();  // the previous chunk's (or the main loop's) LDS reads done
     stage(g);
@@ -888,21 +891,25 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
       const int eacc = ex + ew + (32 - __builtin_clz(9 * rup(p.cin, 16))) + 1 +
                        amax_exp(p.acc_scale ? fabsf(*p.acc_scale) : 1.f);
       const int ls = max(min(min(30 - ea - ez, 100 - eacc), 120), -100);
+      // de-scale, *acc_scale, ReLU mask, bring to 2^ls: run by the phase once its first
+      // chunk's loads are in flight (the mask loads and those overlap)
+      auto prologue = [&]() {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
+          for (int j = 0; j < NI; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] *= descale;
-      epi_scale_mask<TW, RP, NI>(acc, p, et);
-      const float up = __builtin_ldexpf(1.f, ls);
+            for (int r = 0; r < 16; ++r) acc[i][j][r] *= descale;
+        epi_scale_mask<TW, RP, NI>(acc, p, et);
+        const float up = __builtin_ldexpf(1.f, ls);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
+          for (int j = 0; j < NI; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] *= up;
-      phase2_pre<TW, RP>(acc, p, et, ls, ez, smem);
+            for (int r = 0; r < 16; ++r) acc[i][j][r] *= up;
+      };
+      phase2_pre<TW, RP>(acc, p, et, ls, ez, smem, prologue);
       conv_epilogue_plain_body<TW, NI, RP, false>(acc, p, et, __builtin_ldexpf(1.f, -ls), smem);
     } else if constexpr (P2 == 1) {
       conv_epilogue<BM, TW, C::NPIX, 16, RP, NI, true>(acc, p, et, descale,
