@@ -162,6 +162,30 @@ def event_avg_ms(fn, reps=10):
     return e0.elapsed_time(e1) / reps
 
 
+def box_calibration(dev):
+    """Per-box calibration, timed in this process before the legs (box-to-box
+    spread of ~7 % is larger than a round's kernel gains): a fixed fp16 GEMM on the MFMA
+    pipes (8192^3 through torch.matmul = hipBLASLt, TF/s) and a 1 GiB device-to-device
+    copy (read + write bytes, GB/s).  A driver number divided by these separates "the
+    kernels got faster" from "the box is faster"."""
+    n = 8192
+    a = torch.randn(n, n, device=dev, dtype=torch.float16)
+    b = torch.randn(n, n, device=dev, dtype=torch.float16)
+    c = torch.empty(n, n, device=dev, dtype=torch.float16)
+    mm_ms = min(event_avg_ms(lambda: torch.matmul(a, b, out=c), reps=10) for _ in range(3))
+    del a, b, c
+    src = torch.empty(1 << 28, device=dev, dtype=torch.float32)
+    src.fill_(1.0)
+    dst = torch.empty_like(src)
+    cp_ms = min(event_avg_ms(lambda: dst.copy_(src), reps=10) for _ in range(3))
+    nbytes = 2 * src.numel() * 4
+    del src, dst
+    return {"fp16_gemm_tflops": round(2.0 * n ** 3 / (mm_ms * 1e-3) / 1e12, 1),
+            "hbm_copy_gbs": round(nbytes / (cp_ms * 1e-3) / 1e9, 1),
+            "note": "fp16 8192^3 torch.matmul (hipBLASLt) and a 1 GiB torch copy_ (2 GiB "
+                    "moved), HIP events, best of 3 x 10; same process, before the legs"}
+
+
 def gatys_leg(args, world, rank, dev):
     H = args.size
     style = torch.from_numpy(W.synthetic_image(1000 + rank, (1, 3, H, H))).to(dev)
@@ -448,8 +472,12 @@ def convert_leg(args, world, rank, dev):
             print(f"convert leg: graph capture failed ({e}); eager rate reported", file=sys.stderr)
             dt, same = dt_eager, None
     gf = itn_forward_gflop(H, H) * B
+    graph_rate = world * B * n / dt
+    if same is False:  # a capture that changes the output is not a speed-up: eager rate
+        print("convert leg: graph output != eager output; eager rate reported", file=sys.stderr)
+        dt = dt_eager
     return dict(rate=world * B * n / dt, dt=dt, steps=n, batch=B, eager_rate=world * B * n / dt_eager,
-                gflop=gf, tflops=gf * n / dt / 1e3, graph_equals_eager=same)
+                graph_rate=graph_rate, gflop=gf, tflops=gf * n / dt / 1e3, graph_equals_eager=same)
 
 
 def _host_cpu():
@@ -596,6 +624,7 @@ def main():
             print(json.dumps({"fast_st_images_per_s": round(fs["rate"], 3),
                               "ms_per_step": round(1e3 * fs["dt"] / fs["steps"], 3)}))
         return
+    box = box_calibration(dev)
     g = gatys_leg(args, world, rank, dev)
     lb = gatys_lbfgs_leg(args, world, rank, dev) if args.lbfgs_steps > 0 else None
     fs = None if args.skip_fast else fast_st_leg(args, world, rank, dev)
@@ -696,6 +725,7 @@ def main():
                         "MFMA fraction counts the 3 fp16 products per fp32 product",
             },
             "cpu_baseline": cpu,
+            "box": box,
             "gatys_loss": g["loss"],
         }
         if g["run"]:
@@ -768,6 +798,7 @@ def main():
                 "value": round(conv["rate"], 2), "unit": "images/s", "batch": conv["batch"],
                 "ms_per_batch": round(1e3 * conv["dt"] / conv["steps"], 3),
                 "steps": conv["steps"], "eager_value": round(conv["eager_rate"], 2),
+                "graph_value": round(conv["graph_rate"], 2),
                 "gflop_per_batch": round(conv["gflop"], 2),
                 "tflops": round(conv["tflops"], 1),
                 "split_peak_frac": round(conv["tflops"] / PEAK_SPLIT_TFLOPS, 4),

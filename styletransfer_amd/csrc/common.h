@@ -81,6 +81,19 @@ __device__ __forceinline__ int amax_exp(float a) {
   return min(max(e, -60), 60);
 }
 
+// A/B switches for measurement builds only.  The product library is built without STX_AB:
+// every switch is its default, a compile-time constant, so no environment variable can
+// change which kernel runs (and no variable name is left in the library).  `make AB=1`
+// builds the measurement library, in which STX_KNOB reads the named integer variable.
+#ifdef STX_AB
+}  // namespace stx
+#include <cstdlib>
+namespace stx {
+#define STX_KNOB(name, dflt) ([] { const char* e_ = getenv(name); return e_ ? atoi(e_) : (dflt); }())
+#else
+#define STX_KNOB(name, dflt) (dflt)
+#endif
+
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ inline int rup(int a, int b) { return cdiv(a, b) * b; }
 

@@ -469,10 +469,7 @@ static int launch_smallc(const stx_conv_params& p, hipStream_t st) {
   dim3 grid(tiles_x * tiles_y, 1, p.n);
   constexpr int CIS = KS == 9 ? 4 : 8;
   if constexpr (KS == 3) {
-    static const int cfg = [] {
-      const char* e = getenv("STX_SMALLC");
-      return e ? atoi(e) : 0;
-    }();
+    static const int cfg = STX_KNOB("STX_SMALLC", 0);
     if (cfg == 1) {
       const int ty = cdiv(p.ho, 4);
       hipLaunchKernelGGL((conv_smallc_kernel<KS, 4, 4, 4>), dim3(tiles_x * ty, 1, p.n),
@@ -497,10 +494,7 @@ static int launch_smallc(const stx_conv_params& p, hipStream_t st) {
       return check_launch("stx_conv2d(smallc)");
     }
   }
-  static const bool c3 = [] {
-    const char* e = getenv("STX_SMALLC_C3");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool c3 = STX_KNOB("STX_SMALLC_C3", 1) != 0;
   if (p.cout == 3 && c3)  // the ITN's final conv: no idle fourth output channel
     hipLaunchKernelGGL((conv_smallc_kernel<KS, CIS, TH, 2, 3>), grid, dim3(2 * 16 * TH), 0, st,
                        p, tiles_x);
@@ -730,10 +724,7 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     return STX_E_INVALID;
   }
   {  // 3 input channels (VGG conv1_1, ITN conv0, conv22's data gradient)
-    static const bool few_off = [] {
-      const char* e = getenv("STX_FEWIN");
-      return e && atoi(e) == 0;
-    }();
+    static const bool few_off = STX_KNOB("STX_FEWIN", 1) == 0;
     int rc = few_off ? -1 : conv2d_conv9(p, st);  // the ITN's 9x9 layers, split MFMA
     if (rc >= 0) return rc;
     rc = few_off ? -1 : conv2d_fewin(p, st);

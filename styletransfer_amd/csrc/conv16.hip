@@ -936,18 +936,12 @@ static int cus16() {  // compute units (the WM = 2 form pays only in a single ro
 }
 
 static bool wm2_on() {  // STX_V2_WM2=0: 64-cout blocks for every layer (A/B)
-  static const bool on = [] {
-    const char* e = getenv("STX_V2_WM2");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = STX_KNOB("STX_V2_WM2", 1) != 0;
   return on;
 }
 
 static bool p2_split_on() {  // STX_P2_SPLIT=0: the fp32-MFMA phase even given p2_wt_amax (A/B)
-  static const bool on = [] {
-    const char* e = getenv("STX_P2_SPLIT");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = STX_KNOB("STX_P2_SPLIT", 1) != 0;
   return on;
 }
 

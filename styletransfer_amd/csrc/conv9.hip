@@ -464,18 +464,10 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
 }
 
 bool conv9_on() {
-  static const bool on = [] {
-    const char* e = getenv("STX_CONV9");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = STX_KNOB("STX_CONV9", 1) != 0;
   return on;
 }
 
-
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 
 int persistent_grid(int ntiles, int per_cu) {
   static int cus = [] {
@@ -485,7 +477,7 @@ int persistent_grid(int ntiles, int per_cu) {
       n = 256;
     return n > 0 ? n : 256;
   }();
-  static const int over = env_int("STX_CONV9_GRID", 0);  // profiling override
+  static const int over = STX_KNOB("STX_CONV9_GRID", 0);  // profiling override
   return std::min(ntiles, over > 0 ? over : per_cu * cus);  // LDS-limited blocks per CU
 }
 

@@ -592,18 +592,12 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16t_kernel(stx_conv_params p
 }
 
 static bool few16t_on() {
-  static const bool on = [] {
-    const char* e = getenv("STX_FEW16T");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = STX_KNOB("STX_FEW16T", 1) != 0;
   return on;
 }
 
 static bool few16_on() {
-  static const bool on = [] {
-    const char* e = getenv("STX_FEW16");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = STX_KNOB("STX_FEW16", 1) != 0;
   return on;
 }
 

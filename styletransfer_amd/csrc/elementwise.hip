@@ -628,10 +628,7 @@ extern "C" int stx_tv_loss(const float* y, float* loss, float* grad, float gscal
 extern "C" size_t stx_bias_grad_ws(int n, int c) { return (size_t)n * c * sizeof(float) + 64; }
 
 static bool one_pass_bias() {  // STX_BIAS_ONEPASS=0: always the two-pass path (A/B)
-  static const bool on = [] {
-    const char* e = getenv("STX_BIAS_ONEPASS");
-    return e ? atoi(e) != 0 : true;
-  }();
+  static const bool on = STX_KNOB("STX_BIAS_ONEPASS", 1) != 0;
   return on;
 }
 

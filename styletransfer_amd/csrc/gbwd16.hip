@@ -586,14 +586,9 @@ static void launch_gb_v1(const Gb16& p, int nimg, hipStream_t st) {
 // C in {64, 128, 256} (256: no up_dp), h even, w % 16 == 0, dense channels; the caller
 // (stx_conv2d's split 1x1 mode) checks the rest of the contract.
 int gram_bwd16_launch(const Gb16& p, int nimg, int c, hipStream_t st) {
-  static const int nb_env = [] {
-    const char* e = getenv("STX_GB_NB");
-    return e ? atoi(e) : 0;
-  }();
-  static const bool v1 = [] {  // STX_GB_V1=1: the run-time-branch loop schedule (A/B)
-    const char* e = getenv("STX_GB_V1");
-    return e && atoi(e) != 0;
-  }();
+  static const int nb_env = STX_KNOB("STX_GB_NB", 0);
+  // STX_GB_V1=1: the run-time-branch loop schedule (A/B)
+  static const bool v1 = STX_KNOB("STX_GB_V1", 0) != 0;
   const bool two = (nb_env ? nb_env : 2) == 2 && p.w % 32 == 0;
   if (c == 64) {
     if (v1 || p.aux)

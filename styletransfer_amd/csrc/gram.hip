@@ -550,25 +550,17 @@ gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw,
 }
 
 static int gram_tri_splits(int c, int hw, int b) {
-  static const int target = [] {
-    const char* e = getenv("STX_GRAM_TRI_BLOCKS");
-    return e ? std::max(8, atoi(e)) : 256;  // C = 128 @ 256^2: 256 > 128 > 64 blocks (A/B)
-  }();
+  // C = 128 @ 256^2: 256 > 128 > 64 blocks (A/B)
+  static const int target = std::max(8, STX_KNOB("STX_GRAM_TRI_BLOCKS", 256));
   // ~target blocks over the whole batch (the partial slab grows with b * splits)
   return std::max(1, std::min(std::max(1, target / std::max(1, b)), hw / 64));
 }
 
 static bool gram_tri_on(int c, int hw) {
-  static const bool on = [] {
-    const char* e = getenv("STX_GRAM_TRI");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = STX_KNOB("STX_GRAM_TRI", 1) != 0;
   // C = 256 @ 128^2 measured slower than the 64 x 64-tile kernel (36 vs 10 blocks of
   // accumulators per block: 33-37 us vs 32 us with the finalize); STX_GRAM_TRI=2 forces it
-  static const bool all = [] {
-    const char* e = getenv("STX_GRAM_TRI");
-    return e && atoi(e) == 2;
-  }();
+  static const bool all = STX_KNOB("STX_GRAM_TRI", 1) == 2;
   return on && (c == 128 || (all && c == 256)) && hw % 64 == 0;
 }
 
@@ -793,10 +785,7 @@ static void gram_geometry(int c, int hw, int b, int& nsplit, int& split_len, int
 static void gram_geometry16(int c, int hw, int b, int& nsplit, int& split_len, int& ntu) {
   const int nt = cdiv(c, GT);
   ntu = nt * (nt + 1) / 2;
-  static const int target = [] {
-    const char* e = getenv("STX_GRAM_BLOCKS");
-    return e ? std::max(8, atoi(e)) : 640;
-  }();
+  static const int target = std::max(8, STX_KNOB("STX_GRAM_BLOCKS", 640));
   int want = rup(cdiv(target, ntu * b), 8);
   const int max_splits = std::max(1, cdiv(hw, 256));
   want = std::max(8, std::min(want, rup(max_splits, 8)));

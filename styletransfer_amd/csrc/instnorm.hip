@@ -551,9 +551,10 @@ instnorm_bwd_pipe_kernel(const float* __restrict__ dy, const float* __restrict__
 }
 
 static int in_ppb() {  // planes per block of the pipelined 64^2 kernels (1: one-plane kernels)
+  // 1, 2 or 4 (the launches below instantiate these; anything else means 1)
   static const int v = [] {
-    const char* e = getenv("STX_IN_PPB");
-    return e ? atoi(e) : 4;
+    const int k = STX_KNOB("STX_IN_PPB", 4);
+    return k == 2 || k == 4 ? k : 1;
   }();
   return v;
 }
@@ -727,10 +728,7 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
   hipStream_t st = (hipStream_t)stream;
   // 64^2 planes: 512 threads x 2 float4 per thread (fast_st 1801 -> 1811 img/s same box
   // against 256 x 4; 128 x 8 was 0.6 % slower); STX_IN_CFG=0 restores 256 x 4, 1 = 128 x 8
-  static const int cfg = [] {
-    const char* e = getenv("STX_IN_CFG");
-    return e ? atoi(e) : 2;
-  }();
+  static const int cfg = STX_KNOB("STX_IN_CFG", 2);
   if (cfg == 1 && hw % 4 == 0 && hw <= 4 * 128 * 8)
     hipLaunchKernelGGL((instnorm_fwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, x, res,
                        gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
@@ -738,7 +736,7 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
            n * c / in_ppb() >= 256 &&  // enough blocks to fill the chip (B = 8: 256)
            ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) |
              reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
-    const int ppb = in_ppb() >= 4 ? 4 : 2;
+    const int ppb = in_ppb();
     const dim3 grid(n * c / ppb);
 #define STX_IN_FWD_PIPE(P, R)                                                                   \
   hipLaunchKernelGGL((instnorm_fwd_pipe_kernel<512, 2, P, R>), grid, dim3(512), 0, st, x, res, \
@@ -768,10 +766,7 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
 }
 
 static bool greg_on() {
-  static const bool on = [] {
-    const char* e = getenv("STX_IN_GREG");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = STX_KNOB("STX_IN_GREG", 1) != 0;
   return on;
 }
 
@@ -796,16 +791,14 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
   const bool al = ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(y) |
                     reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) |
                     reinterpret_cast<uintptr_t>(du)) & 15) == 0 && hw % 4 == 0;
-  static const int cfg = [] {  // block shape of the 64^2 kernels, as stx_instnorm_fwd
-    const char* e = getenv("STX_IN_CFG");
-    return e ? atoi(e) : 2;
-  }();
+  // block shape of the 64^2 kernels, as stx_instnorm_fwd
+  static const int cfg = STX_KNOB("STX_IN_CFG", 2);
   if (cfg == 1 && al && hw <= 4 * 128 * 8)
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, dy, y, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else if (cfg == 2 && al && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0 &&
            n * c / in_ppb() >= 256) {
-    const int ppb = in_ppb() >= 4 ? 4 : 2;
+    const int ppb = in_ppb();
     const dim3 grid(n * c / ppb);
 #define STX_IN_BWD_PIPE(P, RL, R)                                                               \
   hipLaunchKernelGGL((instnorm_bwd_pipe_kernel<512, 2, P, RL, R>), grid, dim3(512), 0, st, dy, y, \

@@ -327,7 +327,9 @@ lb_solve_kernel(LbHdr* __restrict__ hdr, char* __restrict__ st, int m) {
   __syncthreads();
   if (hdr->accepted && k > 0) {
     const int nw = slot[k - 1];
-    const double dinv = 1.0 / SY[(size_t)nw * m1 + nw];
+    // d = s_n.y_n from the fp64 dots (vc[k-1], shared memory): the loop below overwrites
+    // SY's diagonal entry with the same value, so no lane may read SY[nw][nw] here
+    const double dinv = 1.0 / vc[k - 1];
     for (int i = threadIdx.x; i < k; i += LB_SOLVE_NT) {
       const int si = slot[i];
       SY[(size_t)si * m1 + nw] = vc[i];

@@ -621,10 +621,7 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
 }
 
 static bool wg16_lds_on() {
-  static const bool on = [] {
-    const char* e = getenv("STX_WG16_LDS");
-    return !(e && atoi(e) == 0);
-  }();
+  static const bool on = STX_KNOB("STX_WG16_LDS", 1) != 0;
   return on;
 }
 
@@ -632,20 +629,14 @@ static bool wg16_lds_on() {
 // than the register-direct kernel, 128 cins per block (cin % 128 == 0) 5 % slower on the
 // ITN up conv (188 vs 179 us, same box): off by default
 static bool lds_on_64() {
-  static const bool on = [] {
-    const char* e = getenv("STX_WG16_LDS64");
-    return e && atoi(e) != 0;
-  }();
+  static const bool on = STX_KNOB("STX_WG16_LDS64", 0) != 0;
   return on;
 }
 
 typedef void (*Wg16Kernel)(const float*, const float*, float*, const float*, const float*, Wg16);
 
 static int wg16_pf() {
-  static const int pf = [] {
-    const char* e = getenv("STX_WG16_PF");
-    return e ? atoi(e) : 4;
-  }();
+  static const int pf = STX_KNOB("STX_WG16_PF", 4);
   return pf;
 }
 
@@ -653,10 +644,7 @@ static int wg16_pf() {
 static Wg16Kernel wg16_kernel(const Wg16& g) {
   if (g.lds) {
     const bool up = g.mode == STX_IN_UPSAMPLE2;
-    static const int lpf = [] {
-      const char* e = getenv("STX_WG16_LPF");
-      return e ? atoi(e) : 3;
-    }();
+    static const int lpf = STX_KNOB("STX_WG16_LPF", 3);
     if (g.cout == 128)
       return up ? wgrad16_lds_kernel<4, true, 3>
                 : (lpf >= 7 ? wgrad16_lds_kernel<4, false, 7>
@@ -713,10 +701,8 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   g.mode = in_mode;
   g.hv = hv;
   g.wv = wv;
-  static const bool ci2_on = [] {  // STX_WG16_CI2=0: the 64 x 32 tiling for every cout
-    const char* e = getenv("STX_WG16_CI2");
-    return e ? atoi(e) != 0 : true;
-  }();
+  // STX_WG16_CI2=0: the 64 x 32 tiling for every cout
+  static const bool ci2_on = STX_KNOB("STX_WG16_CI2", 1) != 0;
   g.ci2 = ci2_on && cout <= 32 && in_mode != WG16_S2;
   if (g.ci2) {  // 32 couts x two 32-cin tiles per wave (no all-zero second cout tile)
     g.ncot = 1;
@@ -741,10 +727,7 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   }
   // K splits: as many as fill whole rounds of resident blocks (a ragged last round of a
   // few blocks costs a full block duration: 513 blocks at 256 slots ran 3 rounds)
-  static const int rounds = [] {
-    const char* e = getenv("STX_WG16_ROUNDS");
-    return e ? std::max(1, atoi(e)) : 1;
-  }();
+  static const int rounds = std::max(1, STX_KNOB("STX_WG16_ROUNDS", 1));
   const int slots = rounds * wg16_slots(wg16_kernel(g));
   // blocks per split: (kh x cin tiles) for the LDS kernel; 4 units (waves) per block
   int ns = g.lds ? slots / (3 * g.ncit) : slots * 4 / (3 * g.ncot * g.ncit);

@@ -340,9 +340,8 @@ class StyleNetwork(nn.Module):
             eng = V.GatysLBFGS(self.features(), None, content_image.contiguous(),
                                style_weight, content_weight, targets=targets)
 
-            def log(loss):
-                if LOGGER.isEnabledFor(logging.DEBUG):
-                    LOGGER.debug("Loss: %s", loss)
+            def log(loss):  # a host float from the iteration's one read: no extra sync
+                LOGGER.info("Loss: %s", loss)  # stransfer/network.py:453 logs at INFO
             for _ in tqdm(range(steps)):
                 eng.step(on_eval=log)
             return eng.x.requires_grad_()
@@ -355,8 +354,8 @@ class StyleNetwork(nn.Module):
             total = (self.get_total_current_style_loss(weight=style_weight)
                      + self.get_total_current_content_loss(weight=content_weight))
             total.backward()
-            if LOGGER.isEnabledFor(logging.DEBUG):  # formatting a device tensor syncs
-                LOGGER.debug("Loss: %s", total)
+            if LOGGER.isEnabledFor(logging.INFO):  # formatting a device tensor syncs
+                LOGGER.info("Loss: %s", total)  # stransfer/network.py:453
             return total
 
         for _ in tqdm(range(steps)):

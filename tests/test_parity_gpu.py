@@ -297,8 +297,15 @@ def test_itn_forward_backward_golden(itn_case, dev, monkeypatch):
             continue
         errs.append((e64, r32, i))
         assert e64 <= max(2.5 * r32, 1e-5), (i, e64, r32)
+    # At this size every parameter is flip-affected: the fp32 reference's own run decides
+    # one loss-network branch differently from fp64 (pinned on CPU by
+    # tests/test_forced_ref_pin.py::test_golden_flip_sites), and a VGG flip moves every
+    # ITN gradient.  The tight fp32-class check of all 62 gradients is therefore the
+    # forced-branch one (test_itn_masks_gpu.py), whose fp64 ground truth (forced_ref.py)
+    # is itself pinned to itn_fp64.npz / itn.npz by test_forced_ref_pin.py.
     print("ITN grad error vs fp64 downstream of every flip (hip, fp32-ref, param):",
-          sorted(errs)[-3:], "flip-affected params:", len(flipped))
+          sorted(errs)[-3:], "flip-affected params:", len(flipped),
+          "HIP flips (ITN, VGG) vs fp64:", itn_flip_counts(hip_branches))
 
     with torch.no_grad():
         assert rel(net(batch[:1]), d["y_single"]) < 1e-4
@@ -322,6 +329,13 @@ def itn_flipped_params(hip_branches):
     n32 = R.natural_branches(sd, vgg, d["batch"], torch.float32)
     return (R.flip_upstream(keys, hip_branches[0], n64[0], hip_branches[1], n64[1])
             | R.flip_upstream(keys, n32[0], n64[0], n32[1], n64[1]))
+
+
+def itn_flip_counts(hip_branches):
+    d = g("itn")
+    n64 = R.natural_branches(W.itn_synthetic(4321), W.vgg19_synthetic(1234, 5), d["batch"],
+                             torch.float64)
+    return R.count_flips(hip_branches[0], n64[0]), R.count_flips(hip_branches[1], n64[1])
 
 
 def test_itn_adam_step_golden(itn_case, dev, monkeypatch):

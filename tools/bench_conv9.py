@@ -1,6 +1,6 @@
 """Microbenchmark of the few-channel convs: the 9x9 ITN layers (conv9.hip) at B=8 256^2
 (conv0 fwd 3->32, conv22 fwd 32->3 with a max|x| bound) and VGG conv1_1's data
-gradient (64->3 @ 512^2, convfew.hip), HIP events on the launch stream.  STX_CONV9_DBG selects the profiling variants."""
+gradient (64->3 @ 512^2, convfew.hip), HIP events on the launch stream."""
 import os
 import sys
 
@@ -35,7 +35,6 @@ def main():
     wt22 = ops.conv_weight_prep(w22)
     am = ops.amax(x32)
     gf = 2 * 32 * 3 * 81 * n * h * w / 1e9
-    tag = os.environ.get("STX_CONV9_DBG", "0")
     # VGG conv1_1's data gradient to the image (64 -> 3, 3x3 @ 512^2, convfew.hip)
     d1 = torch.randn(1, 64, 512, 512, generator=g).to(dev)
     w11 = (torch.randn(64, 3, 3, 3, generator=g) * 0.05).to(dev)
@@ -45,7 +44,7 @@ def main():
                      ("conv22 fwd 32->3", lambda: ops.conv2d(x32, wt22, 32, 3, 9, in_amax=am)),
                      ("vgg dgrad1_1 64->3", lambda: ops.conv2d(d1, wt11, 64, 3, 3, in_amax=am1))]:
         ms = ev(fn)
-        print(f"dbg={tag} {name:20s} {ms * 1e3:8.1f} us {gf / ms:7.1f} TF/s", flush=True)
+        print(f"{name:20s} {ms * 1e3:8.1f} us {gf / ms:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
