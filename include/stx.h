@@ -166,6 +166,22 @@ size_t stx_conv_weight16_bytes(int cin, int cout, int ks, int transpose);
  * stx_conv_weight_prep). */
 int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax, int cout, int cin, int ks,
                            int transpose, void* stream);
+/* The data-gradient split slab of a composed weight, for a Gram-backward operator that
+ * feeds a 3x3 conv's data gradient with nothing in between (VGG conv3_1: dZ5 = A5 Z5,
+ * then dP4 = conv3_1^T(dZ5); stransfer/network.py:92-123 StyleLoss backward through
+ * :264-314 the conv3_1 piece):  conv^T_w(A . z) = conv^T_{w'}(z) with
+ *   w'[c][ci][kh][kw] = s * sum_co A[c*pitch + co] * w[co][ci][kh][kw]   (s = *scale or 1)
+ * so the data gradient reads z directly and dZ = A z is never formed.  A is one image's
+ * [cout][pitch] operator (pitch >= cout; stx_style_loss's coef), a_amax an amax group
+ * >= max|A| (the finalize's coef_amax), w [cout][cin][3][3] with w_amax >= max|w|.  One
+ * launch writes the transposed split slab wtT16 (stx_conv_weight16_bytes(cin, cout, 3, 1)
+ * bytes) at the power-of-two scale of the bound |s| * cout * max|A| * max|w| >= max|w'|,
+ * and stores that bound into every slot of the group out_amax: the conv takes
+ * wt16 = wtT16, w_amax = out_amax.  cout <= 256, cin % 4 == 0, w 16-byte aligned; fixed
+ * summation order. */
+int stx_conv_weight_compose16(const float* A, int pitch, const float* a_amax, const float* w,
+                              const float* w_amax, int cout, int cin, const float* scale,
+                              void* wtT16, float* out_amax, void* stream);
 /* Both split slabs of one weight (forward and data gradient) and their shared w_amax in
  * two launches (one max pass, one conversion) -- a trained layer re-preps every step. */
 int stx_conv_weight_prep16_pair(const float* w, void* wt16, void* wtT16, float* w_amax,

@@ -96,6 +96,7 @@ SIGNATURES = {
     "stx_conv_weight16_bytes": (sz, [i32, i32, i32, i32]),
     "stx_conv_weight_prep16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv_weight_prep16_pair": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
+    "stx_conv_weight_compose16": (i32, [vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
     "stx_amax": (i32, [vp, i64, vp, vp]),
     "stx_conv_weight_prep_batch": (i32, [C.POINTER(WprepJob), i32, vp]),
     "stx_conv2d_wgrad_ws": (sz, [i32, i32, i32, i32, i32, i32, i32]),

@@ -1206,6 +1206,116 @@ __global__ void __launch_bounds__(256) weight_prep_batch_kernel(WprepJobs b) {
                        b.gin[j], b.gout[j], i0, step);
 }
 
+// ------------------------------------------------ composed data-gradient weights
+// W'[c][k] = s * sum_co A[c*pitch + co] * W[co][k]  (k = ci*9 + tap, K = cin*9): the 1x1
+// Gram-backward operator A folded into the next 3x3 conv's weights, so that
+//   conv^T_W(A . z) = conv^T_{W'}(z)
+// (stx_conv_weight_compose16), written straight into the data-gradient split slab.  The
+// split needs a power-of-two scale known before W' exists: the bound
+//   max|W'| <= |s| * C * max|A| * max|W|
+// (the producers' amax groups) -- a loose scale only moves hi/lo down the fp16 range (both
+// keep 11 bits; what a headroom of 2^k costs is the lo floor 2^-24, far below fp32
+// rounding of the sums).  Block = 16 rows c x 64 columns k, with A^T and the block's W
+// columns staged in LDS (every load in flight at once); wave w sums co in [64w, 64w + 64)
+// for all of them (lane: 4 rows x 4 columns), then wave 0 adds the four wave sums in wave
+// order (fixed order), splits and stores 8-B runs of the slab.
+constexpr int WC_R = 16, WC_K = 64;
+
+__global__ void __launch_bounds__(256)
+weight_compose16_kernel(const float* __restrict__ A, int pitch, const float* __restrict__ a_amax,
+                        const float* __restrict__ W, const float* __restrict__ w_amax, int C,
+                        int cin, const float* __restrict__ scale, _Float16* __restrict__ slab,
+                        float* __restrict__ out_amax) {
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  const int K = cin * 9;
+  __shared__ __attribute__((aligned(16))) float la[256][WC_R];  // A^T tile (C <= 256)
+  // W columns k0 .. k0 + 63; after the sums, the three wave partials (80 KB per block in
+  // all: two blocks per CU)
+  __shared__ __attribute__((aligned(16))) float lw[256][WC_K];
+  float (*red)[WC_R * WC_K] = reinterpret_cast<float (*)[WC_R * WC_K]>(&lw[0][0]);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c0 = blockIdx.y * WC_R, k0 = blockIdx.x * WC_K;
+  const float sc = scale ? *scale : 1.f;
+  const float bound = fabsf(sc) * (float)C * read_amax(a_amax) * read_amax(w_amax);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid < STX_AMAX_SLOTS) out_amax[tid] = bound;
+  const float sw = __builtin_ldexpf(1.f, 15 - amax_exp(bound));
+  {
+    // A rows c0 .. c0 + 15 (-> la, transposed) and the block's W columns [C][64] (-> lw):
+    // every load issued before the first LDS store (one exposed latency per block);
+    // unconditional descriptor loads (rows past C / columns past K read 0)
+    constexpr int NLD = 256 * WC_K / 4 / 256;  // W float4 per thread (C <= 256)
+    const auto ra = make_srd(A, (uint32_t)C * (uint32_t)pitch * 4u);
+    const auto rw = make_srd(W, (uint32_t)C * (uint32_t)K * 4u);
+    float av[WC_R];
+#pragma unroll
+    for (int r = 0; r < WC_R; ++r)
+      av[r] = buf_ld(ra, (c0 + r < C && tid < C) ? (uint32_t)((c0 + r) * pitch + tid) * 4u : BUF_OOB);
+    f32x4 v[NLD];  // (cin % 4 == 0: a float4 run of a row is all in or all out)
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+      const int f = tid + 256 * u, co = f >> 4, k = k0 + 4 * (f & 15);
+      v[u] = buf_ld4(rw, co < C && k < K ? (uint32_t)(co * K + k) * 4u : BUF_OOB);
+    }
+#pragma unroll
+    for (int r = 0; r < WC_R; r += 4)
+      *reinterpret_cast<f32x4*>(&la[tid][r]) = f32x4{av[r], av[r + 1], av[r + 2], av[r + 3]};
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+      const int f = tid + 256 * u;
+      *reinterpret_cast<f32x4*>(&lw[f >> 4][4 * (f & 15)]) = v[u];
+    }
+  }
+  __syncthreads();
+  const int r4 = 4 * (lane >> 4), q4 = 4 * (lane & 15);
+  const int kk = k0 + q4;
+  float acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
+  const int cb = 64 * wave, ce = min(C, cb + 64);
+#pragma unroll 8
+  for (int co = cb; co < ce; ++co) {
+    const f32x4 a4 = *reinterpret_cast<const f32x4*>(&la[co][r4]);
+    const f32x4 w4 = *reinterpret_cast<const f32x4*>(&lw[co][q4]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = fmaf(a4[a], w4[b], acc[a][b]);
+  }
+  __syncthreads();  // every wave's lw reads done (red aliases lw)
+  if (wave > 0) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) red[wave - 1][(r4 + a) * WC_K + q4 + b] = acc[a][b];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const int gout64 = rup(cin, 64);
+  // slab [ci'/16][tap][P][cg][co' < gout64][8] of the data-gradient GEMM:
+  // W_T[co' = ci][ci' = c][tap'] = W'[c][ci][2 - kh][2 - kw]
+  const int c = c0 + r4, chunk = c >> 4, cg = (c >> 3) & 1, e0 = c & 7;  // e0 in {0, 4}
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int k = kk + b;
+    if (k >= K || c >= C) continue;
+    const int ci = k / 9, tap = k - 9 * ci, tapf = 8 - tap;  // (2-kh)*3 + (2-kw)
+    f16x4 hi, lo;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int o = (r4 + a) * WC_K + q4 + b;
+      const float v = (((acc[a][b] + red[0][o]) + red[1][o]) + red[2][o]) * sc * sw;
+      hi[a] = (_Float16)v;
+      lo[a] = (_Float16)(v - (float)hi[a]);
+    }
+    const size_t u0 = ((((size_t)chunk * 9 + tapf) * 2 + 0) * 2 + cg) * gout64 + ci;
+    const size_t u1 = ((((size_t)chunk * 9 + tapf) * 2 + 1) * 2 + cg) * gout64 + ci;
+    *reinterpret_cast<f16x4*>(slab + u0 * 8 + e0) = hi;
+    *reinterpret_cast<f16x4*>(slab + u1 * 8 + e0) = lo;
+  }
+}
+
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st) {
   switch (p.stride == 2 ? LM_S2 : p.in_mode) {
     case STX_IN_RAW: return dispatch16_tw<STX_IN_RAW>(p, st);
@@ -1343,6 +1453,31 @@ extern "C" int stx_conv_weight_prep_batch(const stx_wprep_job* jobs, int njobs, 
     hipLaunchKernelGGL(amax_batch_kernel, dim3(na * STX_AMAX_SLOTS), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(weight_prep_batch_kernel, dim3(blocks), dim3(256), 0, st, b);
   return check_launch("stx_conv_weight_prep_batch");
+}
+
+extern "C" int stx_conv_weight_compose16(const float* A, int pitch, const float* a_amax,
+                                         const float* w, const float* w_amax, int cout, int cin,
+                                         const float* scale, void* wtT16, float* out_amax,
+                                         void* stream) {
+  if (!A || !a_amax || !w || !w_amax || !wtT16 || !out_amax || cout <= 0 || cout > 256 ||
+      cin <= 0 || cin % 4 || pitch < cout || (reinterpret_cast<uintptr_t>(w) & 15)) {
+    set_error("stx_conv_weight_compose16: invalid arguments (1 <= cout <= 256, cin % 4 == 0, "
+              "w 16-byte aligned)");
+    return STX_E_INVALID;
+  }
+  const long long total = (long long)rup(cout, 16) * 9 * 2 * rup(cin, 64);
+  if ((long long)cout * cin * 9 >= (1ll << 31) || total >= (1ll << 31)) {
+    set_error("stx_conv_weight_compose16: weight too large");
+    return STX_E_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  // slab padding (channels past cout / cin) must read as zero: cleared first when present
+  if (cout % 16 || cin % 64)
+    (void)hipMemsetAsync(wtT16, 0, (size_t)total * sizeof(_Float16), st);
+  hipLaunchKernelGGL(weight_compose16_kernel, dim3(cdiv(cin * 9, WC_K), cdiv(cout, WC_R)), dim3(256),
+                     0, st, A, pitch, a_amax, w, w_amax, cout, cin, scale,
+                     reinterpret_cast<_Float16*>(wtT16), out_amax);
+  return check_launch("stx_conv_weight_compose16");
 }
 
 extern "C" int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax, int cout, int cin,

@@ -260,6 +260,28 @@ def conv_weight_prep16(w: torch.Tensor, transpose: bool = False):
     return wt16, w_amax
 
 
+def conv_weight_compose16(coef, coef_amax, w: torch.Tensor, w_amax, out_amax, scale=None,
+                          out=None):
+    """The data-gradient split slab of w' = scale * A w (A = coef [cout][pitch], one image's
+    Gram-backward operator, coef_amax >= max|A|; w [cout][cin][3][3], w_amax >= max|w|):
+    conv^T_w(A z) = conv^T_{w'}(z) (stx_conv_weight_compose16, one launch).  out_amax (an
+    amax group) receives the slab's scale bound; the conv takes wt16=(slab, out_amax).
+    out: the slab buffer to reuse.  Returns the slab."""
+    _req(w, "weight")
+    _req(coef, "coef")
+    cout, cin, ks, _ = w.shape
+    assert ks == 3 and coef.shape[-2] == cout and coef.numel() == cout * coef.shape[-1], coef.shape
+    L = lib()
+    if out is None:
+        out = torch.empty(L.stx_conv_weight16_bytes(cin, cout, ks, 1), device=w.device,
+                          dtype=torch.uint8)
+    check(L.stx_conv_weight_compose16(coef.data_ptr(), coef.shape[-1], coef_amax.data_ptr(),
+                                      w.data_ptr(), w_amax.data_ptr(), cout, cin, _p(scale),
+                                      out.data_ptr(), out_amax.data_ptr(), _stream()),
+          "stx_conv_weight_compose16")
+    return out
+
+
 def conv_weight_prep16_pair(w: torch.Tensor):
     """(forward slab, data-gradient slab), sharing one device max|w| (two launches)."""
     _req(w, "weight")

@@ -353,7 +353,8 @@ _SIDE = {}
 
 # amax groups of LossState.amax: 0..5 forward, 6..10 backward split-conv inputs, 11 / 12
 # max|A| of the taps whose Gram backward is a data-gradient conv's second phase
-COEF_AMAX_SLOT = {0: 11, 2: 12}
+COEF_AMAX_SLOT = {0: 11, 2: 12, 4: 14}  # max|A| per tap (split phase / composed weights)
+COMPOSE_AMAX_SLOT = 13  # max|A5 W| of the composed conv3_1 data-gradient weights
 
 
 def slot(amax, k):
@@ -397,14 +398,30 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
 
     folded = st.folded
     s = (lambda i: None) if folded else (lambda i: g[i:i + 1])
-    am = st.amax  # slots 0..5: forward; 6..10: backward split-conv inputs; COEF_AMAX_SLOT
-    # conv3_1 output: dZ5 = A5 Z5
+    am = st.amax  # slots 0..5: forward; 6..10: backward split-conv inputs; COEF_AMAX_SLOT;
+    # COMPOSE_AMAX_SLOT
     sp = feat.wt16[1] is not None  # split kernels in use
-    dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4),
-                             out_amax=slot(am, 6), z_amax=slot(am, 5) if sp else None)
-    # -> grad wrt pool(relu Z4)
     n4 = (B, 128, z[3].shape[2] // 2, z[3].shape[3] // 2)
-    dp2 = feat.dgrad(4, dz5, buf("dp2", n4), in_amax=slot(am, 6))
+    # (STX_COMPOSE=0: the Gram backward of conv3_1 as its own 1x1 pass, dZ5 = A5 Z5; A/B)
+    ca = st.coef_amax if st.coef_amax else [None] * 5
+    if sp and B == 1 and feat.wtT16[4] is not None and ca[4] is not None and \
+            os.environ.get("STX_COMPOSE", "1") != "0":
+        # conv3_1's output feeds only its style loss, so dP2 = conv3_1^T(A5 Z5) =
+        # conv^T_{A5 W}(Z5): A5 folded into the data-gradient weights (one small GEMM
+        # launch that writes the split slab), dZ5 never formed.  One operator per image:
+        # B == 1.
+        sc["compose5"] = ops.conv_weight_compose16(
+            st.coef[4], ca[4], feat.w[4], feat.wtT16[4][1], slot(am, COMPOSE_AMAX_SLOT),
+            scale=s(4), out=sc.get("compose5"))
+        cout, cin = VGG_CONV_SHAPES[4]
+        dp2 = ops.conv2d(z[4], None, cout, cin, 3, out=buf("dp2", n4),
+                         wt16=(sc["compose5"], slot(am, COMPOSE_AMAX_SLOT)), in_amax=slot(am, 5))
+    else:
+        # conv3_1 output: dZ5 = A5 Z5
+        dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4),
+                                 out_amax=slot(am, 6), z_amax=slot(am, 5) if sp else None)
+        # -> grad wrt pool(relu Z4)
+        dp2 = feat.dgrad(4, dz5, buf("dp2", n4), in_amax=slot(am, 6))
     # dZ4 = unpool(dP2)*[Z4>0] + A4 Z4 (+ content)
     dz4 = ops.gram_bwd_fused(st.coef[3], z[3], out=buf("dz4", z[3].shape), acc_scale=s(3),
                              up_dp=dp2, aux=st.c4 if folded else None, aux_scale=-st.alpha,
@@ -418,7 +435,6 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
             ops.diff_scale(z[3], st.c4, 4.0 / (float(n) * float(n)), s1=g[6:7],
                            s2=st.fmean[1:2], relu=True, out=dz4, accumulate=True)
     # dZ3 = conv2_2^T(dZ4)*[Z3>0] + A3 Z3
-    ca = st.coef_amax if st.coef_amax else [None] * 5
     dz3 = feat.dgrad(3, dz4, buf("dz3", z[2].shape), mask=z[2], p2_z=z[2],
                      p2_coef=st.coef[2], p2_scale=s(2), in_amax=dz4_amax, out_amax=slot(am, 8),
                      p2_amax=slot(am, 3), p2_wt_amax=ca[2])

@@ -615,3 +615,31 @@ def test_split_dgrad_upsample_sum(dev, case):
     assert rel(dx, ref) < TOL64
     dv = ops.conv2d(dy, None, cout, cin, 3, wt16=w16, in_amax=ops.amax(dy))
     assert rel(dx, ops.upsample2x_bwd(dv)) < 1e-6
+
+
+@pytest.mark.parametrize("hw,scale", [(128, 1.0), (40, 1e-3), (18, 30.0)])
+def test_composed_dgrad_weights(dev, hw, scale):
+    """stx_conv_weight_compose16: the data gradient of conv3_1 with its Gram-backward
+    operator folded into the weights, conv^T_{sAW}(z) == conv^T_W(s A z) (vgg.loss_backward's
+    dP2 at B = 1, stransfer/network.py:92-123 through :264-314), against fp64 of the
+    unfused form; the fused form at 2e-6 like every split kernel, plus the scale bound against the composed weights' fp64 maximum."""
+    cout, cin = 256, 128
+    g = torch.Generator(device="cpu").manual_seed(7)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) * 0.05).to(dev)
+    A = (torch.randn(1, cout, cout, generator=g) * 1e-3).to(dev)
+    z = (torch.randn(1, cout, hw, hw, generator=g) * 2.0).to(dev)
+    s = torch.tensor([scale], device=dev)
+    wT16 = ops.conv_weight_prep16(w, transpose=True)  # (slab, max|w|) of the plain weights
+    bound = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    slab = ops.conv_weight_compose16(A, ops.amax(A), w, wT16[1], bound, scale=s)
+    wc64 = scale * torch.einsum("ck,kx->cx", A[0].double(), w.double().reshape(cout, -1))
+    # the slab's scale bound covers max|w'| (a loose power of two is as exact)
+    assert float(bound.max()) >= float(wc64.abs().max())
+    dz64 = scale * torch.einsum("ck,nchw->nkhw", A[0].double(), z.double())
+    ref = F.conv_transpose2d(dz64, w.double(), padding=1)
+    y = ops.conv2d(z, None, cout, cin, 3, wt16=(slab, bound), in_amax=ops.amax(z))
+    assert rel(y, ref) < TOL64, rel(y, ref)
+    # the unfused pair (1x1 split Gram backward, then the split data gradient) for scale
+    dz = ops.gram_bwd_fused(A, z, acc_scale=s, z_amax=ops.amax(z))
+    y2 = ops.conv2d(dz, ops.conv_weight_prep(w, transpose=True), cout, cin, 3, wt16=wT16)
+    print(f"composed {rel(y, ref):.2e}, unfused {rel(y2, ref):.2e}")

@@ -32,6 +32,16 @@ if [ -n "${PMC:-}" ]; then
   timeout -k 10 600 bash tools/pmc_r3.sh ${tag} > gpurun_out/${tag}_pmc.log 2>&1 || { tail -10 gpurun_out/${tag}_pmc.log; exit 1; }
   cp profiles/${tag}_pmc.json gpurun_out/${tag}_pmc.json
 fi
+if [ -n "${AB:-}" ]; then
+  echo "== ab $AB"
+  timeout -k 10 400 python tools/ab_engine.py $AB ${AB_ARGS:-} > gpurun_out/${tag}_ab.log 2>&1 || { tail -20 gpurun_out/${tag}_ab.log; exit 1; }
+  tail -12 gpurun_out/${tag}_ab.log
+fi
+if [ -n "${MICRO:-}" ]; then
+  echo "== micro $MICRO"
+  timeout -k 10 300 python $MICRO > gpurun_out/${tag}_micro.log 2>&1 || { tail -20 gpurun_out/${tag}_micro.log; exit 1; }
+  tail -40 gpurun_out/${tag}_micro.log
+fi
 if [ -n "${BENCH:-}" ]; then
   echo "== bench"
   timeout -k 10 500 python bench.py ${BENCH_ARGS:-} > gpurun_out/${tag}_bench.json 2> gpurun_out/${tag}_bench.err || { tail -20 gpurun_out/${tag}_bench.err; exit 1; }
