@@ -468,6 +468,7 @@ static int launch_smallc(const stx_conv_params& p, hipStream_t st) {
   const int tiles_x = cdiv(p.wo, SC_TW), tiles_y = cdiv(p.ho, TH);
   dim3 grid(tiles_x * tiles_y, 1, p.n);
   constexpr int CIS = KS == 9 ? 4 : 8;
+#ifdef STX_AB  // measured tilings (not in the product build)
   if constexpr (KS == 3) {
     static const int cfg = STX_KNOB("STX_SMALLC", 0);
     if (cfg == 1) {
@@ -494,6 +495,7 @@ static int launch_smallc(const stx_conv_params& p, hipStream_t st) {
       return check_launch("stx_conv2d(smallc)");
     }
   }
+#endif
   static const bool c3 = STX_KNOB("STX_SMALLC_C3", 1) != 0;
   if (p.cout == 3 && c3)  // the ITN's final conv: no idle fourth output channel
     hipLaunchKernelGGL((conv_smallc_kernel<KS, CIS, TH, 2, 3>), grid, dim3(2 * 16 * TH), 0, st,

@@ -882,9 +882,11 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
     } else if (c == 128)
       hipLaunchKernelGGL(gram_tri_f16_kernel<128>, dim3(nsplit, 1, b), dim3(256), 0, st, z, slabs,
                          hw, nsplit, split_len, z_amax);
+#ifdef STX_AB  // C = 256 on the triangle kernel (measured slower; STX_GRAM_TRI=2)
     else
       hipLaunchKernelGGL(gram_tri_f16_kernel<256>, dim3(nsplit, 1, b), dim3(256), 0, st, z, slabs,
                          hw, nsplit, split_len, z_amax);
+#endif
   } else if (f16) {
     hipLaunchKernelGGL(gram_partial_f16_kernel, dim3(nsplit * ntu, 1, b), dim3(256), 0, st, z,
                        slabs, c, hw, nsplit, split_len, z_amax);

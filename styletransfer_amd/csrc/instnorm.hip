@@ -729,10 +729,13 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
   // 64^2 planes: 512 threads x 2 float4 per thread (fast_st 1801 -> 1811 img/s same box
   // against 256 x 4; 128 x 8 was 0.6 % slower); STX_IN_CFG=0 restores 256 x 4, 1 = 128 x 8
   static const int cfg = STX_KNOB("STX_IN_CFG", 2);
+#ifdef STX_AB  // 128 x 8 blocks for the 64^2 planes (measured 0.6 % slower)
   if (cfg == 1 && hw % 4 == 0 && hw <= 4 * 128 * 8)
     hipLaunchKernelGGL((instnorm_fwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, x, res,
                        gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
-  else if (cfg == 2 && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0 &&
+  else
+#endif
+  if (cfg == 2 && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0 &&
            n * c / in_ppb() >= 256 &&  // enough blocks to fill the chip (B = 8: 256)
            ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) |
              reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
@@ -793,10 +796,13 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
                     reinterpret_cast<uintptr_t>(du)) & 15) == 0 && hw % 4 == 0;
   // block shape of the 64^2 kernels, as stx_instnorm_fwd
   static const int cfg = STX_KNOB("STX_IN_CFG", 2);
+#ifdef STX_AB
   if (cfg == 1 && al && hw <= 4 * 128 * 8)
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, dy, y, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
-  else if (cfg == 2 && al && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0 &&
+  else
+#endif
+  if (cfg == 2 && al && hw == 4 * 512 * 2 && in_ppb() > 1 && (n * c) % in_ppb() == 0 &&
            n * c / in_ppb() >= 256) {
     const int ppb = in_ppb();
     const dim3 grid(n * c / ppb);

@@ -644,21 +644,25 @@ static int wg16_pf() {
 static Wg16Kernel wg16_kernel(const Wg16& g) {
   if (g.lds) {
     const bool up = g.mode == STX_IN_UPSAMPLE2;
+#ifdef STX_AB  // measured variants (not in the product build): load-ring depths, cout 64
     static const int lpf = STX_KNOB("STX_WG16_LPF", 3);
-    if (g.cout == 128)
-      return up ? wgrad16_lds_kernel<4, true, 3>
-                : (lpf >= 7 ? wgrad16_lds_kernel<4, false, 7>
-                            : (lpf >= 5 ? wgrad16_lds_kernel<4, false, 5>
-                                        : wgrad16_lds_kernel<4, false, 3>));
-    if (g.cin % 128 == 0)
-      return up ? wgrad16_lds_kernel<2, true, 3, 128> : wgrad16_lds_kernel<2, false, 3, 128>;
-    return up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>;
+    if (g.cout == 128 && !up && lpf >= 5)
+      return lpf >= 7 ? wgrad16_lds_kernel<4, false, 7> : wgrad16_lds_kernel<4, false, 5>;
+    if (g.cout != 128) {
+      if (g.cin % 128 == 0)
+        return up ? wgrad16_lds_kernel<2, true, 3, 128> : wgrad16_lds_kernel<2, false, 3, 128>;
+      return up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>;
+    }
+#endif
+    return up ? wgrad16_lds_kernel<4, true, 3> : wgrad16_lds_kernel<4, false, 3>;
   }
   if (g.ci2) return wgrad16_kernel<4, false, true>;
   if (g.mode == WG16_S2) return wgrad16_kernel<4, true>;
+#ifdef STX_AB
   const int pf = wg16_pf();
-  return pf >= 12 ? wgrad16_kernel<12, false>
-                  : (pf >= 8 ? wgrad16_kernel<8, false> : wgrad16_kernel<4, false>);
+  if (pf >= 8) return pf >= 12 ? wgrad16_kernel<12, false> : wgrad16_kernel<8, false>;
+#endif
+  return wgrad16_kernel<4, false>;
 }
 
 // resident blocks of `k` over the whole device (CUs x blocks per CU at 256 threads);
