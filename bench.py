@@ -353,6 +353,7 @@ def coco_loader_leg(args, dev, fast_rate=None):
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
         return dict(rate=count / dt, images=count, s=dt, workers=workers, files=n,
+                    usable_cpus=dataset.usable_cpus(),
                     jpeg_kb=round(sum(os.path.getsize(os.path.join(tmp, f))
                                       for f in os.listdir(tmp)) / n / 1024, 1))
     finally:
@@ -637,8 +638,14 @@ def main():
         vid = video_leg(args, world, rank, dev)
         conv = convert_leg(args, world, rank, dev)
     ld = None
-    if world == 1 and args.loader_images > 0 and not args.skip_infer:
+    if args.loader_images > 0 and not args.skip_infer:
+        # every rank runs its own loader on its share of the node's CPUs (the worker count
+        # follows LOCAL_WORLD_SIZE); the line reports the slowest rank
         ld = coco_loader_leg(args, dev)
+        if world > 1:
+            t = torch.tensor([ld["rate"]], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ld["rate_min_rank"] = float(t.item())
     cpu = None
     if rank == 0 and world == 1 and not args.skip_cpu:
         cpu = cpu_baseline(args)
@@ -771,14 +778,25 @@ def main():
                 "graph": fs64["graph"], "note": "config-4 global batch 64 on one GPU (the "
                 "1-GPU point of the strong-scaling view; the weak-scaling legs keep 8/GPU)"}
         if ld:
+            per_rank_step = fs["rate"] / world if fs else None
+            per_worker = ld["rate"] / max(1, ld["workers"])
             res["coco_loader"] = {
-                "value": round(ld["rate"], 1), "unit": "images/s", "batch": args.fast_batch,
-                "workers": ld["workers"], "images": ld["images"], "seconds": round(ld["s"], 3),
+                "value": round(ld.get("rate_min_rank", ld["rate"]), 1), "unit": "images/s",
+                "per_rank": True, "batch": args.fast_batch,
+                "workers": ld["workers"], "usable_cpus": ld["usable_cpus"],
+                "images_per_s_per_worker": round(per_worker, 1),
+                "images": ld["images"], "seconds": round(ld["s"], 3),
                 "jpeg": f"{ld['files']} synthetic 640x480 JPEGs, {ld['jpeg_kb']} KB avg",
-                "vs_fast_st_step_rate": round(ld["rate"] / fs["rate"], 3) if fs else None,
+                "vs_fast_st_step_rate": round(ld.get("rate_min_rank", ld["rate"]) / per_rank_step, 3)
+                if fs else None,
+                "cpus_for_8_ranks": (round(8 * (per_rank_step / per_worker + 1), 1)
+                                     if fs else None),
                 "note": "dataset.get_coco_loader(gpu_conditioning=True): decode workers -> "
                         "pinned packed batch -> side-stream upload + GPU crop/resize/normalise "
-                        "(bit-identical to the PIL path); per rank, fed by this rank's CPU share"}
+                        "(bit-identical to the PIL path); per rank, fed by this rank's CPU share "
+                        "(usable CPUs / LOCAL_WORLD_SIZE - 1 workers); value = the slowest rank; "
+                        "cpus_for_8_ranks = 8 x (the per-rank fast_st step rate / images per "
+                        "worker + 1 for the training loop)"}
         if vid:
             res["video_st"] = {
                 "value": round(vid["rate"], 2), "unit": "frames/s",

@@ -76,9 +76,9 @@ def _pack_collate(batch):
     return packed, shapes
 
 
-def default_workers():
-    """Decode workers for the GPU-conditioned loader: the CPUs this process may use
-    (affinity, cgroup quota) minus one for the training loop, at most 16."""
+def usable_cpus():
+    """The CPUs this process may run on: its affinity mask, capped by the cgroup CPU quota
+    (on a shared GPU box the box's share, not os.cpu_count())."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -90,7 +90,17 @@ def default_workers():
                 n = min(n, max(1, int(int(q) / int(per))))
     except (OSError, ValueError):
         pass
-    return max(0, min(16, n - 1))
+    return n
+
+
+def default_workers(local_world=None):
+    """Decode workers for the GPU-conditioned loader of ONE rank: the usable CPUs split
+    evenly over the ranks of this node (LOCAL_WORLD_SIZE, torchrun's per-node rank count;
+    the ranks share the node's CPUs), minus one for the rank's training loop, at most 16."""
+    if local_world is None:
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
+    share = usable_cpus() // max(1, local_world)
+    return max(0, min(16, share - 1))
 
 
 class GpuConditionedLoader:

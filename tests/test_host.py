@@ -180,3 +180,17 @@ def test_cli_help():
     assert r.exit_code == 0 and "--batch-size" in r.output
     r = CliRunner().invoke(cli, ["fast_st", "convert-image", "--help"])
     assert r.exit_code == 0 and "--out-dir" in r.output
+
+
+def test_loader_workers_per_rank(monkeypatch):
+    """The GPU-conditioned COCO loader's decode workers are sized per rank: the usable
+    CPUs (affinity, cgroup quota) split over the node's ranks (LOCAL_WORLD_SIZE), minus one
+    for the rank's training loop, at most 16 (stransfer/dataset.py:141-197's loader, fed
+    at the data-parallel step rate)."""
+    from styletransfer_amd import dataset as D
+    n = D.usable_cpus()
+    assert n >= 1
+    for lw in (1, 2, 8):
+        assert D.default_workers(lw) == max(0, min(16, n // lw - 1))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert D.default_workers() == max(0, min(16, n // 4 - 1))
