@@ -637,7 +637,11 @@ __global__ void __launch_bounds__(256 * WM, WM == 2 ? 1 : ((NI == 1 && TW <= 32)
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   using C = C16v2<TW, NI, WM>;
   constexpr int NT = C::NT;
-  constexpr bool RP = TW == 64 && NI == 2;  // row-pair tiles (fused pool / unpool)
+  // PAR: the zero-dilated data gradient (a stride-2 conv's input gradient) on 64 x 4 tiles
+  // whose N-tiles are output parity classes: of the 9 taps x 3 kernel rows only those that
+  // meet the dilated input's non-zero (even) positions run -- a quarter of the MFMAs
+  constexpr bool PAR = LM == STX_IN_DILATE2 && TW == 64 && NI == 2 && WM == 1 && P2 == 0;
+  constexpr bool RP = TW == 64 && NI == 2 && !PAR;  // row-pair tiles (fused pool / unpool)
   static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
   static_assert(P2 != 2, "1x1 mode: v1 kernel");
   static_assert(WM == 1 || (P2 == 0 && !RP), "WM = 2: plain epilogue only");
@@ -769,7 +773,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     int ty, tx;
-    tile_pix<TW, RP, NI>(wn, j, l32, ty, tx);
+    tile_pix<TW, RP, NI, PAR>(wn, j, l32, ty, tx);
     boff[j] = (h * C::NPOS + ty * C::RW + tx) * 16;
   }
   const int aoff = 2 * C::HB + (h * BM + wm * 64 + l32) * 16;
@@ -827,6 +831,45 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
             for (int j = 0; j < NI; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
         };
+        if constexpr (PAR) {
+          // staging for step s+1 first (every wave), then this step's taps, only in the
+          // waves whose output row meets a non-zero dilated row at this kernel row (the
+          // tile's rows start even: the wave's row parity is wn's) and, per tap, only the
+          // N-tile of the column parity that meets a non-zero column
+          if (s + 1 < nsteps) st_w((s + 1) & 1);
+          if (c + 1 < nchunks) {
+#pragma unroll
+            for (int r = k; r < C::NIT; r += 3) st_halo((c + 1) & 1, r);
+          }
+          if (s + 2 < nsteps) ld_w(s + 2);
+          {
+            const int cn = k < 2 ? c + 1 : c + 2;
+            if (cn < nchunks) {
+#pragma unroll
+              for (int r = (k + 1) % 3; r < C::NIT; r += 3) ld_halo(cn, r);
+            }
+          }
+          if (((k + wn) & 1) == 1) {
+#pragma unroll
+            for (int tl = 0; tl < 3; ++tl) {
+              const int jt = (tl + 1) & 1;  // x + tl - 1 even <=> x parity != tl parity
+              f16x8 ah[2], al[2];
+              rdA(tl, 0, ah);
+              rdA(tl, 1, al);
+              const f16x8 bh = *reinterpret_cast<const f16x8*>(bbase[jt] + (k * C::RW + tl) * 16);
+              const f16x8 bl =
+                  *reinterpret_cast<const f16x8*>(bbase[jt] + (C::NITEM + k * C::RW + tl) * 16);
+#pragma unroll
+              for (int i = 0; i < 2; ++i) {
+                acc[i][jt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh, acc[i][jt], 0, 0, 0);
+                acc[i][jt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, acc[i][jt], 0, 0, 0);
+                acc[i][jt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, acc[i][jt], 0, 0, 0);
+              }
+            }
+          }
+          __syncthreads();
+          continue;
+        }
         f16x8 ahi[2], alo[2], bhi[NI], blo[NI];
         rdA(0, 0, ahi);
         rdB(0, 0, bhi);
@@ -880,7 +923,9 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     EpiTile et{n, co0, ty0, tx0, wm, wn, h, l32};
     et.tile = tile;
     et.ntiles = ntiles;
-    if constexpr (WM == 2) {
+    if constexpr (PAR) {
+      conv_epilogue_plain<TW, NI, false, true>(acc, p, et, descale, smem);  // (launch16v2)
+    } else if constexpr (WM == 2) {
       conv_epilogue_plain<TW, NI, RP>(acc, p, et, descale, smem);  // (eligibility: launch16v2)
     } else if constexpr (P2 == 3) {
       // (eligibility: launch16v2 -- data gradient + mask + the phase, bias / out_amax only)
@@ -983,6 +1028,12 @@ static int launch16v2(const stx_conv_params& p, hipStream_t st) {
                          tiles_x, ntiles);
       return check_launch("stx_conv2d(f16x3 v2, 128 couts)");
     }
+  if constexpr (LM == STX_IN_DILATE2 && TW == 64 && NI == 2)
+    if (p.mask || p.accumulate || p.acc_scale || p.up_dp || p.pool_out || p.pool_sum ||
+        p.gram_part || (p.aux && p.relu_out)) {
+      set_error("stx_conv2d: zero-dilated input on 64 x 4 tiles takes the plain epilogue only");
+      return STX_E_INVALID;
+    }
   hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI>), grid, dim3(256), 0, st, p,
                      tiles_x, ntiles);
   return check_launch("stx_conv2d(f16x3 v2)");
@@ -1028,6 +1079,12 @@ static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
   // (34 x 10 halo) instead of 64 x 4 (66 x 6) -- same-box profile of the fast_st step:
   // upsampling convs 92 -> 84 and 49 -> 45 us, dilated (stride-2 dgrad) 89 -> 85 and
   // 55 -> 52, ReLU 101 -> 98; raw-input launches measured 1 % slower and keep 64 x 4.
+  // the zero-dilated input (a stride-2 conv's data gradient) with the plain epilogue: 64 x 4
+  // parity-class tiles (PAR in conv3x3_f16x3_v2_kernel: a quarter of the MFMAs)
+  if constexpr (TW == 64 && LM == STX_IN_DILATE2)
+    if (!p.mask && !p.accumulate && !p.acc_scale && !p.up_dp && !p.pool_out && !p.pool_sum &&
+        !p.gram_part && !p.p2_z && !(p.aux && p.relu_out))
+      return launch16<64, LM, 2>(p, st);
   if constexpr (TW == 64 && LM != STX_IN_RAW)
     if (!p.pool_out && !p.gram_part && !p.p2_z && !p.up_dp)
       return launch16<32, LM, 2>(p, st);

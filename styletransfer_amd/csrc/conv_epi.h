@@ -28,9 +28,16 @@ struct EpiTile {
 // row-major tile order.  ROWPAIR (TW == 64): wave column wn covers x in
 // [32*(wn&1), +32) of rows 2*(wn>>1) + {0, 1}, so every 2x2 pooling window lies in
 // one wave (tiles j = 0/1 x lanes l32, l32^1) -- the fused ReLU+MaxPool output.
-template <int TW, bool ROWPAIR, int NI = 2>
+// PAR (TW == 64, NI == 2: the zero-dilated data gradient): wave column wn owns tile row
+// wn, N-tile j the pixels of column parity j (x = 2 l32 + j) -- every N-tile is one output
+// parity class, so the taps that only meet dilation zeros are skipped per N-tile
+template <int TW, bool ROWPAIR, int NI = 2, bool PAR = false>
 __device__ __forceinline__ void tile_pix(int wn, int j, int l32, int& ty, int& tx) {
-  if (ROWPAIR) {
+  if (PAR) {
+    static_assert(!PAR || (TW == 64 && NI == 2), "parity mapping needs 64 x 4 tiles");
+    tx = 2 * l32 + j;
+    ty = wn;
+  } else if (ROWPAIR) {
     static_assert(!ROWPAIR || TW == 64, "row-pair mapping needs TW == 64");
     tx = (wn & 1) * 32 + l32;
     ty = (wn >> 1) * 2 + j;
@@ -224,14 +231,32 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
   const int wave = threadIdx.x >> 6, h = t.h, l32 = t.l32;
   const int e = gram_block_exp(vmax_u, red);
   const float sx = __builtin_ldexpf(1.f, 15 - e);
+  // two neighbouring pixels per 4-B LDS store: for the registers (r, r+1) (channels ch,
+  // ch+1) the lane pair (px even, px+1) swaps one value by DPP, then the even lane holds
+  // channel ch at (px, px+1) and the odd lane channel ch+1 at (px-1, px) -- half the
+  // ds_write instructions of one fp16 per store
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  const int q = l32 & 1;
 #pragma unroll
   for (int j = 0; j < NI; ++j)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ch = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        gram_put(H, GP::HP, ch, wave * 64 + j * 32 + l32, lane_ok[j] ? acc[i][j][r] * sx : 0.f);
+      for (int r = 0; r < 16; r += 2) {
+        const float va = lane_ok[j] ? acc[i][j][r] * sx : 0.f;
+        const float vb = lane_ok[j] ? acc[i][j][r + 1] * sx : 0.f;
+        const float recv = __int_as_float(
+            __builtin_amdgcn_mov_dpp(__float_as_int(q ? va : vb), 0xB1, 0xF, 0xF, false));
+        const float v0 = q ? recv : va, v1 = q ? vb : recv;
+        const int ch = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h + q;
+        const int p0 = wave * 64 + j * 32 + l32 - q;
+        f16x2 hi, lo;
+        hi[0] = (_Float16)v0;
+        hi[1] = (_Float16)v1;
+        lo[0] = (_Float16)(v0 - (float)hi[0]);
+        lo[1] = (_Float16)(v1 - (float)hi[1]);
+        *reinterpret_cast<f16x2*>(H + ch * GP::HP + p0) = hi;
+        *reinterpret_cast<f16x2*>(H + (64 + ch) * GP::HP + p0) = lo;
       }
   __syncthreads();
   f32x16 g;
@@ -256,7 +281,7 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
 // through a descriptor at the store offsets
 // POOLSUM: pool_out = 2x2 sum of the output and no y stores (stx_conv_params.pool_sum)
 template <int TW, int NI, bool ROWPAIR, bool RELU, bool AUX = false,
-          bool POOLSUM = false>
+          bool POOLSUM = false, bool PAR = false>
 __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
                                                          const stx_conv_params& p,
                                                          const EpiTile& t, float scale,
@@ -274,7 +299,7 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     int ty, tx;
-    tile_pix<TW, ROWPAIR, NI>(t.wn, j, l32, ty, tx);
+    tile_pix<TW, ROWPAIR, NI, PAR>(t.wn, j, l32, ty, tx);
     const int oy = t.ty0 + ty, ox = t.tx0 + tx;
     lane_ok[j] = oy < p.ho && ox < p.wo;
     vo[j] = lane_ok[j] ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u : BUF_OOB;
@@ -307,13 +332,30 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
         float v = fmaf(acc[i][j][r], scale, bias_r[i][r]);
         if (AUX) v += p.aux_scale * buf_ld(raux, vo[j] + (uint32_t)row * pb);
         if (RELU) v = fmaxf(v, 0.f);
-        if constexpr (!POOLSUM) buf_st(ry, vo[j] + (uint32_t)row * pb, v);
-        acc[i][j][r] = v;  // kept for the fused pooled output
+        if constexpr (!POOLSUM && !PAR) buf_st(ry, vo[j] + (uint32_t)row * pb, v);
+        acc[i][j][r] = v;  // kept for the fused pooled output (PAR: for the paired stores)
         uint32_t m = lmask[j];
         if (!rows_full) m = (row + 4 * h < rows) ? m : 0u;
         vmax_u = max(vmax_u, __float_as_uint(v) & m);
       }
     }
+  }
+  if constexpr (PAR) {
+    // the lane's two N-tiles are the neighbouring pixels 2 l32 and 2 l32 + 1: one 8-B store
+    // per row (a 4-B store where the odd pixel is past a ragged right edge)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t o = vo[0] + (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * pb;
+        if (lane_ok[1]) {
+          typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+          const u32x2_t d = {__float_as_uint(acc[i][0][r]), __float_as_uint(acc[i][1][r])};
+          __builtin_amdgcn_raw_buffer_store_b64(d, ry, o, 0, 0);
+        } else {
+          buf_st(ry, o, acc[i][0][r]);
+        }
+      }
   }
   if constexpr (ROWPAIR) if (p.pool_out) {
     // relu(maxpool2x2(y)) = maxpool2x2(relu(y)) -> pool_out [n][cout][ho/2][wo/2]
@@ -369,7 +411,7 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
-template <int TW, int NI, bool ROWPAIR>
+template <int TW, int NI, bool ROWPAIR, bool PAR = false>
 __device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const stx_conv_params& p,
                                                     const EpiTile& t, float scale, char* smem) {
   if (p.mask || p.accumulate || p.acc_scale || p.up_dp || p.p2_z) return false;
@@ -380,11 +422,11 @@ __device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const 
   }
   if (p.aux) {
     if (p.relu_out || p.pool_out || p.gram_part) return false;
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, true>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, true, false, PAR>(acc, p, t, scale, smem);
   } else if (p.relu_out) {
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, true>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, true, false, false, PAR>(acc, p, t, scale, smem);
   } else {
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, false>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, false, false, PAR>(acc, p, t, scale, smem);
   }
   return true;
 }

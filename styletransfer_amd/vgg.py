@@ -191,6 +191,7 @@ class LossState:
     lws: list = field(default_factory=lambda: [None] * 5)    # per-layer style-loss scratch
     parts: list = field(default_factory=lambda: [None] * 5)  # deferred loss partials
     grams: list = field(default_factory=lambda: [None] * 5)  # fused Gram partial slabs
+    fin_jobs: list = None                       # the last batched finalize's jobs (bench)
 
 
 def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
@@ -333,6 +334,8 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
             for c in st.coef:
                 c.record_stream(main)
     if fin is not None:
+        # (the jobs stay on the state for bench.py's per-tap cost of the batched launch)
+        st.fin_jobs = list(fin.jobs)
         fin.flush()  # every tap's G, backward operator A and loss partials: one launch
     # the 5 style losses (+ the weighted total) in one launch
     w = None
