@@ -106,13 +106,15 @@ typedef struct stx_conv_params {
    * dz = s*A[n].z, stx_gram_bwd) given in_amax and wt16 = (void*)1 runs as that
    * phase alone on the split kernel (no ReLU mask allowed there). */
   const float* p2_amax;
-  /* optional fused Gram partials of the output (StyleLoss.gram_matrix of a 64-channel
-   * VGG tap, stransfer/network.py:92-108, computed where the tile is produced instead
-   * of re-reading y): split path, stride 1, cout == 64, wo > 32, and the plain
-   * epilogue (no mask / aux / accumulate / acc_scale / up_dp / p2_z / relu_out).
-   * Block t of image n writes sum over its output pixels of y y^T (64 x 64 fp32, fp16
-   * hi/lo MFMA with a block-local power-of-two scale) to gram_part + (n * T + t) * 4096,
-   * T = stx_conv_gram_tiles(p); stx_style_loss_from_parts reduces them. */
+  /* optional fused Gram partials of the output (StyleLoss.gram_matrix of a 64- or
+   * 128-channel VGG tap, stransfer/network.py:92-108, computed where the tile is produced
+   * instead of re-reading y): split path, stride 1, cout == 64 or 128, wo > 32, and the
+   * plain epilogue (no mask / aux / accumulate / acc_scale / up_dp / p2_z / relu_out;
+   * cout 128: raw or ReLU input).  Block t of image n writes sum over its output pixels
+   * of y y^T (fp32, fp16 hi/lo MFMA with a block-local power-of-two scale) as U 64 x 64
+   * tiles: tile u to gram_part + ((n * U + u) * T + t) * 4096, T = stx_conv_gram_tiles(p),
+   * U = 1 (cout 64) or 3 (cout 128: tiles (0,0), (0,1), (1,1) of the 128 x 128 matrix,
+   * diagonal tiles whole); stx_style_loss_from_parts reduces them. */
   float* gram_part;
   /* with pool_out: pool_out = the 2x2 SUM of the output (no ReLU) and y is not written
    * -- the backward of nearest x2 upsampling (torch.nn.Upsample(scale_factor=2), the
@@ -135,6 +137,18 @@ typedef struct stx_conv_params {
    * folded in by the kernel).  The Gram-backward phase then runs on the fp16 hi/lo
    * split MFMA with this precomputed scale instead of the fp32 MFMA. */
   const float* p2_wt_amax;
+  /* optional with gram_part on a 128-channel tap (the content layer conv2_2,
+   * stransfer/network.py:134-201): the content target ref [n][cout][ho][wo]; block t of
+   * image n then also writes sum (y - ref)^2 and sum (relu y - relu ref)^2 over its
+   * outputs to mse_parts[2 (n T + t) + 0 / 1] (n * T * 2 floats), which
+   * stx_style_content_loss_from_parts reduces into the content / feature losses. */
+  const float* mse_ref;
+  float* mse_parts;
+  /* optional with in_mode STX_IN_UPSAMPLE2 on the split path (wt16 / w_amax of the same
+   * weights): the parity-class slab (stx_conv_weight_prep16_up).  The conv then runs as
+   * four output-parity 2x2 convs over the un-upsampled input (64 x 8 output tiles of one
+   * row parity per block); plain epilogue only (bias, relu_out, out_amax), wo > 32. */
+  const void* wt16_up;
 } stx_conv_params;
 
 #define STX_GRAM_GROUP 8
@@ -186,6 +200,15 @@ int stx_conv_weight_compose16(const float* A, int pitch, const float* a_amax, co
  * two launches (one max pass, one conversion) -- a trained layer re-preps every step. */
 int stx_conv_weight_prep16_pair(const float* w, void* wt16, void* wtT16, float* w_amax,
                                 int cout, int cin, int ks, void* stream);
+/* The parity-class split slab of a 3x3 conv that reads a nearest x2 upsampled input
+ * (UpsampleConvLayer, stransfer/network.py:578-600): each output parity class (a, b) of
+ * the conv over the upsampled image is a 2x2 conv over the input with summed weights
+ * W'[a][b][ry][rx] (16 instead of 36 tap MACs per 2x2 output group).  w [cout][cin][3][3]
+ * -> wt16_up (stx_conv_weight16up_bytes(cin, cout) bytes), *w_amax = max|w| (the slab is
+ * split at 2^(13 - e), |W'| <= 4 max|w|); stx_conv_params.wt16_up takes it. */
+size_t stx_conv_weight16up_bytes(int cin, int cout);
+int stx_conv_weight_prep16_up(const float* w, void* wt16_up, float* w_amax, int cout, int cin,
+                              void* stream);
 /* Every slab of a trained network in two launches (one max|w| pass over the distinct
  * split-slab weights, one conversion pass over all jobs) instead of two launches per
  * slab: the per-step re-prep of ImageTransformNet's 14 conv weights after each Adam
@@ -197,6 +220,7 @@ int stx_conv_weight_prep16_pair(const float* w, void* wt16, void* wtT16, float* 
 #define STX_WPREP_MAX 48
 #define STX_WPREP_F32 0
 #define STX_WPREP_F16 1
+#define STX_WPREP_F16UP 2 /* the parity-class slab (stx_conv_weight_prep16_up), transpose 0 */
 typedef struct stx_wprep_job {
   const float* w;
   void* slab;
@@ -327,13 +351,22 @@ int stx_style_content_loss(const float* z, const float* target, float* coef, flo
                            int b, int c, int hw, int target_batched, float weight,
                            float diag_alpha, const float* z_amax, const float* content,
                            float* mse_out, void* ws, size_t ws_bytes, void* stream);
-/* stx_style_loss from precomputed Gram partials (stx_conv_params.gram_part; c <= 64):
- * parts [b][nparts][64][64] summed in a fixed order, then the same G, coef, loss and
- * deferred loss partials (ws >= stx_gram_ws(b, c, hw); stx_style_loss_parts). */
+/* stx_style_loss from precomputed Gram partials (stx_conv_params.gram_part; c <= 64 or
+ * c == 128): parts [b][U][nparts][64][64] (U = 1, or 3 tiles for c = 128) summed in a
+ * fixed order, then the same G, coef, loss and deferred loss partials
+ * (ws >= stx_gram_ws(b, c, hw); stx_style_loss_parts). */
 int stx_style_loss_from_parts(const float* parts, int nparts, const float* target,
                               float* g_out, float* coef, float* loss, int b, int c, int hw,
                               int target_batched, float weight, float diag_alpha, void* ws,
                               size_t ws_bytes, void* stream);
+/* stx_style_loss_from_parts plus the content tap's content / feature / feature-mse values
+ * (stx_style_content_loss's mse_out) from the conv epilogue's MSE sums
+ * (stx_conv_params.mse_parts: b * nparts pairs), finalized by the same launch. */
+int stx_style_content_loss_from_parts(const float* parts, int nparts, const float* target,
+                                      float* coef, float* loss, int b, int c, int hw,
+                                      int target_batched, float weight, float diag_alpha,
+                                      const float* mse_parts, float* mse_out, void* ws,
+                                      size_t ws_bytes, void* stream);
 /* Deferred Gram finalizes.  The *_deferred forms of stx_style_loss,
  * stx_style_content_loss and stx_style_loss_from_parts launch only their partial
  * kernel(s) (if any) and describe the finalize (G, coef, loss partials, the fused content
@@ -369,6 +402,12 @@ int stx_style_loss_from_parts_deferred(const float* parts, int nparts, const flo
                                        float* coef, int b, int c, int hw, int target_batched,
                                        float weight, float diag_alpha, void* ws, size_t ws_bytes,
                                        stx_gram_fin_job* job, void* stream);
+int stx_style_content_loss_from_parts_deferred(const float* parts, int nparts,
+                                               const float* target, float* coef, int b, int c,
+                                               int hw, int target_batched, float weight,
+                                               float diag_alpha, const float* mse_parts,
+                                               float* mse_out, void* ws, size_t ws_bytes,
+                                               stx_gram_fin_job* job, void* stream);
 int stx_gram_finalize_batch(const stx_gram_fin_job* jobs, int njobs, void* stream);
 
 /* *out = sum_i w_host[i] * s[i]   (k <= 16 device scalars, fixed order) */

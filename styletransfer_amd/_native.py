@@ -38,7 +38,8 @@ class ConvParams(C.Structure):
         ("up_dp", vp), ("up_z", vp),
         ("wt16", vp), ("w_amax", vp), ("in_amax", vp), ("out_amax", vp),
         ("pool_out", vp), ("p2_amax", vp), ("gram_part", vp), ("pool_sum", i32),
-        ("gram_cnt", vp), ("p2_wt_amax", vp),
+        ("gram_cnt", vp), ("p2_wt_amax", vp), ("mse_ref", vp), ("mse_parts", vp),
+        ("wt16_up", vp),
     ]
 
 
@@ -55,7 +56,7 @@ class WprepJob(C.Structure):
                 ("cin", i32), ("ks", i32), ("transpose", i32), ("pad_", i32)]
 
 
-STX_WPREP_MAX, STX_WPREP_F32, STX_WPREP_F16 = 48, 0, 1
+STX_WPREP_MAX, STX_WPREP_F32, STX_WPREP_F16, STX_WPREP_F16UP = 48, 0, 1, 2
 
 
 class PGradJob(C.Structure):
@@ -96,6 +97,8 @@ SIGNATURES = {
     "stx_conv_weight16_bytes": (sz, [i32, i32, i32, i32]),
     "stx_conv_weight_prep16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv_weight_prep16_pair": (i32, [vp, vp, vp, vp, i32, i32, i32, vp]),
+    "stx_conv_weight16up_bytes": (sz, [i32, i32]),
+    "stx_conv_weight_prep16_up": (i32, [vp, vp, vp, i32, i32, vp]),
     "stx_conv_weight_compose16": (i32, [vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
     "stx_amax": (i32, [vp, i64, vp, vp]),
     "stx_conv_weight_prep_batch": (i32, [C.POINTER(WprepJob), i32, vp]),
@@ -129,6 +132,8 @@ SIGNATURES = {
                              vp]),
     "stx_style_loss_from_parts": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32, i32, f32, f32,
                                         vp, sz, vp]),
+    "stx_style_content_loss_from_parts": (i32, [vp, i32, vp, vp, vp, i32, i32, i32, i32, f32,
+                                                f32, vp, vp, vp, sz, vp]),
     "stx_style_content_ws": (sz, [i32, i32, i32]),
     "stx_style_content_loss": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, vp, vp, vp,
                                      vp, sz, vp]),
@@ -138,6 +143,9 @@ SIGNATURES = {
                                               vp, vp, sz, C.POINTER(GramFinJob), vp]),
     "stx_style_loss_from_parts_deferred": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, f32, f32,
                                                  vp, sz, C.POINTER(GramFinJob), vp]),
+    "stx_style_content_loss_from_parts_deferred": (i32, [vp, i32, vp, vp, i32, i32, i32, i32,
+                                                         f32, f32, vp, vp, vp, sz,
+                                                         C.POINTER(GramFinJob), vp]),
     "stx_gram_finalize_batch": (i32, [C.POINTER(GramFinJob), i32, vp]),
     "stx_gram_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp, vp, f32, i32, vp]),
     "stx_mse_ws": (sz, [i64]),

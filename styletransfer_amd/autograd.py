@@ -24,6 +24,12 @@ def _upsample_fuse_on():
     return os.environ.get("STX_UPSAMPLE_FUSE", "1") != "0"
 
 
+def _upar_on():
+    """STX_UPAR=0: upsampled-input convs over the upsampled halo (no parity classes; A/B)."""
+    import os
+    return os.environ.get("STX_UPAR", "1") != "0"
+
+
 def _grad_into(param, g, accumulate_fn):
     """Parameter gradients straight into an existing `param.grad` (e.g. the flat
     gradient buffer of train.FastStTrainer): `accumulate_fn(dst)` adds the gradient
@@ -59,7 +65,7 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, in_mode, wt=None, wt16=None, wtT=None, wtT16=None,
-                link=None):
+                link=None, wt16_up=None):
         x = _c(x)
         # link (ResLink): a skip gradient to add into dx (raw-input stride-1 convs only)
         ctx.link = link if (stride == 1 and in_mode == N.STX_IN_RAW) else None
@@ -95,9 +101,13 @@ class Conv2dFn(torch.autograd.Function):
             x_amax = ops.ARENA.lookup(x)
             if x_amax is None:
                 x_amax = ops.amax(x)
+        if split and in_mode == N.STX_IN_UPSAMPLE2 and wt16_up is None and _upar_on() and \
+                ks == 3 and 2 * x.shape[3] > 32:
+            # (trained / cached layers hand the parity-class slab in; prepped per call here)
+            wt16_up = ops.conv_weight_prep16_up(w.detach().contiguous())
         y = ops.conv2d(x, wt, cin, cout, ks, stride=stride, pad=pad, in_mode=in_mode,
                        bias=None if b is None else b.detach(), wt16=wt16 if split else None,
-                       in_amax=x_amax)
+                       in_amax=x_amax, wt16_up=wt16_up if split and _upar_on() else None)
         ctx.save_for_backward(x, w)
         ctx.x_amax = x_amax
         ctx.b_ref = b
@@ -186,14 +196,14 @@ class Conv2dFn(torch.autograd.Function):
             b = ctx.b_ref
             db = _grad_into(b, lambda: ops.bias_grad(dy),
                             lambda dst: ops.bias_grad(dy, db=dst, accumulate=True))
-        return dx, dw, db, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None
 
 
 def conv2d(x, w, b=None, stride=1, pad=None, in_mode=N.STX_IN_RAW, wt=None, wt16=None,
-           wtT=None, wtT16=None, link=None):
+           wtT=None, wtT16=None, link=None, wt16_up=None):
     ks = w.shape[-1]
     return Conv2dFn.apply(x, w, b, stride, ks // 2 if pad is None else pad, in_mode, wt, wt16,
-                          wtT, wtT16, link)
+                          wtT, wtT16, link, wt16_up)
 
 
 # ----------------------------------------------------------------------- relu / pool
@@ -417,8 +427,8 @@ class FastStLossFn(torch.autograd.Function):
         st = V.LossState()
         st.losses = torch.empty(V.N_LOSSES + 2, device=dev, dtype=torch.float32)
         st.fmean = st.losses[6:8]
-        tvg = torch.empty_like(y)
-        ops.tv_loss(y, tv_factor, grad=tvg, out=st.losses[8])
+        tvg = torch.empty_like(y)  # MINUS the TV gradient (see backward)
+        ops.tv_loss(y, tv_factor, grad=tvg, gscale=-1.0, out=st.losses[8])
         total = torch.empty((), device=dev, dtype=torch.float32)
         V.loss_forward(feat, targets, y, _c(c4), st=st, folded_weights=(sw, cw), total=total,
                        extra_slot=True)
@@ -428,7 +438,8 @@ class FastStLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         dx = V.loss_backward(ctx.feat, ctx.st, feature_grad=False)
-        dx.add_(ctx.tvg).mul_(g)
+        # dx = g * (d(VGG losses) + d(TV)) in one launch: g * (dx - (-dTV))
+        ops.diff_scale(dx, ctx.tvg, 1.0, s1=g.reshape(1), out=dx)
         ctx.st = ctx.tvg = None
         return dx, None, None, None, None, None, None
 

@@ -36,7 +36,7 @@ extern "C" const char* stx_last_error_string(void) { return stx::g_err; }
 // one of these
 extern "C" int stx_abi_layout(long long* out, int n) {
   const long long v[] = {
-      (long long)sizeof(stx_conv_params),  (long long)offsetof(stx_conv_params, p2_wt_amax),
+      (long long)sizeof(stx_conv_params),  (long long)offsetof(stx_conv_params, wt16_up),
       (long long)sizeof(stx_wprep_job),    (long long)offsetof(stx_wprep_job, pad_),
       (long long)sizeof(stx_loss_parts),   (long long)offsetof(stx_loss_parts, k),
       (long long)sizeof(stx_gram_fin_job), (long long)offsetof(stx_gram_fin_job, coef_amax),

@@ -23,6 +23,14 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations complete, then
+// s_barrier.  __syncthreads() also drains the wave's outstanding global stores (vmcnt(0)),
+// which in a conv epilogue serialises the whole output write before the LDS phase that
+// follows it (the fused Gram tiles).
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Deterministic block-wide sum (fixed tree order). `red` must hold
 // blockDim.x/64 floats. Result valid in every thread.
 template <int NT>

@@ -583,19 +583,40 @@ extern "C" int stx_conv_weight_prep(const float* w, float* wt, int cout, int cin
   return check_launch("stx_conv_weight_prep");
 }
 
+static int device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
 extern "C" int stx_conv_gram_tiles(const stx_conv_params* pp) {
   if (!pp) return 0;
   const stx_conv_params& p = *pp;
-  // conv16's 256-pixel (64 x 4) tiles through the plain epilogue
+  // conv16's 256-pixel (64 x 4) tiles through the plain epilogue (cout 128: the 8-wave
+  // block of launch16_gram128, raw or ReLU input, and only for a single round of blocks:
+  // with one 135 KB block per CU a second round waits for the first one's epilogue, and
+  // the fast_st batch (B = 8, 512 blocks) measured no faster than the standalone triangle
+  // kernel -- Gatys' 256-block conv2_x: 10.8 us per iteration saved, same-box profile)
+  const int tiles = cdiv(p.wo, 64) * cdiv(p.ho, 4);
   const bool ok = p.wt16 && p.wt16 != (const void*)1 && p.ks == 3 && p.pad == 1 &&
-                  p.stride == 1 && p.cin >= 16 && p.cout == 64 && p.wo > 32 &&
-                  p.wt_batch_stride == 0 && !p.mask && !p.aux && !p.accumulate &&
-                  !p.acc_scale && !p.up_dp && !p.p2_z && !p.relu_out;
-  if (ok) return cdiv(p.wo, 64) * cdiv(p.ho, 4);
+                  p.stride == 1 && p.cin >= 16 &&
+                  (p.cout == 64 ||
+                   (p.cout == 128 && (p.in_mode == STX_IN_RAW || p.in_mode == STX_IN_RELU) &&
+                    (long long)tiles * p.n <= device_cus())) &&
+                  p.wo > 32 && p.wt_batch_stride == 0 && !p.mask && !p.aux && !p.accumulate &&
+                  !p.acc_scale && !p.up_dp && !p.p2_z && !p.relu_out && !p.pool_sum;
+  if (ok) return tiles;
+  if (p.cout != 64) return 0;
   return fewin_gram_tiles(p);  // 3 input channels (VGG conv1_1): 64 x 8 tiles
 }
 
 extern "C" int stx_conv_gram_groups(const stx_conv_params* pp) {
+  if (!pp || pp->cout != 64) return 0;  // the grouped sums: 64-channel tiles only
   const int t = stx_conv_gram_tiles(pp);
   return t > 0 ? cdiv(t, STX_GRAM_GROUP) : 0;
 }
@@ -671,8 +692,29 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
     return STX_E_INVALID;
   }
   if (p.gram_part && !stx_conv_gram_tiles(&p)) {
-    set_error("stx_conv2d: fused Gram partials need the split path, stride 1, cout 64, "
+    set_error("stx_conv2d: fused Gram partials need the split path, stride 1, cout 64 or 128, "
               "wo > 32 and the plain epilogue");
+    return STX_E_INVALID;
+  }
+  if (p.gram_part && p.cout == 128 && 3LL * stx_conv_gram_tiles(&p) * 16384 >= (1ll << 31)) {
+    set_error("stx_conv2d: 128-channel Gram partials per image >= 2 GB");
+    return STX_E_INVALID;
+  }
+  if (p.gram_cnt && p.cout != 64) {
+    set_error("stx_conv2d: gram_cnt (grouped Gram sums) needs cout 64");
+    return STX_E_INVALID;
+  }
+  if (p.wt16_up &&
+      (p.in_mode != STX_IN_UPSAMPLE2 || !p.wt16 || p.wt16 == (const void*)1 || p.ks != 3 ||
+       p.pad != 1 || p.stride != 1 || p.cin < 16 || p.cout <= 4 || p.wo <= 32 ||
+       p.wt_batch_stride || p.mask || p.aux || p.accumulate || p.acc_scale || p.up_dp ||
+       p.p2_z || p.pool_out || p.pool_sum || p.gram_part)) {
+    set_error("stx_conv2d: wt16_up needs an upsampled-input split conv (3x3 stride 1, wo > 32) "
+              "with the plain epilogue (bias / relu_out / out_amax)");
+    return STX_E_INVALID;
+  }
+  if ((p.mse_ref || p.mse_parts) && (!p.mse_ref || !p.mse_parts || !p.gram_part || p.cout != 128)) {
+    set_error("stx_conv2d: mse_ref / mse_parts go together, with gram_part on a 128-channel tap");
     return STX_E_INVALID;
   }
   // fp16 hi/lo split MFMA path (conv16.hip) for the 3x3 stride-1 layers it covers;

@@ -28,6 +28,7 @@
 // (stransfer/network.py:246-314) and the ImageTransformNet 3x3 convs
 // (stransfer/network.py:468-481, 525-609), forward and data-gradient.
 #include <stdlib.h>
+#include <type_traits>
 
 #include "common.h"
 #include "conv_epi.h"
@@ -626,25 +627,48 @@ struct C16v2 {
   static constexpr int WU = 3 * 4 * BM;                // weight units per step: [tap][P][cg][co]
   static constexpr int NWU = WU / NT;
   static constexpr int WB = WU * 16;                   // one weight buffer
-  static constexpr int LDS_BYTES = 2 * HB + 2 * WB;
+  static constexpr int LOOP_BYTES = 2 * HB + 2 * WB;
+  // (the 128-channel fused Gram planes of a WM = 2, 64 x 4 tile: 135 KB, one block per CU)
+  static constexpr int LDS_BYTES =
+      WM == 2 && TW == 64 && NI == 2 && LOOP_BYTES < GramPlanes128::BYTES ? GramPlanes128::BYTES
+                                                                           : LOOP_BYTES;
   static_assert(WU % NT == 0, "weight units per thread");
   static_assert(16 * NPIX * 4 + 16 * BM * 4 <= LDS_BYTES, "phase-2 staging fits");
   static_assert(TW != 64 || NI != 2 || GramPlanes<256>::BYTES <= LDS_BYTES, "Gram planes fit");
 };
 
+// UPP geometry: the parity-class form of a conv over a nearest x2 upsampled input
+// (stx_conv_params.wt16_up).  A block takes 64 output columns x 4 output rows of ONE row
+// parity a (rows ty0 + 2 wn + a), the N-tile j of a wave the column parity b = j (x =
+// 2 l32 + j): every output row / column reads 2 input rows / columns, so the halo is the
+// input's own 5 x 34 window, K steps are (16-channel chunk, ry) and each step holds the
+// 4 (b, rx) taps' weights of parity a.
+struct C16up {
+  static constexpr int NT = 256, BM = 64, NPIX = 256, TH = 8;
+  static constexpr int RH = 5, RW = 34, NPOS = RH * RW;
+  static constexpr int NITEM = 2 * NPOS, NIT = (NITEM + NT - 1) / NT;
+  static constexpr int HB = 2 * NITEM * 16;
+  static constexpr int WU = 4 * 4 * BM, NWU = WU / NT, WB = WU * 16;
+  static constexpr int LOOP_BYTES = 2 * HB + 2 * WB, LDS_BYTES = LOOP_BYTES;
+  static_assert(16 * NPIX * 4 + 16 * BM * 4 <= LDS_BYTES, "phase-2 staging fits");
+};
+
 template <int TW, int LM, int P2, int NI, int WM = 1>
 __global__ void __launch_bounds__(256 * WM, WM == 2 ? 1 : ((NI == 1 && TW <= 32) ? 3 : 2))
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
-  using C = C16v2<TW, NI, WM>;
-  constexpr int NT = C::NT;
   // PAR: the zero-dilated data gradient (a stride-2 conv's input gradient) on 64 x 4 tiles
   // whose N-tiles are output parity classes: of the 9 taps x 3 kernel rows only those that
   // meet the dilated input's non-zero (even) positions run -- a quarter of the MFMAs
   constexpr bool PAR = LM == STX_IN_DILATE2 && TW == 64 && NI == 2 && WM == 1 && P2 == 0;
-  constexpr bool RP = TW == 64 && NI == 2 && !PAR;  // row-pair tiles (fused pool / unpool)
+  // UPP: the nearest-x2 upsampled input as four output-parity 2x2 convs (C16up)
+  constexpr bool UPP = LM == STX_IN_UPSAMPLE2 && TW == 64 && NI == 2 && WM == 1 && P2 == 0;
+  using C = std::conditional_t<UPP, C16up, C16v2<TW, NI, WM>>;
+  constexpr int NT = C::NT;
+  constexpr int KS = UPP ? 2 : 3;  // K steps per 16-channel chunk
+  constexpr bool RP = TW == 64 && NI == 2 && !PAR && !UPP;  // row-pair tiles (pool / unpool)
   static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
   static_assert(P2 != 2, "1x1 mode: v1 kernel");
-  static_assert(WM == 1 || (P2 == 0 && !RP), "WM = 2: plain epilogue only");
+  static_assert(WM == 1 || P2 == 0, "WM = 2: plain epilogue only");
   constexpr int BM = C::BM;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
 
@@ -667,9 +691,9 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   // Gatys 679.6 -> 674.5 us per iteration, fast_st within noise)
   if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
   const int nchunks = cdiv(p.cin, 16);
-  const int nsteps = 3 * nchunks;
+  const int nsteps = KS * nchunks;
   const int ex = amax_exp(read_amax(p.in_amax));
-  const int ew = amax_exp(read_amax(p.w_amax));
+  const int ew = amax_exp(read_amax(p.w_amax)) + (UPP ? 2 : 0);  // (UPP: |W'| <= 4 max|w|)
   const float sx = __builtin_ldexpf(1.f, 15 - ex);
   const float descale = __builtin_ldexpf(1.f, ex + ew - 30);
 
@@ -679,8 +703,8 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
 
   // weight units of a step: u = tid + q*256 -> (seg = tap*4 + P*2 + cg, co)
   const int cout64 = rup(p.cout, 64);
-  const uint32_t chunk_bytes = (uint32_t)(36 * cout64 * 16);
-  const uint32_t step_bytes = (uint32_t)(12 * cout64 * 16);
+  const uint32_t chunk_bytes = (uint32_t)((UPP ? 32 : 36) * cout64 * 16);
+  const uint32_t step_bytes = (uint32_t)((UPP ? 16 : 12) * cout64 * 16);
   uint32_t woff[C::NWU];
 #pragma unroll
   for (int q = 0; q < C::NWU; ++q) {
@@ -688,11 +712,30 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     const int seg = u / BM, co = u - seg * BM;
     woff[q] = (uint32_t)((seg * cout64 + co0 + co) * 16);
   }
-  const char* __restrict__ wt16 = reinterpret_cast<const char*>(p.wt16);
+  const char* __restrict__ wt16 = reinterpret_cast<const char*>(UPP ? p.wt16_up : p.wt16);
 
   uint32_t hoff[C::NIT];
-  int ty0 = 0, tx0 = 0;
+  int ty0 = 0, tx0 = 0, upa = 0;
   auto halo_offsets = [&](int tile) {
+    if constexpr (UPP) {
+      // tile -> (8-row band, row parity a, 64-column band); the halo: input rows
+      // ty0/2 + a - 1 .. +4, columns tx0/2 - 1 .. +33
+      const int r2 = tile / tiles_x;
+      upa = r2 & 1;
+      ty0 = (r2 >> 1) * C::TH;
+      tx0 = (tile % tiles_x) * TW;
+      const int yb = (ty0 >> 1) + upa - 1, xb = (tx0 >> 1) - 1;
+#pragma unroll
+      for (int r = 0; r < C::NIT; ++r) {
+        const int idx = tid + r * NT;
+        const int cg = idx / C::NPOS, pos = idx - cg * C::NPOS;
+        const int rr = pos / C::RW, cc = pos - rr * C::RW;
+        const int sy = yb + rr, sx_ = xb + cc;
+        const bool ok = idx < C::NITEM && sy >= 0 && sx_ >= 0 && sy < p.h && sx_ < p.w;
+        hoff[r] = ok ? (uint32_t)((cg * 8) * plane_in + sy * p.w + sx_) * 4u : BUF_OOB;
+      }
+      return;
+    }
     ty0 = (tile / tiles_x) * C::TH;
     tx0 = (tile % tiles_x) * TW;
     const int vy0 = ty0 - 1, vx0 = tx0 - 1;
@@ -753,9 +796,11 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
       *reinterpret_cast<f16x8*>(hb + (C::NITEM + idx) * 16) = lo;
     }
   };
-  auto ld_w = [&](int step) {  // step = chunk * 3 + kh
-    const int chunk = step / 3, kh = step - 3 * chunk;
-    const auto rw = make_srd(reinterpret_cast<const float*>(wt16 + (size_t)chunk * chunk_bytes +
+  auto ld_w = [&](int step) {  // step = chunk * KS + kh (UPP: ry)
+    const int chunk = step / KS, kh = step - KS * chunk;
+    const size_t base = UPP ? (size_t)upa * nchunks * chunk_bytes : 0;  // (UPP: parity a)
+    const auto rw = make_srd(reinterpret_cast<const float*>(wt16 + base +
+                                                            (size_t)chunk * chunk_bytes +
                                                             (size_t)kh * step_bytes),
                              step_bytes);
 #pragma unroll
@@ -774,7 +819,9 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   for (int j = 0; j < NI; ++j) {
     int ty, tx;
     tile_pix<TW, RP, NI, PAR>(wn, j, l32, ty, tx);
-    boff[j] = (h * C::NPOS + ty * C::RW + tx) * 16;
+    // UPP: halo row wn (+ ry), column l32 + j (+ rx) -- see C16up
+    boff[j] = UPP ? (h * C::NPOS + wn * C::RW + l32 + j) * 16
+                  : (h * C::NPOS + ty * C::RW + tx) * 16;
   }
   const int aoff = 2 * C::HB + (h * BM + wm * 64 + l32) * 16;
 
@@ -792,7 +839,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     if (nsteps > 1) ld_w(1);
     if (nchunks > 1) {
 #pragma unroll
-      for (int r = 0; r < C::NIT; r += 3) ld_halo(1, r);
+      for (int r = 0; r < C::NIT; r += KS) ld_halo(1, r);
     }
     __syncthreads();
 
@@ -807,8 +854,8 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     for (int c = 0; c < nchunks; ++c) {
       const int hbo = (c & 1) * C::HB;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int s = 3 * c + k;
+      for (int k = 0; k < KS; ++k) {
+        const int s = KS * c + k;
         const int wbo = (s & 1) * C::WB;
         const char* abase = smem + aoff + wbo;
         const char* bbase[NI];
@@ -831,6 +878,42 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
             for (int j = 0; j < NI; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
         };
+        if constexpr (UPP) {
+          // staging for step s+1 first, then this step's 4 taps (b = j, rx) at input row
+          // wn + ry (= k) of the halo: 2 A fragments and 2 B fragments per tap
+          if (s + 1 < nsteps) st_w((s + 1) & 1);
+          if (c + 1 < nchunks) {
+#pragma unroll
+            for (int r = k; r < C::NIT; r += KS) st_halo((c + 1) & 1, r);
+          }
+          if (s + 2 < nsteps) ld_w(s + 2);
+          {
+            const int cn = k < KS - 1 ? c + 1 : c + 2;
+            if (cn < nchunks) {
+#pragma unroll
+              for (int r = (k + 1) % KS; r < C::NIT; r += KS) ld_halo(cn, r);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int rx = 0; rx < 2; ++rx) {
+              f16x8 ah[2], al[2];
+              rdA(2 * j + rx, 0, ah);
+              rdA(2 * j + rx, 1, al);
+              const f16x8 bh = *reinterpret_cast<const f16x8*>(bbase[j] + (k * C::RW + rx) * 16);
+              const f16x8 bl =
+                  *reinterpret_cast<const f16x8*>(bbase[j] + (C::NITEM + k * C::RW + rx) * 16);
+#pragma unroll
+              for (int i = 0; i < 2; ++i) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, acc[i][j], 0, 0, 0);
+              }
+            }
+          __syncthreads();
+          continue;
+        }
         if constexpr (PAR) {
           // staging for step s+1 first (every wave), then this step's taps, only in the
           // waves whose output row meets a non-zero dilated row at this kernel row (the
@@ -923,10 +1006,16 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     EpiTile et{n, co0, ty0, tx0, wm, wn, h, l32};
     et.tile = tile;
     et.ntiles = ntiles;
-    if constexpr (PAR) {
+    if constexpr (UPP) {
+      // the PAR pixel mapping (x = 2 l32 + j, y = wn) with rows 2 wn + a: paired stores
+      et.wn = 2 * wn;
+      et.ty0 = ty0 + upa;
+      conv_epilogue_plain<TW, NI, false, true>(acc, p, et, descale, smem);  // (launch16up)
+    } else if constexpr (PAR) {
       conv_epilogue_plain<TW, NI, false, true>(acc, p, et, descale, smem);  // (launch16v2)
     } else if constexpr (WM == 2) {
-      conv_epilogue_plain<TW, NI, RP>(acc, p, et, descale, smem);  // (eligibility: launch16v2)
+      // (eligibility: launch16v2 / launch16_gram128)
+      conv_epilogue_plain<TW, NI, RP, false, WM>(acc, p, et, descale, smem);
     } else if constexpr (P2 == 3) {
       // (eligibility: launch16v2 -- data gradient + mask + the phase, bias / out_amax only)
       const int ez = amax_exp(read_amax(p.p2_amax));
@@ -1028,6 +1117,16 @@ static int launch16v2(const stx_conv_params& p, hipStream_t st) {
                          tiles_x, ntiles);
       return check_launch("stx_conv2d(f16x3 v2, 128 couts)");
     }
+#ifdef STX_AB  // STX_FORCE_WM2=1: 8-wave 128-cout blocks on 64 x 4 tiles without the Gram (A/B)
+  if constexpr (NI == 2 && TW == 64 && (LM == STX_IN_RAW || LM == STX_IN_RELU))
+    if (STX_KNOB("STX_FORCE_WM2", 0) && p.cout % 128 == 0 && !p.mask && !p.accumulate &&
+        !p.acc_scale && !p.up_dp && !p.pool_sum && !p.gram_part && !p.aux) {
+      dim3 g2(ntiles, p.cout / 128, p.n);
+      hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<TW, LM, 0, NI, 2>), g2, dim3(512), 0, st, p,
+                         tiles_x, ntiles);
+      return check_launch("stx_conv2d(f16x3 v2, 128 couts, forced)");
+    }
+#endif
   if constexpr (LM == STX_IN_DILATE2 && TW == 64 && NI == 2)
     if (p.mask || p.accumulate || p.acc_scale || p.up_dp || p.pool_out || p.pool_sum ||
         p.gram_part || (p.aux && p.relu_out)) {
@@ -1062,8 +1161,22 @@ static int launch16(const stx_conv_params& p, hipStream_t st) {
 // 256-pixel tiles (NI = 2) unless that grid leaves CUs idle: then 128-pixel tiles
 // (twice the blocks; not with the fused pool output or the Gram-backward phase,
 // which rely on the 256-pixel row-pair tile)
+// the 128-channel fused Gram (conv_gram_tile128): one 8-wave block per 64 x 4 tile holds
+// all 128 couts (stx_conv_gram_tiles admits only these: plain epilogue, raw / ReLU input)
+template <int LM>
+static int launch16_gram128(const stx_conv_params& p, hipStream_t st) {
+  using C = C16v2<64, 2, 2>;
+  const int tiles_x = cdiv(p.wo, 64), tiles_y = cdiv(p.ho, C::TH);
+  const int ntiles = tiles_x * tiles_y;
+  hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<64, LM, 0, 2, 2>), dim3(ntiles, 1, p.n), dim3(512),
+                     0, st, p, tiles_x, ntiles);
+  return check_launch("stx_conv2d(f16x3 v2, 128 couts + fused Gram)");
+}
+
 template <int TW, int LM>
 static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
+  if constexpr (TW == 64 && (LM == STX_IN_RAW || LM == STX_IN_RELU))
+    if (p.gram_part && p.cout == 128) return launch16_gram128<LM>(p, st);
   const long long blocks2 = (long long)cdiv(p.wo, TW) * cdiv(p.ho, 256 / TW) *
                             cdiv(p.cout, 64) * p.n;
   // 256-pixel-tile grids smaller than two resident rounds use 128-px tiles
@@ -1088,7 +1201,22 @@ static int launch16_ni(const stx_conv_params& p, hipStream_t st) {
   if constexpr (TW == 64 && LM != STX_IN_RAW)
     if (!p.pool_out && !p.gram_part && !p.p2_z && !p.up_dp)
       return launch16<32, LM, 2>(p, st);
-  return launch16<TW, LM, 2>(p, st);
+  if constexpr (TW == 64 && LM == STX_IN_UPSAMPLE2) {
+    // (the 64 x 4 instantiation of this loader is the parity-class kernel, launch16up)
+    set_error("stx_conv2d: an upsampled-input conv takes no fused pool output / Gram / "
+              "unpool epilogue");
+    return STX_E_INVALID;
+  } else {
+    return launch16<TW, LM, 2>(p, st);
+  }
+}
+
+// the parity-class form of a conv over a nearest x2 upsampled input (stx_conv_params.wt16_up)
+static int launch16up(const stx_conv_params& p, hipStream_t st) {
+  const int tiles_x = cdiv(p.wo, 64), ntiles = tiles_x * 2 * cdiv(p.ho, C16up::TH);
+  hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<64, STX_IN_UPSAMPLE2, 0, 2>),
+                     dim3(ntiles, cdiv(p.cout, 64), p.n), dim3(256), 0, st, p, tiles_x, ntiles);
+  return check_launch("stx_conv2d(f16x3 v2, upsampled input as parity classes)");
 }
 
 template <int LM>
@@ -1137,6 +1265,60 @@ __device__ __forceinline__ void weight_prep16_body(const float* __restrict__ w,
     const _Float16 vh = (_Float16)v;
     out[i] = P == 0 ? vh : (_Float16)(v - (float)vh);
   }
+}
+
+// The parity-class slab of a conv behind a nearest x2 upsampling (the ImageTransformNet's
+// UpsampleConvLayer, stransfer/network.py:578-600): output pixel (2y + a, 2x + b) of the
+// 3x3 conv over the upsampled input is a 2x2 conv over the input itself,
+//   sum_{ry, rx} W'[a][b][ry][rx] x[y - 1 + a + ry][x - 1 + b + rx],
+// W'[a][b][ry][rx] = sum of W[kh][kw] over kh in K(a, ry), kw in K(b, rx),
+// K(0,0) = {0}, K(0,1) = {1,2}, K(1,0) = {0,1}, K(1,1) = {2} (rows y-1 / y or y / y+1 of the
+// input: the zero padding of the upsampled image is the input's own).  Slab
+// [a][cin16/16][ry][b*2+rx][P][cg][cout64][8] fp16, split at 2^(15 - e - 2) (|W'| <= 4
+// max|w| < 2^(e+2)); sums in kh, kw order.
+__device__ __forceinline__ void weight_prep16up_body(const float* __restrict__ w,
+                                                     _Float16* __restrict__ out,
+                                                     const float* __restrict__ w_amax, int cout,
+                                                     int cin, int gin16, int gout64, long long i0,
+                                                     long long step) {
+  const int total = 2 * gin16 * 2 * 4 * 2 * 2 * gout64 * 8;
+  const float sw = __builtin_ldexpf(1.f, 13 - amax_exp(read_amax(w_amax)));
+  for (int i = (int)i0; i < total; i += (int)step) {
+    const int e = i & 7;
+    unsigned r = (unsigned)i >> 3;
+    const int co = (int)(r % (unsigned)gout64);
+    r /= (unsigned)gout64;
+    const int cg = (int)(r & 1);
+    const int P = (int)((r >> 1) & 1);
+    const int t4 = (int)((r >> 2) & 3);
+    const int ry = (int)((r >> 4) & 1);
+    r >>= 5;
+    const int chunk = (int)(r % (unsigned)gin16);
+    const int a = (int)(r / (unsigned)gin16);
+    const int b = t4 >> 1, rx = t4 & 1;
+    const int ci = chunk * 16 + cg * 8 + e;
+    const int kh0 = a == 0 ? (ry == 0 ? 0 : 1) : (ry == 0 ? 0 : 2);
+    const int kh1 = a == 0 ? (ry == 0 ? 0 : 2) : (ry == 0 ? 1 : 2);
+    const int kw0 = b == 0 ? (rx == 0 ? 0 : 1) : (rx == 0 ? 0 : 2);
+    const int kw1 = b == 0 ? (rx == 0 ? 0 : 2) : (rx == 0 ? 1 : 2);
+    float v = 0.f;
+    if (co < cout && ci < cin) {
+      const float* wp = w + ((size_t)co * cin + ci) * 9;
+      for (int kh = kh0; kh <= kh1; ++kh)
+        for (int kw = kw0; kw <= kw1; ++kw) v += wp[kh * 3 + kw];
+    }
+    v *= sw;
+    const _Float16 vh = (_Float16)v;
+    out[i] = P == 0 ? vh : (_Float16)(v - (float)vh);
+  }
+}
+
+__global__ void weight_prep16up_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
+                                       const float* __restrict__ w_amax, int cout, int cin,
+                                       int gin16, int gout64) {
+  weight_prep16up_body(w, out, w_amax, cout, cin, gin16, gout64,
+                       blockIdx.x * (long long)blockDim.x + threadIdx.x,
+                       (long long)gridDim.x * blockDim.x);
 }
 
 __global__ void weight_prep16_kernel(const float* __restrict__ w, _Float16* __restrict__ out,
@@ -1258,6 +1440,9 @@ __global__ void __launch_bounds__(256) weight_prep_batch_kernel(WprepJobs b) {
   if (t.kind == STX_WPREP_F16)
     weight_prep16_body(t.w, reinterpret_cast<_Float16*>(t.slab), t.w_amax, t.cout, t.cin,
                        t.transpose, b.gin[j], b.gout[j], i0, step);
+  else if (t.kind == STX_WPREP_F16UP)
+    weight_prep16up_body(t.w, reinterpret_cast<_Float16*>(t.slab), t.w_amax, t.cout, t.cin,
+                         b.gin[j] / 16, b.gout[j], i0, step);
   else
     weight_prep32_body(t.w, reinterpret_cast<float*>(t.slab), t.cout, t.cin, t.ks, t.transpose,
                        b.gin[j], b.gout[j], i0, step);
@@ -1378,7 +1563,9 @@ int conv2d_f16x3(const stx_conv_params& p, hipStream_t st) {
     case STX_IN_RAW: return dispatch16_tw<STX_IN_RAW>(p, st);
     case STX_IN_RELU: return dispatch16_tw<STX_IN_RELU>(p, st);
     case STX_IN_RELU_POOL2: return dispatch16_tw<STX_IN_RELU_POOL2>(p, st);
-    case STX_IN_UPSAMPLE2: return dispatch16_tw<STX_IN_UPSAMPLE2>(p, st);
+    case STX_IN_UPSAMPLE2:
+      if (p.wt16_up) return launch16up(p, st);  // (eligibility: stx_conv2d)
+      return dispatch16_tw<STX_IN_UPSAMPLE2>(p, st);
     case LM_S2:  // stride 2 (raw input): 32 x 4 output tiles, two blocks per CU
       if (p.pool_out || p.p2_z) {
         set_error("stx_conv2d: stride 2 takes no fused pool output / Gram phase");
@@ -1422,6 +1609,31 @@ extern "C" int stx_amax(const float* x, long long n, float* out, void* stream) {
   return check_launch("stx_amax");
 }
 
+extern "C" size_t stx_conv_weight16up_bytes(int cin, int cout) {
+  if (cin <= 0 || cout <= 0) return 0;
+  return (size_t)2 * rup(cin, 16) * 2 * 4 * 2 * rup(cout, 64) * sizeof(_Float16);
+}
+
+extern "C" int stx_conv_weight_prep16_up(const float* w, void* wt16_up, float* w_amax, int cout,
+                                         int cin, void* stream) {
+  if (!w || !wt16_up || !w_amax || cout <= 0 || cin <= 0) {
+    set_error("stx_conv_weight_prep16_up: pointers non-NULL, cout / cin > 0");
+    return STX_E_INVALID;
+  }
+  int rc = stx_amax(w, (long long)cout * cin * 9, w_amax, stream);
+  if (rc) return rc;
+  const long long total = (long long)rup(cin, 16) * 32 * rup(cout, 64);
+  if (total >= (1ll << 31)) {
+    set_error("stx_conv_weight_prep16_up: slab too large");
+    return STX_E_INVALID;
+  }
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(weight_prep16up_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w,
+                     reinterpret_cast<_Float16*>(wt16_up), w_amax, cout, cin, rup(cin, 16) / 16,
+                     rup(cout, 64));
+  return check_launch("stx_conv_weight_prep16_up");
+}
+
 extern "C" int stx_conv_weight_prep16_pair(const float* w, void* wt16, void* wtT16, float* w_amax,
                                            int cout, int cin, int ks, void* stream) {
   if (ks != 3 || !w || !wt16 || !wtT16 || !w_amax || cout <= 0 || cin <= 0) {
@@ -1455,21 +1667,22 @@ extern "C" int stx_conv_weight_prep_batch(const stx_wprep_job* jobs, int njobs, 
   for (int j = 0; j < njobs; ++j) {
     const stx_wprep_job& t = jobs[j];
     if (!t.w || !t.slab || t.cout <= 0 || t.cin <= 0 ||
-        (t.kind != STX_WPREP_F32 && t.kind != STX_WPREP_F16) ||
-        (t.kind == STX_WPREP_F16 && (t.ks != 3 || !t.w_amax))) {
+        (t.kind != STX_WPREP_F32 && t.kind != STX_WPREP_F16 && t.kind != STX_WPREP_F16UP) ||
+        (t.kind != STX_WPREP_F32 && (t.ks != 3 || !t.w_amax)) ||
+        (t.kind == STX_WPREP_F16UP && t.transpose)) {
       set_error("stx_conv_weight_prep_batch: job %d invalid", j);
       return STX_E_INVALID;
     }
     const int gin = t.transpose ? t.cout : t.cin, gout = t.transpose ? t.cin : t.cout;
     long long total;
-    if (t.kind == STX_WPREP_F16) {
+    if (t.kind != STX_WPREP_F32) {
       if (reinterpret_cast<uintptr_t>(t.w) & 15) {
         set_error("stx_conv_weight_prep_batch: job %d weight not 16-byte aligned", j);
         return STX_E_INVALID;
       }
       b.gin[j] = rup(gin, 16);
       b.gout[j] = rup(gout, 64);
-      total = (long long)b.gin[j] * 9 * 2 * b.gout[j];
+      total = (long long)b.gin[j] * (t.kind == STX_WPREP_F16UP ? 32 : 18) * b.gout[j];
       bool seen = false;  // the forward / data-gradient slabs of a weight share one group
       for (int k = 0; k < na; ++k) {
         if (a.out[k] == t.w_amax) {

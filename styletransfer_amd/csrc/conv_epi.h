@@ -66,7 +66,7 @@ __device__ __forceinline__ void block_max_to(float* group, float m) {
   }
   const int tid = threadIdx.x;
   if ((tid & 63) == 0) red[tid >> 6] = m;
-  __syncthreads();
+  lds_sync();  // (not a __syncthreads: the caller's output stores need not drain first)
   if (tid == 0) {
     float r = red[0];
     for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
@@ -97,15 +97,16 @@ struct GramPlanes {
   static constexpr int BYTES = 2 * 64 * HP * 2 + 16;  // hi + lo planes, 4 floats of max
 };
 
-// block max over 4 waves (IEEE bits of |y|) -> the scale exponent e (barrier inside)
+// block max over NW waves (IEEE bits of |y|) -> the scale exponent e (barrier inside)
+template <int NW = 4>
 __device__ __forceinline__ int gram_block_exp(uint32_t m, float* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = __uint_as_float(m);
-  __syncthreads();
+  lds_sync();  // (the epilogue's y stores stay in flight)
   uint32_t bm = 0u;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) bm = max(bm, __float_as_uint(red[w]));
+  for (int w = 0; w < NW; ++w) bm = max(bm, __float_as_uint(red[w]));
   int e = 0;
   frexpf(__uint_as_float(bm), &e);
   return min(max(e, -60), 60);
@@ -151,6 +152,35 @@ __device__ __forceinline__ void gram_store(float* out, const f32x16& g, int wave
     const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
     out[(I * 32 + row) * 64 + J * 32 + l32] = g[r];
     if (I != J) out[(J * 32 + l32) * 64 + I * 32 + row] = g[r];
+  }
+}
+
+// gram_store through LDS: waves 0..2's blocks (and the mirror of (0,1)) into O (>= 64 x 68
+// floats of LDS no wave reads any more once every wave is past the first barrier), then
+// coalesced 16-B stores by all NT threads -- the scattered 4-B stores (the mirrored block
+// a column per lane) cost ~20 us per 1024-block launch (measurement build)
+template <int NT>
+__device__ __forceinline__ void gram_store_lds(float* out, const f32x16& g, int wave, int h,
+                                               int l32, float* O) {
+  constexpr int OP = 68;
+  lds_sync();
+  if (wave < 3) {
+    const int I = wave == 2 ? 1 : 0, J = wave == 0 ? 0 : 1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      O[(I * 32 + row) * OP + J * 32 + l32] = g[r];
+      if (I != J) O[(J * 32 + l32) * OP + I * 32 + row] = g[r];
+    }
+  }
+  lds_sync();
+  const auto rg = make_srd(out, 16384u);
+#pragma unroll
+  for (int k = 0; k < 1024 / NT; ++k) {  // 64 rows x 16 float4
+    const int idx = threadIdx.x + NT * k, row = idx >> 4, c4 = idx & 15;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(O + row * OP + 4 * c4);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rg,
+                                           (uint32_t)(row * 64 + 4 * c4) * 4u, 0, 0);
   }
 }
 
@@ -229,7 +259,14 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
   _Float16* H = reinterpret_cast<_Float16*>(smem);
   float* red = reinterpret_cast<float*>(smem + GP::BYTES - 16);
   const int wave = threadIdx.x >> 6, h = t.h, l32 = t.l32;
+#ifdef STX_AB  // stage cut-off for timing (aux_scale = 1..3; aux is unused with gram_part)
+  const int dbg = (int)p.aux_scale;
+  if (dbg == 4) return;
+#else
+  constexpr int dbg = 0;
+#endif
   const int e = gram_block_exp(vmax_u, red);
+  if (dbg == 1) return;
   const float sx = __builtin_ldexpf(1.f, 15 - e);
   // two neighbouring pixels per 4-B LDS store: for the registers (r, r+1) (channels ch,
   // ch+1) the lane pair (px even, px+1) swaps one value by DPP, then the even lane holds
@@ -258,7 +295,8 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
         *reinterpret_cast<f16x2*>(H + ch * GP::HP + p0) = hi;
         *reinterpret_cast<f16x2*>(H + (64 + ch) * GP::HP + p0) = lo;
       }
-  __syncthreads();
+  lds_sync();
+  if (dbg == 2) return;
   f32x16 g;
 #pragma unroll
   for (int q = 0; q < 16; ++q) g[q] = 0.f;
@@ -270,10 +308,195 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
   }
   const int tix = t.tile >= 0 ? t.tile : (int)blockIdx.x;
   const int ntl = t.tile >= 0 ? t.ntiles : (int)gridDim.x;
+  if (dbg == 3) {
+    if (g[0] == 12345.f) p.gram_part[0] = g[1];  // (keeps the MFMAs)
+    return;
+  }
   if (p.gram_cnt) {  // (red's block maxima were read before the barrier above)
     gram_store_grouped(p, blockIdx.z, tix, ntl, g, wave, h, l32, red);
-  } else if (wave < 3) {
-    gram_store(p.gram_part + ((size_t)blockIdx.z * ntl + tix) * 4096, g, wave, h, l32);
+    return;
+  }
+  gram_store_lds<256>(p.gram_part + ((size_t)blockIdx.z * ntl + tix) * 4096, g, wave, h, l32,
+                      reinterpret_cast<float*>(smem));
+}
+
+// The 128-channel taps (VGG conv2_1 / conv2_2): an 8-wave (WM = 2) block holds all 128
+// channels of its 256-pixel tile, so the whole C x C partial of the tile comes out of the
+// epilogue (the standalone triangle kernel's re-read of y is gone).  Same split as the
+// 64-channel tile (block-local power-of-two scale, fp16 hi/lo planes [plane][channel]
+// [pixel], 3 MFMAs per 16 pixels); the 10 upper-triangle 32 x 32 blocks go to waves
+// 0..7 (waves 0 and 1 take blocks 8 and 9 too) and are stored in the 64 x 64-tile layout
+// of the triangle kernel: gram_part + ((n * 3 + u) * T + t) * 4096, u the tile (0,0),
+// (0,1), (1,1), diagonal tiles with the mirrored lower-left quadrant.
+// MSE (p.mse_ref, the content target at conv2_2): also the block's sums of (y - ref)^2
+// and (relu y - relu ref)^2 over its valid outputs -> mse_parts[2 (n T + t) + 0/1] (the
+// content / feature losses' pass over y, stransfer/network.py:134-201).
+struct GramPlanes128 {
+  static constexpr int HP = 256 + 8;                   // pitch (halves)
+  static constexpr int BYTES = 2 * 128 * HP * 2 + 128;  // hi + lo planes, 32 floats of sums
+};
+
+template <int TW, bool ROWPAIR>
+__device__ __forceinline__ void conv_gram_tile128(const f32x16 (&acc)[2][2],
+                                                  const stx_conv_params& p, const EpiTile& t,
+                                                  const bool (&lane_ok)[2],
+                                                  const uint32_t (&vo)[2], uint32_t vmax_u,
+                                                  char* smem) {
+  using GP = GramPlanes128;
+  constexpr int HP = GP::HP;
+  _Float16* H = reinterpret_cast<_Float16*>(smem);
+  float* red = reinterpret_cast<float*>(smem + GP::BYTES - 128);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = t.h, l32 = t.l32;
+  const int tix = t.tile >= 0 ? t.tile : (int)blockIdx.x;
+  const int ntl = t.tile >= 0 ? t.ntiles : (int)gridDim.x;
+  // the content target's values at this lane's outputs, in flight during the staging
+#ifdef STX_AB  // stage cut-off for timing (aux_scale = 1..4; aux is unused with gram_part)
+  const int dbg = (int)p.aux_scale;
+  if (dbg == 4) return;
+#else
+  constexpr int dbg = 0;
+#endif
+  const bool mse = p.mse_ref != nullptr;
+  float rf[2][2][16];
+  if (mse) {
+    const size_t plane = (size_t)p.ho * p.wo;
+    const uint32_t pb = (uint32_t)plane * 4u;
+    const int co_w = t.co0 + t.wm * 64;
+    const auto rr = make_srd(p.mse_ref + ((size_t)t.n * p.cout + co_w) * plane,
+                             (uint32_t)max(0, p.cout - co_w) * pb);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          rf[j][i][r] = buf_ld(rr, vo[j] + (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * pb);
+  }
+  const int e = gram_block_exp<8>(vmax_u, red);
+  if (dbg == 1) return;
+  const float sx = __builtin_ldexpf(1.f, 15 - e);
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  const int q = l32 & 1;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float va = lane_ok[j] ? acc[i][j][r] * sx : 0.f;
+        const float vb = lane_ok[j] ? acc[i][j][r + 1] * sx : 0.f;
+        const float recv = __int_as_float(
+            __builtin_amdgcn_mov_dpp(__float_as_int(q ? va : vb), 0xB1, 0xF, 0xF, false));
+        const float v0 = q ? recv : va, v1 = q ? vb : recv;
+        const int ch = t.wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h + q;
+        const int p0 = t.wn * 64 + j * 32 + l32 - q;  // any pixel order: a sum over pixels
+        f16x2 hi, lo;
+        hi[0] = (_Float16)v0;
+        hi[1] = (_Float16)v1;
+        lo[0] = (_Float16)(v0 - (float)hi[0]);
+        lo[1] = (_Float16)(v1 - (float)hi[1]);
+        *reinterpret_cast<f16x2*>(H + ch * HP + p0) = hi;
+        *reinterpret_cast<f16x2*>(H + (128 + ch) * HP + p0) = lo;
+      }
+  if (mse) {
+    float ms = 0.f, msr = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = acc[i][j][r], c = rf[j][i][r];
+          const float d = lane_ok[j] ? v - c : 0.f;
+          const float dr = lane_ok[j] ? fmaxf(v, 0.f) - fmaxf(c, 0.f) : 0.f;
+          ms += d * d;
+          msr += dr * dr;
+        }
+    // fixed-order block sums (the red slots were last read before the staging)
+    ms = wave_sum(ms);
+    msr = wave_sum(msr);
+    if ((threadIdx.x & 63) == 0) {
+      red[8 + wave] = ms;  // (slots 0..7: the block max, possibly still being read)
+      red[16 + wave] = msr;
+    }
+    lds_sync();  // (also: the planes are complete)
+    if (threadIdx.x == 0) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        s0 += red[8 + w];
+        s1 += red[16 + w];
+      }
+      float* mp = p.mse_parts + 2 * ((size_t)blockIdx.z * ntl + tix);
+      mp[0] = s0;
+      mp[1] = s1;
+    }
+  } else {
+    lds_sync();
+  }
+  if (dbg == 2) return;
+  const float inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  constexpr int LO = 128 * HP;
+  // the upper-triangle blocks b = wave (and 8 + wave for waves 0, 1), row-major over the
+  // 4 x 4 block grid
+  f32x16 g[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int b = wave + 8 * q;
+    if (b >= 10) break;
+    const int bi = b < 4 ? 0 : b < 7 ? 1 : b < 9 ? 2 : 3;
+    const int bj = bi + b - (bi == 0 ? 0 : bi == 1 ? 4 : bi == 2 ? 7 : 9);
+    const _Float16* ra = H + (bi * 32 + l32) * HP + 8 * h;
+    const _Float16* rb = H + (bj * 32 + l32) * HP + 8 * h;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) g[q][k] = 0.f;
+#pragma unroll 4
+    for (int ks = 0; ks < 16; ++ks) {
+      const h8 ah = *reinterpret_cast<const h8*>(ra + ks * 16);
+      const h8 al = *reinterpret_cast<const h8*>(ra + LO + ks * 16);
+      const h8 bh = *reinterpret_cast<const h8*>(rb + ks * 16);
+      const h8 bl = *reinterpret_cast<const h8*>(rb + LO + ks * 16);
+      g[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, g[q], 0, 0, 0);
+      g[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, g[q], 0, 0, 0);
+      g[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, g[q], 0, 0, 0);
+    }
+  }
+  if (dbg == 3) {
+    if (g[0][0] == 12345.f) p.gram_part[0] = g[0][1] + g[1][1];  // (keeps the MFMAs)
+    return;
+  }
+  lds_sync();  // every wave's plane reads are done: the planes become the output tiles
+  // the three 64 x 64 tiles in LDS (pitch 68 floats: the mirrored column writes of a wave
+  // spread over 16 banks), then streamed out with coalesced 16-B stores
+  constexpr int OP = 68;
+  float* O = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int b = wave + 8 * q;
+    if (b >= 10) break;
+    const int bi = b < 4 ? 0 : b < 7 ? 1 : b < 9 ? 2 : 3;
+    const int bj = bi + b - (bi == 0 ? 0 : bi == 1 ? 4 : bi == 2 ? 7 : 9);
+    const int I = bi >> 1, J = bj >> 1, qi = bi & 1, qj = bj & 1;
+    float* T = O + (I == 0 ? J : 2) * 64 * OP;  // tile_index(I, J, 2)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float v = g[q][r] * inv2;
+      T[(qi * 32 + row) * OP + qj * 32 + l32] = v;
+      if (I == J && qi != qj) T[(qj * 32 + l32) * OP + qi * 32 + row] = v;  // mirror
+    }
+  }
+  lds_sync();
+  const auto rg = make_srd(p.gram_part + (size_t)blockIdx.z * 3 * ntl * 4096,
+                           (uint32_t)(3 * ntl) * 16384u);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {  // 3 tiles x 64 rows x 16 float4 over 512 threads
+    const int idx = threadIdx.x + 512 * k;
+    const int u = idx >> 10, row = (idx >> 4) & 63, c4 = idx & 15;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(O + (u * 64 + row) * OP + 4 * c4);
+    const uint32_t off = (uint32_t)(((u * ntl + tix) * 64 + row) * 64 + 4 * c4) * 4u;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rg, off, 0, 0);
   }
 }
 
@@ -281,7 +504,7 @@ __device__ __forceinline__ void conv_gram_tile(const f32x16 (&acc)[2][NI],
 // through a descriptor at the store offsets
 // POOLSUM: pool_out = 2x2 sum of the output and no y stores (stx_conv_params.pool_sum)
 template <int TW, int NI, bool ROWPAIR, bool RELU, bool AUX = false,
-          bool POOLSUM = false, bool PAR = false>
+          bool POOLSUM = false, bool PAR = false, int WM = 1>
 __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
                                                          const stx_conv_params& p,
                                                          const EpiTile& t, float scale,
@@ -404,29 +627,35 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
         buf_st(rp, po + (uint32_t)row * ppb, __uint_as_float(m));
       }
   }
-  if constexpr (NI == 2 && TW == 64 && !RELU) if (p.gram_part) {
+  if constexpr (NI == 2 && TW == 64 && !RELU && WM == 1) if (p.gram_part) {
     // the max over valid pixels of all 64 rows (cout == 64: rows_full)
     conv_gram_tile<NI>(acc, p, t, lane_ok, vmax_u, smem);
+  }
+  if constexpr (NI == 2 && TW == 64 && !RELU && !PAR && WM == 2) if (p.gram_part) {
+    // (cout == 128: both halves rows_full)
+    conv_gram_tile128<TW, ROWPAIR>(acc, p, t, lane_ok, vo, vmax_u, smem);
   }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
 
-template <int TW, int NI, bool ROWPAIR, bool PAR = false>
+template <int TW, int NI, bool ROWPAIR, bool PAR = false, int WM = 1>
 __device__ __forceinline__ bool conv_epilogue_plain(f32x16 (&acc)[2][NI], const stx_conv_params& p,
                                                     const EpiTile& t, float scale, char* smem) {
   if (p.mask || p.accumulate || p.acc_scale || p.up_dp || p.p2_z) return false;
   if (p.pool_sum) {  // validated by stx_conv2d: plain epilogue, row-pair tiles
     if constexpr (ROWPAIR)
-      conv_epilogue_plain_body<TW, NI, ROWPAIR, false, false, true>(acc, p, t, scale, smem);
+      conv_epilogue_plain_body<TW, NI, ROWPAIR, false, false, true, false, WM>(acc, p, t, scale,
+                                                                               smem);
     return true;
   }
   if (p.aux) {
     if (p.relu_out || p.pool_out || p.gram_part) return false;
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, true, false, PAR>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, true, false, PAR, WM>(acc, p, t, scale, smem);
   } else if (p.relu_out) {
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, true, false, false, PAR>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, true, false, false, PAR, WM>(acc, p, t, scale, smem);
   } else {
-    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, false, false, PAR>(acc, p, t, scale, smem);
+    conv_epilogue_plain_body<TW, NI, ROWPAIR, false, false, false, PAR, WM>(acc, p, t, scale,
+                                                                            smem);
   }
   return true;
 }

@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
         for (int r = 0; r < 16; ++r)
           gram_put(gH, GPL::HP, 32 * mt + 8 * (r >> 2) + 4 * h + (r & 3), wave * 32 + l32,
                    acc[mt][r] * gs);
-      __syncthreads();
+      lds_sync();  // (the y stores stay in flight)
       if (wave < 3) {
         f32x16 gc;
 #pragma unroll
@@ -344,9 +344,9 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16_kernel(stx_conv_params p,
   if constexpr (GRAM) if (gram) {
     if (p.gram_cnt)
       gram_store_grouped(p, blockIdx.z, blockIdx.x, gridDim.x, g, wave, h, l32, gred);
-    else if (wave < 3)
-      gram_store(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, g, wave,
-                 h, l32);
+    else
+      gram_store_lds<256>(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, g,
+                          wave, h, l32, reinterpret_cast<float*>(gsm));
   }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16t_kernel(stx_conv_params p
 #pragma unroll
     for (int b3 = 0; b3 < 3; ++b3)
       *reinterpret_cast<f32x16*>(&gsum[((wave * 3 + b3) * 64 + lane) * 16]) = g[b3];
-    __syncthreads();
+    lds_sync();  // (the y stores stay in flight)
     f32x16 s;
 #pragma unroll
     for (int q = 0; q < 16; ++q) s[q] = 0.f;
@@ -584,9 +584,9 @@ __global__ void __launch_bounds__(256, 2) conv_fewin16t_kernel(stx_conv_params p
     }
     if (p.gram_cnt)  // (gsum's first word becomes the reducer flag after the helper's barrier)
       gram_store_grouped(p, blockIdx.z, blockIdx.x, gridDim.x, s, wave, h, l32, gsum);
-    else if (wave < 3)
-      gram_store(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, s, wave, h,
-                 l32);
+    else
+      gram_store_lds<256>(p.gram_part + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4096, s,
+                          wave, h, l32, gsum);
   }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }

@@ -1088,14 +1088,25 @@ extern "C" int stx_style_content_loss_deferred(const float* z, const float* targ
                             diag_alpha, z_amax, content, mse_out, ws, ws_bytes, stream, job);
 }
 
+// gparts: [b][ntu][nparts][64 x 64] (ntu = 1 for c <= 64, 3 for c = 128: the fused conv
+// epilogue tiles, stx_conv_params.gram_part); mse_parts (c = 128, the content tap): the
+// epilogue's 2 sums per block, b * nparts pairs, finalized into mse_out like
+// gram_tri_f16_kernel<128, true>'s
 static int from_parts_impl(const float* gparts, int nparts, const float* target, float* g_out,
                            float* coef, float* loss, int b, int c, int hw, int target_batched,
                            float weight, float diag_alpha, void* ws, size_t ws_bytes,
-                           void* stream, stx_gram_fin_job* defer) {
-  if (!gparts || !target || nparts <= 0 || b <= 0 || c <= 0 || c > GT || hw <= 0) {
-    set_error("stx_style_loss_from_parts: invalid arguments (c <= 64)");
+                           void* stream, stx_gram_fin_job* defer,
+                           const float* mse_parts = nullptr, float* mse_out = nullptr) {
+  if (!gparts || !target || nparts <= 0 || b <= 0 || c <= 0 || (c > GT && c != 2 * GT) ||
+      hw <= 0) {
+    set_error("stx_style_loss_from_parts: invalid arguments (c <= 64 or c == 128)");
     return STX_E_INVALID;
   }
+  if ((mse_parts != nullptr) != (mse_out != nullptr)) {
+    set_error("stx_style_content_loss_from_parts: mse_parts and mse_out go together");
+    return STX_E_INVALID;
+  }
+  const int nt = cdiv(c, GT), ntu = nt * (nt + 1) / 2;
   const size_t need = gram_ws_bytes(b, c, hw);
   if (!ws || ws_bytes < need) {
     set_error("stx_style_loss_from_parts: workspace %zu < %zu", ws_bytes, need);
@@ -1111,19 +1122,50 @@ static int from_parts_impl(const float* gparts, int nparts, const float* target,
                        dim3(256), 0, st, coef, cnt);
   }
   float* lparts = (float*)((char*)ws + gram_parts_offset(b, c, hw, nullptr));
+  const int mse_nparts = mse_parts ? b * nparts : 0;
+  const double mse_n = (double)b * c * hw;
   if (defer) {
     fill_job(defer, gparts, c, nparts, (float)(1.0 / n), g_out, target,
-             target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts, nullptr,
-             0, 1.0, nullptr, b);
+             target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts,
+             mse_parts, mse_nparts, mse_n, mse_out, b);
     return check_launch("stx_style_loss_from_parts_deferred");
   }
-  hipLaunchKernelGGL(gram_finalize_kernel, dim3(fin_blocks_per_tile(nparts), b), dim3(FNT), 0, st, gparts, c, nparts,
-                     (float)(1.0 / n), g_out, target,
-                     target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts);
+  hipLaunchKernelGGL(gram_finalize_kernel, dim3(ntu * fin_blocks_per_tile(nparts), b), dim3(FNT),
+                     0, st, gparts, c, nparts, (float)(1.0 / n), g_out, target,
+                     target_batched ? (long long)c * c : 0ll, coef, cpad, cA, diag_alpha, lparts,
+                     mse_parts, mse_nparts, mse_n, mse_out);
   if (loss)
-    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, lparts, b * FSUB,
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, st, lparts, b * ntu * FSUB,
                        (float)(1.0 / ((double)b * c * c)), loss);
   return check_launch("stx_style_loss_from_parts");
+}
+
+extern "C" int stx_style_content_loss_from_parts(const float* gparts, int nparts,
+                                                 const float* target, float* coef, float* loss,
+                                                 int b, int c, int hw, int target_batched,
+                                                 float weight, float diag_alpha,
+                                                 const float* mse_parts, float* mse_out, void* ws,
+                                                 size_t ws_bytes, void* stream) {
+  if (!mse_parts || !mse_out) {
+    set_error("stx_style_content_loss_from_parts: mse_parts and mse_out are required");
+    return STX_E_INVALID;
+  }
+  return from_parts_impl(gparts, nparts, target, nullptr, coef, loss, b, c, hw, target_batched,
+                         weight, diag_alpha, ws, ws_bytes, stream, nullptr, mse_parts, mse_out);
+}
+
+extern "C" int stx_style_content_loss_from_parts_deferred(
+    const float* gparts, int nparts, const float* target, float* coef, int b, int c, int hw,
+    int target_batched, float weight, float diag_alpha, const float* mse_parts, float* mse_out,
+    void* ws, size_t ws_bytes, stx_gram_fin_job* job, void* stream) {
+  if (!job || !mse_parts || !mse_out) {
+    set_error("stx_style_content_loss_from_parts_deferred: job, mse_parts and mse_out are "
+              "required");
+    return STX_E_INVALID;
+  }
+  return from_parts_impl(gparts, nparts, target, nullptr, coef, nullptr, b, c, hw,
+                         target_batched, weight, diag_alpha, ws, ws_bytes, stream, job, mse_parts,
+                         mse_out);
 }
 
 extern "C" int stx_style_loss_from_parts(const float* gparts, int nparts, const float* target,

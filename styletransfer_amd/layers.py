@@ -30,6 +30,9 @@ class Conv2d(nn.Conv2d):
             raise NotImplementedError(f"kernel_size {self.kernel_size}")
         self._wt_cache = None
         self._train_slabs = None  # set by ops.TrainedSlabs.prep() (fast_st trainers)
+        # reads a nearest x2 upsampled input (ImageTransformNet's UpsampleConvLayer): the
+        # split path also gets the parity-class slab (ops.conv_weight_prep16_up)
+        self._up_input = False
 
     def prepped(self):
         """Cached GEMM slabs (fp32, and the fp16 hi/lo split slab where the shape
@@ -43,22 +46,24 @@ class Conv2d(nn.Conv2d):
             w16 = ops.conv_weight_prep16(wd) if (A._split_on() and self.padding[0] == 1 and
                                                  ops.split_eligible(cin, cout, ks, self.stride[0])) \
                 else None
-            self._wt_cache = (key, ops.conv_weight_prep(wd), w16)
-        return self._wt_cache[1], self._wt_cache[2]
+            up = ops.conv_weight_prep16_up(wd) if (w16 is not None and self._up_input and
+                                                   A._upar_on()) else None
+            self._wt_cache = (key, ops.conv_weight_prep(wd), w16, up)
+        return self._wt_cache[1], self._wt_cache[2], self._wt_cache[3]
 
     def forward(self, x, in_mode=N.STX_IN_RAW, bias_grad=True, link=None):
         """bias_grad=False: the bias enters detached -- for a conv feeding an
         InstanceNorm2d that is handed the bias (`conv_bias=`) and produces its gradient."""
-        wt = wt16 = wtT = wtT16 = None
+        wt = wt16 = wtT = wtT16 = up = None
         ts = self._train_slabs
         w = self.weight
         if ts is not None and ts[0] == (w.data_ptr(), w._version, w.device):
-            _, wt, wt16, wtT, wtT16 = ts  # the trainer's batched prep of this version
+            _, wt, wt16, wtT, wtT16, up = ts  # the trainer's batched prep of this version
         elif not w.requires_grad or not torch.is_grad_enabled():
-            wt, wt16 = self.prepped()  # frozen or inference: slabs cached per weight version
+            wt, wt16, up = self.prepped()  # frozen or inference: slabs cached per weight version
         b = self.bias if bias_grad or self.bias is None else self.bias.detach()
         return A.conv2d(x, w, b, self.stride[0], self.padding[0], in_mode, wt, wt16, wtT, wtT16,
-                        link)
+                        link, wt16_up=up)
 
 
 class ReLU(nn.ReLU):

@@ -400,8 +400,10 @@ class ResidualBlock(nn.Module):
 
 
 def _itn_layers(in_channels=3):
-    def conv(i, o, k, s):
-        return Conv2d(i, o, kernel_size=k, stride=s, padding=k // 2, padding_mode="reflection")
+    def conv(i, o, k, s, up=False):
+        c = Conv2d(i, o, kernel_size=k, stride=s, padding=k // 2, padding_mode="reflection")
+        c._up_input = up  # behind an Upsample (forward fuses it into the conv)
+        return c
 
     return [
         conv(in_channels, 32, 9, 1), InstanceNorm2d(32, affine=True), ReLU(),
@@ -410,9 +412,9 @@ def _itn_layers(in_channels=3):
         ResidualBlock(128, 128, 3), ResidualBlock(128, 128, 3), ResidualBlock(128, 128, 3),
         ResidualBlock(128, 128, 3), ResidualBlock(128, 128, 3),
         Upsample(mode="nearest", scale_factor=2),
-        conv(128, 64, 3, 1), InstanceNorm2d(64, affine=True), ReLU(),
+        conv(128, 64, 3, 1, up=True), InstanceNorm2d(64, affine=True), ReLU(),
         Upsample(mode="nearest", scale_factor=2),
-        conv(64, 32, 3, 1), InstanceNorm2d(32, affine=True), ReLU(),
+        conv(64, 32, 3, 1, up=True), InstanceNorm2d(32, affine=True), ReLU(),
         conv(32, 3, 9, 1),
     ]
 

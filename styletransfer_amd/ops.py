@@ -260,6 +260,20 @@ def conv_weight_prep16(w: torch.Tensor, transpose: bool = False):
     return wt16, w_amax
 
 
+def conv_weight_prep16_up(w: torch.Tensor):
+    """[cout][cin][3][3] -> (parity-class split slab, device max|w|) of a conv over a
+    nearest x2 upsampled input (stx_conv_weight_prep16_up; conv2d(wt16_up=...))."""
+    _req(w, "weight")
+    cout, cin, ks, _ = w.shape
+    assert ks == 3, ks
+    L = lib()
+    slab = torch.empty(L.stx_conv_weight16up_bytes(cin, cout), device=w.device, dtype=torch.uint8)
+    w_amax = torch.empty(N.STX_AMAX_SLOTS, device=w.device, dtype=torch.float32)
+    check(L.stx_conv_weight_prep16_up(w.data_ptr(), slab.data_ptr(), w_amax.data_ptr(), cout,
+                                      cin, _stream()), "conv_weight_prep16_up")
+    return slab, w_amax
+
+
 def conv_weight_compose16(coef, coef_amax, w: torch.Tensor, w_amax, out_amax, scale=None,
                           out=None):
     """The data-gradient split slab of w' = scale * A w (A = coef [cout][pitch], one image's
@@ -307,9 +321,10 @@ class TrainedSlabs:
     data-gradient GEMM; forward and data-gradient split slabs share one max|w| group.
 
     `prep()` enqueues the batch and hands each layer `_train_slabs = (key, wt, wt16,
-    wtT, wtT16)` keyed on the weight's (pointer, version): layers.Conv2d uses the
-    slabs only while the key matches, so a weight changed behind the trainer's back
-    falls back to per-call preps."""
+    wtT, wtT16, wt16_up)` keyed on the weight's (pointer, version): layers.Conv2d uses
+    the slabs only while the key matches, so a weight changed behind the trainer's back
+    falls back to per-call preps.  wt16_up: the parity-class slab of a conv that reads a
+    nearest x2 upsampled input (layers.Conv2d._up_input), sharing the max|w| group."""
 
     def __init__(self, convs):
         self.convs = list(convs)
@@ -353,7 +368,14 @@ class TrainedSlabs:
                     jobs.append(N.WprepJob(w.data_ptr(), slab.data_ptr(), None,
                                            N.STX_WPREP_F32, cout, cin, ks, t, 0))
                     out.append((slab, None))
-            self.slabs.append((w.data_ptr(), out[0][0], out[0][1], out[1][0], out[1][1]))
+            up = None
+            if f16 and stride == 1 and ks == 3 and getattr(conv, "_up_input", False) and \
+                    os.environ.get("STX_UPAR", "1") != "0":
+                up = torch.empty(L.stx_conv_weight16up_bytes(cin, cout), device=dev,
+                                 dtype=torch.uint8)
+                jobs.append(N.WprepJob(w.data_ptr(), up.data_ptr(), am.data_ptr(),
+                                       N.STX_WPREP_F16UP, cout, cin, ks, 0, 0))
+            self.slabs.append((w.data_ptr(), out[0][0], out[0][1], out[1][0], out[1][1], up))
         if len(jobs) > N.STX_WPREP_MAX:
             raise N.NativeError(f"{len(jobs)} weight slabs > STX_WPREP_MAX")
         self._jobs = (N.WprepJob * len(jobs))(*jobs)
@@ -371,9 +393,10 @@ class TrainedSlabs:
         if self._njobs:
             check(lib().stx_conv_weight_prep_batch(self._jobs, self._njobs, _stream()),
                   "conv_weight_prep_batch")
-        for c, (_, wt, wt16, wtT, wtT16) in zip(self.convs, self.slabs):
+        for c, (_, wt, wt16, wtT, wtT16, up) in zip(self.convs, self.slabs):
             w = c.weight
-            c._train_slabs = ((w.data_ptr(), w._version, w.device), wt, wt16, wtT, wtT16)
+            c._train_slabs = ((w.data_ptr(), w._version, w.device), wt, wt16, wtT, wtT16,
+                              None if up is None else (up, wt16[1]))
 
 
 _S2_FWD = os.environ.get("STX_S2_FWD", "1") != "0"
@@ -425,7 +448,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
            relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
            p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
            pool_out=None, p2_amax=None, split_1x1=False, gram_part=None, pool_sum=False,
-           gram_cnt=None, p2_wt_amax=None):
+           gram_cnt=None, p2_wt_amax=None, mse_ref=None, mse_parts=None, wt16_up=None):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
     up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
@@ -438,7 +461,11 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
     SUM of the output instead and the full-resolution output is not written (returned:
     pool_out) -- the nearest-x2 upsampling backward fused into a data gradient.
     p2_wt_amax: amax group >= max|p2_coef| over the batch (a FinalizeBatch job's
-    coef_amax): the split path's Gram-backward phase then runs on the fp16 split MFMA."""
+    coef_amax): the split path's Gram-backward phase then runs on the fp16 split MFMA.
+    mse_ref/mse_parts (with gram_part, cout 128): the content target and the per-tile
+    content / feature MSE sums of the output (stx_conv_params.mse_ref).
+    wt16_up=(slab, w_amax) from conv_weight_prep16_up: an upsampled-input conv with the
+    plain epilogue runs as four output-parity 2x2 convs (stx_conv_params.wt16_up)."""
     _req(x, "x")
     n, c, h, w = x.shape
     assert c == cin, (c, cin)
@@ -472,6 +499,11 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         if in_amax is None:
             in_amax = amax(x)
         p.wt16, p.w_amax, p.in_amax = wt16[0].data_ptr(), wt16[1].data_ptr(), in_amax.data_ptr()
+        if wt16_up is not None and in_mode == N.STX_IN_UPSAMPLE2 and ks == 3 and stride == 1 \
+                and pad == 1 and wo > 32 and not any(
+                    v is not None for v in (mask, aux, acc_scale, p2_z, up_dp, pool_out,
+                                            gram_part)) and not accumulate:
+            p.wt16_up, p.w_amax = wt16_up[0].data_ptr(), wt16_up[1].data_ptr()
         if p2_z is not None:
             p.p2_amax = (p2_amax if p2_amax is not None else amax(p2_z)).data_ptr()
             if p2_wt_amax is not None:
@@ -492,18 +524,33 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         assert pool_out.shape == (n, cout, ho // 2, wo // 2), pool_out.shape
         p.pool_out = pool_out.data_ptr()
         p.pool_sum = int(bool(pool_sum))
+    assert mse_ref is None or gram_part is not None, "mse_ref rides on the fused Gram"
     if gram_part is not None:
         _req(gram_part, "gram_part")
         nt = lib().stx_conv_gram_tiles(C.byref(p))
         ng = lib().stx_conv_gram_groups(C.byref(p)) if gram_cnt is not None else 0
-        assert nt > 0 and gram_part.numel() >= n * (nt + ng) * 4096, (nt, ng, gram_part.numel())
+        ntu = gram_tile_units(cout)
+        assert nt > 0 and gram_part.numel() >= n * (ntu * nt + ng) * 4096, \
+            (nt, ng, gram_part.numel())
         p.gram_part = gram_part.data_ptr()
+        if mse_ref is not None:
+            _req(mse_ref, "mse_ref")
+            _req(mse_parts, "mse_parts")
+            assert mse_ref.shape == out.shape and mse_parts.numel() >= 2 * n * nt, \
+                (mse_ref.shape, mse_parts.numel(), n * nt)
+            p.mse_ref, p.mse_parts = mse_ref.data_ptr(), mse_parts.data_ptr()
         if gram_cnt is not None:
             assert gram_cnt.is_cuda and gram_cnt.dtype == torch.int32 and \
                 gram_cnt.numel() >= n * ng, (gram_cnt.dtype, gram_cnt.numel(), n * ng)
             p.gram_cnt = gram_cnt.data_ptr()
     check(lib().stx_conv2d(C.byref(p), _stream()), "stx_conv2d")
     return out
+
+
+def gram_tile_units(c):
+    """64 x 64 tiles of the upper triangle of a c x c Gram (the partial slab's U)."""
+    nt = (c + 63) // 64
+    return nt * (nt + 1) // 2
 
 
 def conv_gram_tiles(cin, cout, ho, wo, n=1, in_mode=N.STX_IN_RAW):
@@ -721,12 +768,19 @@ def style_content_loss(z, target, content, mse_out, weight=1.0, diag_alpha=0.0, 
 
 
 def style_loss_from_parts(gparts, nparts, b, c, hw, target, weight=1.0, diag_alpha=0.0,
-                          coef=None, defer_ws=None, fin=None):
+                          coef=None, defer_ws=None, fin=None, mse_parts=None, mse_out=None):
     """style_loss from the fused Gram partials a conv wrote (conv2d(gram_part=...)):
-    gparts [b][nparts][64][64].  Returns (deferred LossPart, coef) as style_loss with
-    defer_ws."""
+    gparts [b][U][nparts][64][64] (U = 3 for c = 128, else 1).  mse_parts (the content
+    tap: conv2d(mse_ref=content, mse_parts=...)) with mse_out [3]: the content, feature
+    and feature-mse values as style_content_loss writes them, from the same launch.
+    Returns (deferred LossPart, coef) as style_loss with defer_ws."""
     _req(gparts, "gram partials")
     _req(target, "target")
+    if (mse_parts is None) != (mse_out is None):
+        raise ValueError("mse_parts and mse_out go together")
+    if mse_parts is not None:
+        _req(mse_parts, "mse_parts")
+        assert mse_parts.numel() >= 2 * b * nparts and mse_out.numel() >= 3
     tb = target.numel() == b * c * c and b > 1
     if not tb and target.numel() != c * c:
         raise ValueError(f"style target {tuple(target.shape)} cannot expand to ({b},{c},{c})")
@@ -737,7 +791,19 @@ def style_loss_from_parts(gparts, nparts, b, c, hw, target, weight=1.0, diag_alp
     need = L.stx_gram_ws(b, c, hw)
     assert defer_ws is not None and defer_ws.numel() >= need, need
     wp, wn = defer_ws.data_ptr(), defer_ws.numel()
-    if fin is not None:
+    if mse_parts is not None:
+        if fin is not None:
+            check(L.stx_style_content_loss_from_parts_deferred(
+                gparts.data_ptr(), int(nparts), target.data_ptr(), coef.data_ptr(), b, c, hw,
+                int(tb), float(weight), float(diag_alpha), mse_parts.data_ptr(),
+                mse_out.data_ptr(), wp, wn, C.byref(fin.new()), _stream()),
+                "stx_style_content_loss_from_parts_deferred")
+        else:
+            check(L.stx_style_content_loss_from_parts(
+                gparts.data_ptr(), int(nparts), target.data_ptr(), coef.data_ptr(), None, b, c,
+                hw, int(tb), float(weight), float(diag_alpha), mse_parts.data_ptr(),
+                mse_out.data_ptr(), wp, wn, _stream()), "stx_style_content_loss_from_parts")
+    elif fin is not None:
         check(L.stx_style_loss_from_parts_deferred(gparts.data_ptr(), int(nparts),
                                                    target.data_ptr(), coef.data_ptr(), b, c, hw,
                                                    int(tb), float(weight), float(diag_alpha), wp,

@@ -117,7 +117,15 @@ class VGGFeatures:
         # conv1_1 (3 input channels) runs on convfew.hip's split kernel without a slab
         if (cin >= 16 and self.wt16[l] is None) or os.environ.get("STX_GRAM_FUSE", "1") == "0":
             return 0
-        return ops.conv_gram_tiles(cin, cout, ho, wo, n=n, in_mode=IN_MODES[l])
+        return ops.conv_gram_tiles(cin, cout, ho, wo, n=n, in_mode=self._run_mode(l, wo))
+
+    def _run_mode(self, l, wo):
+        """The loader mode conv l runs with (forward): raw where conv l-1 writes the
+        pooled input for it."""
+        mode = IN_MODES[l]
+        if mode == N.STX_IN_RELU_POOL2 and l > 0 and self.fuses_pool(l - 1, 2 * wo):
+            return N.STX_IN_RAW
+        return mode
 
     def gram_groups(self, l, ho, wo, n=1):
         """In-kernel group sums per image of conv l's fused Gram (0: not grouped).  Off
@@ -127,9 +135,10 @@ class VGGFeatures:
         if os.environ.get("STX_GRAM_GROUPED", "0") != "1" or not self.gram_tiles(l, ho, wo, n):
             return 0
         cout, cin = VGG_CONV_SHAPES[l]
-        return ops.conv_gram_groups(cin, cout, ho, wo, n=n, in_mode=IN_MODES[l])
+        return ops.conv_gram_groups(cin, cout, ho, wo, n=n, in_mode=self._run_mode(l, wo))
 
-    def forward(self, x, upto=5, outs=None, amax=None, pools=None, on_layer=None, grams=None):
+    def forward(self, x, upto=5, outs=None, amax=None, pools=None, on_layer=None, grams=None,
+                content=None):
         """[Z1..Z_upto] (pre-ReLU conv outputs).  amax: device [>=5] slots, zeroed by
         the caller; slot l+1 receives max|Z_l| (the next split conv's input scale);
         each slot is an amax group of N.STX_AMAX_SLOTS floats (slot(amax, k)).
@@ -137,7 +146,8 @@ class VGGFeatures:
         pools[l] if given) and conv l+1 reads P directly.  grams[l] (if given and not
         None): conv l writes its fused Gram partials there (gram_tiles); a (slab,
         counters) pair instead: the in-kernel group sums (gram_groups) after the per-tile
-        scratch."""
+        scratch.  content=(c4, parts): the content tap's conv (fused Gram, 128 channels)
+        also writes its content / feature MSE sums against c4 into parts."""
         zs, cur, pin = [], x, None
         for l in range(upto):
             cout, cin = VGG_CONV_SHAPES[l]
@@ -161,6 +171,8 @@ class VGGFeatures:
                     kw["gram_part"], kw["gram_cnt"] = grams[l]
                 else:
                     kw["gram_part"] = grams[l]
+                if content is not None and l == CONTENT_CONV:
+                    kw["mse_ref"], kw["mse_parts"] = content
             cur = ops.conv2d(src, self.wt[l], cin, cout, 3, in_mode=mode, bias=self.b[l],
                              out=None if outs is None else outs[l], wt16=self.wt16[l], **kw)
             zs.append(cur)
@@ -192,6 +204,7 @@ class LossState:
     parts: list = field(default_factory=lambda: [None] * 5)  # deferred loss partials
     grams: list = field(default_factory=lambda: [None] * 5)  # fused Gram partial slabs
     fin_jobs: list = None                       # the last batched finalize's jobs (bench)
+    mse_parts: torch.Tensor = None              # content tap's fused MSE sums (2 per tile)
 
 
 def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
@@ -263,10 +276,18 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                 st.grams[l] = (torch.empty(B * (nt + ng) * 4096, device=dev, dtype=torch.float32),
                                torch.zeros(B * ng, device=dev, dtype=torch.int32))
         elif st.grams[l] is None or isinstance(st.grams[l], tuple) or \
-                st.grams[l].numel() != B * nt * 4096:
-            st.grams[l] = torch.empty(B * nt * 4096, device=dev, dtype=torch.float32)
+                st.grams[l].numel() != B * ops.gram_tile_units(VGG_CONV_SHAPES[l][0]) * nt * 4096:
+            st.grams[l] = torch.empty(B * ops.gram_tile_units(VGG_CONV_SHAPES[l][0]) * nt * 4096,
+                                      device=dev, dtype=torch.float32)
 
     fuse_content = os.environ.get("STX_CONTENT_FUSE", "1") != "0"
+    # the content tap's Gram in its conv epilogue: the content / feature MSE sums too
+    content = None
+    if st.grams[CONTENT_CONV] is not None and fuse_content:
+        nt4 = feat.gram_tiles(CONTENT_CONV, hs[CONTENT_CONV], hs[CONTENT_CONV] * W // H, n=B)
+        if st.mse_parts is None or st.mse_parts.numel() != 2 * B * nt4:
+            st.mse_parts = torch.empty(2 * B * nt4, device=dev, dtype=torch.float32)
+        content = (c4, st.mse_parts)
     # the five taps' Gram finalizes in one launch after the forward (STX_FIN_BATCH=0: one
     # finalize launch per tap, right after its partials)
     # (with the loss stream the jobs are recorded on the side stream's calls and the one
@@ -279,21 +300,25 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                 z, targets[i], c4, st.losses[5:8], weight=sw, diag_alpha=alpha,
                 coef=st.coef[i], z_amax=slot(st.amax, l + 1), defer_ws=st.lws[i], fin=fin)
             return
+        fused_mse = False
         if st.grams[l] is not None:
             gp = st.grams[l]
             if isinstance(gp, tuple):  # the group sums after the B * nt tile slots
                 ng = gp[1].numel() // b_
                 gp = gp[0][gp[0].numel() - b_ * ng * 4096:]
+            fused_mse = l == CONTENT_CONV and content is not None
             st.parts[i], st.coef[i] = ops.style_loss_from_parts(
-                gp, gp.numel() // (b_ * 4096), b_, c_, z[0, 0].numel(),
+                gp, gp.numel() // (b_ * ops.gram_tile_units(c_) * 4096), b_, c_, z[0, 0].numel(),
                 targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
-                coef=st.coef[i], defer_ws=st.lws[i], fin=fin)
+                coef=st.coef[i], defer_ws=st.lws[i], fin=fin,
+                mse_parts=st.mse_parts if fused_mse else None,
+                mse_out=st.losses[5:8] if fused_mse else None)
         else:
             st.parts[i], st.coef[i] = ops.style_loss(
                 z, targets[i], weight=sw, diag_alpha=alpha if l == CONTENT_CONV else 0.0,
                 coef=st.coef[i], z_amax=slot(st.amax, l + 1) if split else None,
                 defer_ws=st.lws[i], fin=fin)
-        if l == CONTENT_CONV:  # content, feature, feature-mse: one pass
+        if l == CONTENT_CONV and not fused_mse:  # content, feature, feature-mse: one pass
             ops.mse(z, c4, mode=2, out=st.losses[5:8])
 
     st.coef_amax = [None] * 5
@@ -327,7 +352,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                 fin.jobs[-1].coef_amax = st.coef_amax[i].data_ptr()
 
     st.z = feat.forward(x, 5, st.z if st.z else None, amax=st.amax, pools=st.pools,
-                        on_layer=on_layer, grams=st.grams)
+                        on_layer=on_layer, grams=st.grams, content=content)
     if overlap:
         main.wait_stream(side)
         if not capturing:

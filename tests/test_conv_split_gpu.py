@@ -105,6 +105,40 @@ def test_split_conv_stride2(dev, case):
     assert float(amax.max()) == float(y.abs().max())
 
 
+@pytest.mark.parametrize("case", [(8, 128, 64, 64, 64, False),    # ITN up-conv 1 (B = 8)
+                                  (8, 64, 32, 128, 128, False),   # ITN up-conv 2
+                                  (2, 32, 48, 20, 45, True),      # ragged tiles, relu_out
+                                  (1, 16, 20, 17, 33, False),     # wo = 66, odd bands
+                                  (1, 128, 64, 270, 480, False)])  # video 1080p / 4
+def test_split_conv_upsample_parity(dev, case):
+    """The upsampled-input conv as four output-parity 2x2 convs over the input
+    (stx_conv_params.wt16_up, summed weights W'[a][b][ry][rx]) vs fp64 of
+    conv(nearest_x2(x)) (UpsampleConvLayer, stransfer/network.py:578-600), and the
+    upsampled-halo kernel on the same inputs; out_amax is the exact max|y|."""
+    n, cin, cout, h, w, relu = case
+    x = rnd(n, cin, h, w, dev=dev, seed=17, scale=2, shift=-1)
+    wgt = rnd(cout, cin, 3, 3, dev=dev, seed=18, scale=0.2, shift=-0.1)
+    b = rnd(cout, dev=dev, seed=19)
+    wt, w16 = ops.conv_weight_prep(wgt), ops.conv_weight_prep16(wgt)
+    up = ops.conv_weight_prep16_up(wgt)
+    amax = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    mode = N.STX_IN_UPSAMPLE2
+    y = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=b, wt16=w16, wt16_up=up,
+                   relu_out=relu, out_amax=amax)
+    y2 = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=b, wt16=w16, relu_out=relu)
+    torch.cuda.synchronize()
+    assert float(amax.max()) == float(y.abs().max())
+    if n * h * w * cin > 3_000_000:  # (no fp64 conv at the full sizes: the other kernel)
+        assert rel(y, y2) < 1e-5, rel(y, y2)
+        return
+    ref = F.conv2d(vinput(x.double().cpu(), mode), wgt.double().cpu(), b.double().cpu(),
+                   padding=1)
+    if relu:
+        ref = ref.relu()
+    assert y.shape == ref.shape
+    assert rel(y, ref) < TOL64, (rel(y, ref), rel(y2, ref))
+
+
 @pytest.mark.parametrize("scale", [1e-9, 1.0, 3e4])
 def test_split_conv_scales(dev, scale):
     """Per-tensor power-of-two scaling: tiny and large inputs keep fp32 accuracy."""
@@ -373,6 +407,77 @@ def test_fused_gram_partials(dev, case):
     l32, a32 = ops.style_loss(y, t, weight=3.0)
     assert rel(lf[0], l32) < 1e-5
     assert rel(a_f, a32) < 1e-5
+
+
+@pytest.mark.parametrize("case", [(1, 64, 256, 256, N.STX_IN_RAW, False, False),   # Gatys conv2_1
+                                  (1, 128, 256, 256, N.STX_IN_RELU, True, True),   # Gatys conv2_2
+                                  (2, 128, 128, 128, N.STX_IN_RELU, True, True),
+                                  (4, 64, 128, 128, N.STX_IN_RAW, False, False),   # 256 blocks
+                                  (2, 128, 38, 72, N.STX_IN_RELU, False, True),    # ragged
+                                  (3, 64, 70, 100, N.STX_IN_RAW, True, False)])
+def test_fused_gram128(dev, case):
+    """The 128-channel taps' Gram out of the conv epilogue (8-wave blocks, three 64 x 64
+    tiles per block, conv_gram_tile128): the partials add up to the Gram of the stored
+    output (vs fp64), y and the pooled output equal the unfused launch bit for bit, and
+    style_loss_from_parts equals style_loss on y.  With mse_ref (the content tap): the
+    epilogue's MSE sums give the same content / feature / feature-mse values as stx_mse on
+    y (stransfer/network.py:134-201)."""
+    n, cin, h, w, mode, pool, with_mse = case
+    cout = 128
+    x = rnd(n, cin, h, w, dev=dev, seed=291, scale=2, shift=-1)
+    wgt = rnd(cout, cin, 3, 3, dev=dev, seed=292, scale=0.1, shift=-0.05)
+    bias = rnd(cout, dev=dev, seed=293, scale=0.2, shift=-0.1)
+    wt, w16 = ops.conv_weight_prep(wgt), ops.conv_weight_prep16(wgt)
+    nt = ops.conv_gram_tiles(cin, cout, h, w, n=n, in_mode=mode)
+    assert nt == -(-w // 64) * -(-h // 4), nt
+    assert ops.conv_gram_groups(cin, cout, h, w, n=n, in_mode=mode) == 0  # 64-channel only
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    # more than one round of 8-wave blocks: the standalone Gram (fast_st's B = 8)
+    assert ops.conv_gram_tiles(cin, cout, h, w, n=cus // nt + 1, in_mode=mode) == 0
+    assert ops.conv_gram_tiles(cin, cout, h, w, n=n, in_mode=N.STX_IN_UPSAMPLE2) == 0
+    parts = torch.full((n * 3 * nt * 4096,), float("nan"), device=dev)
+    kw = {}
+    if pool:
+        kw["pool_out"] = torch.empty(n, cout, h // 2, w // 2, device=dev)
+    c = None
+    if with_mse:
+        c = rnd(n, cout, h, w, dev=dev, seed=295, scale=1.0, shift=-0.4)
+        kw["mse_ref"] = c
+        kw["mse_parts"] = torch.full((2 * n * nt,), float("nan"), device=dev)
+    y = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=bias, wt16=w16, gram_part=parts, **kw)
+    kw2 = {}
+    if pool:
+        kw2["pool_out"] = torch.empty(n, cout, h // 2, w // 2, device=dev)
+    y2 = ops.conv2d(x, wt, cin, cout, 3, in_mode=mode, bias=bias, wt16=w16, **kw2)
+    assert torch.equal(y, y2)
+    if pool:
+        assert torch.equal(kw["pool_out"], kw2["pool_out"])
+    assert torch.isfinite(parts).all()
+    pt = parts.view(n, 3, nt, 64, 64).double().sum(2).cpu()
+    g = torch.empty(n, cout, cout, dtype=torch.float64)
+    g[:, :64, :64], g[:, :64, 64:], g[:, 64:, 64:] = pt[:, 0], pt[:, 1], pt[:, 2]
+    g[:, 64:, :64] = pt[:, 1].transpose(1, 2)
+    g /= cout * h * w
+    f = y.double().cpu().reshape(n, cout, h * w)
+    ref = torch.bmm(f, f.transpose(1, 2)) / (cout * h * w)
+    assert rel(g, ref) < TOL64, rel(g, ref)
+    t = rnd(cout, cout, dev=dev, seed=294, scale=0.02)
+    ws = torch.empty(N.lib().stx_gram_ws(n, cout, h * w), device=dev, dtype=torch.uint8)
+    mo = torch.full((3,), float("nan"), device=dev) if with_mse else None
+    lp, a_f = ops.style_loss_from_parts(parts, nt, n, cout, h * w, t, weight=3.0, defer_ws=ws,
+                                        mse_parts=kw.get("mse_parts"), mse_out=mo)
+    lf = torch.zeros(1, device=dev)
+    ops.loss_finalize([lp], lf)
+    l32, a32 = ops.style_loss(y, t, weight=3.0)
+    assert rel(lf[0], l32) < 1e-5
+    assert rel(a_f, a32) < 1e-5
+    if with_mse:
+        m32 = ops.mse(y, c, mode=2)
+        yd, cd = y.double(), c.double()
+        m64 = [float(((yd - cd) ** 2).mean()), float(((yd.relu() - cd.relu()) ** 2).mean())]
+        assert abs(float(mo[0]) - m64[0]) < 1e-5 * m64[0], (float(mo[0]), m64[0])
+        assert abs(float(mo[2]) - m64[1]) < 1e-5 * m64[1], (float(mo[2]), m64[1])
+        assert rel(mo, m32) < 1e-5, (mo, m32)
 
 
 @pytest.mark.parametrize("case", [(1, 64, 512, 512, N.STX_IN_RELU, True),   # Gatys conv1_2

@@ -33,7 +33,7 @@ def test_struct_mirrors_match_the_library():
     from styletransfer_amd import _native as N
     out = (C.c_longlong * 12)()
     assert N.lib().stx_abi_layout(C.cast(out, C.c_void_p), 12) == 12
-    mirrors = [(N.ConvParams, "p2_wt_amax"), (N.WprepJob, "pad_"), (N.LossParts, "k"),
+    mirrors = [(N.ConvParams, "wt16_up"), (N.WprepJob, "pad_"), (N.LossParts, "k"),
                (N.GramFinJob, "coef_amax"), (N.PGradJob, "pad_"), (N.ImageMeta, "tmp_offset")]
     for i, (S, last) in enumerate(mirrors):
         assert S._fields_[-1][0] == last, S

@@ -224,10 +224,11 @@ def test_gatys_lbfgs_512_history100_direction_vs_fp64(dev):
     eng = V.GatysLBFGS(V.VGGFeatures(V.load_vgg19_weights(), dev), s, c, init=noise).capture()
     opt = eng.opt
     steps = 0
-    while steps < 12:
+    while steps < 16:  # until the full ring has evicted (slot 100 in use)
         eng.step()
         steps += 1
-        if opt.state[eng.x]["n_iter"] > 115 and eng.history()[0] == 100:
+        if opt.state[eng.x]["n_iter"] > 115 and eng.history()[0] == 100 and \
+                sorted(_lb_hdr(opt)["order"]) != list(range(100)):
             break
     hdr0 = _lb_hdr(opt)
     assert hdr0["count"] == 100 and hdr0["n_iter"] > 101, hdr0
