@@ -429,6 +429,273 @@ wgrad16_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg1
   }
 }
 
+// ---- parity classes of an upsampled-input conv (UpsampleConvLayer, stransfer/network.py
+// :578-600).  Output pixel (2y + a, 2x + b) of the conv over the nearest x2 upsampled input
+// reads input rows y - 1 + a + ry and columns x - 1 + b + rx (ry, rx in {0, 1}), so
+//   dW'[a][b][ry][rx] = sum over the class-(a, b) outputs of dY * x[..][..]
+// takes 4 instead of 9 MACs per output, and dW[kh][kw] = sum of dW' over the (a, ry) with
+// kh in K(a, ry) and the (b, rx) with kw in K(b, rx) (K(0,0) = {0}, K(0,1) = {1,2},
+// K(1,0) = {0,1}, K(1,1) = {2}) -- wgrad16up_reduce_kernel.  A wave owns (64 couts |
+// CI2: 32 couts x 64 cins, 32 cins, ry, a) over a K split of the parity-a output rows; a
+// step is 32 output columns of one row: the lane's 16 dY pixels split into the b = 0 / 1
+// halves (evens / odds: two A fragments) and its 10 input pixels give the three shifted B
+// fragments, shift b + rx (the kw fragments of the plain kernel).  Partials
+// [split][a*8 + ry*4 + b*2 + rx][co][ci].
+constexpr int WG16_UPP = 17;  // private mode: the parity-class form of STX_IN_UPSAMPLE2
+
+template <int PF, bool CI2>
+__global__ void __launch_bounds__(256)
+wgrad16up_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ ws,
+                 const float* __restrict__ x_amax, const float* __restrict__ dy_amax, Wg16 g) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  int unit = xcd_block(blockIdx.x, gridDim.x) * 4 + wave;
+  const int cit = unit % g.ncit;
+  unit /= g.ncit;
+  const int cot = unit % g.ncot;
+  unit /= g.ncot;
+  const int q4 = unit % 4, ry = q4 >> 1, a = q4 & 1;
+  const int split = unit / 4;
+  if (split >= g.nsplit) return;  // (no barriers in this kernel)
+
+  const int ex = wg_amax_exp(read_amax(x_amax)), ed = wg_amax_exp(read_amax(dy_amax));
+  const float sv = __builtin_ldexpf(1.f, 15 - ex), sd = __builtin_ldexpf(1.f, 15 - ed);
+  const float descale = __builtin_ldexpf(1.f, ex + ed - 30);
+  const int co = cot * (CI2 ? 32 : 64) + l32, ci = cit * (CI2 ? 64 : 32) + l32;
+  const bool co_ok = co < g.cout, co2_ok = !CI2 && co + 32 < g.cout, ci_ok = ci < g.cin;
+  const bool ci2_ok = CI2 && ci + 32 < g.cin;
+  const int H = g.hv, W = g.wv, hin = g.h, win = g.w, wsteps = W / 32;
+
+  f32x16 acc[2][4];  // [cout tile | CI2: cin tile][b * 2 + rx]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][k][r] = 0.f;
+
+  const auto rdy = make_srd(dy, (uint32_t)((size_t)g.n * g.cout * H * W * 4u));
+  const auto rx_ = make_srd(x, (uint32_t)((size_t)g.n * g.cin * hin * win * 4u));
+  struct Step {
+    f32x4 d[2][4];  // dY rows co (, co + 32): output columns X0 + 16h .. +15
+    f32x4 b[2][2];  // input rows ci (, ci + 32 for CI2): columns c0 + 1 .. c0 + 8
+    float bl[2], br[2];  // columns c0 and c0 + 9 (c0 = X0 / 2 + 8h - 1)
+  };
+  int ln, ly, lxs;  // image, input row y (output row 2y + a), 32-column step
+  auto load = [&](Step& t) {
+    const int n = ln, y = ly, X0 = lxs * 32;
+    if (++lxs == wsteps) {
+      lxs = 0;
+      if (++ly == hin) {
+        ly = 0;
+        ++ln;
+      }
+    }
+    const int Y = 2 * y + a;
+    const uint32_t oa = (uint32_t)((((size_t)n * g.cout + co) * H + Y) * W + X0 + 16 * h) * 4u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t.d[0][k] = buf_ld4(rdy, co_ok ? oa + 16u * k : BUF_OOB);
+    if constexpr (!CI2) {
+      const uint32_t oc = oa + (uint32_t)32 * H * W * 4u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t.d[1][k] = buf_ld4(rdy, co2_ok ? oc + 16u * k : BUF_OOB);
+    }
+    const int iy = y - 1 + a + ry, c1 = X0 / 2 + 8 * h;  // c1 = c0 + 1
+#pragma unroll
+    for (int j = 0; j < (CI2 ? 2 : 1); ++j) {
+      const bool bok = (j ? ci2_ok : ci_ok) && iy >= 0 && iy < hin;
+      const uint32_t ob =
+          (uint32_t)((((size_t)n * g.cin + ci + 32 * j) * hin + iy) * win + c1) * 4u;
+      t.b[j][0] = buf_ld4(rx_, bok ? ob : BUF_OOB);
+      t.b[j][1] = buf_ld4(rx_, bok ? ob + 16u : BUF_OOB);
+      t.bl[j] = buf_ld(rx_, (bok && c1 > 0) ? ob - 4u : BUF_OOB);
+      t.br[j] = buf_ld(rx_, (bok && c1 + 8 < win) ? ob + 32u : BUF_OOB);
+    }
+  };
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  auto split2 = [](f2 v, uint32_t& hi, uint32_t& lo) {
+    const auto hh = __builtin_amdgcn_cvt_pkrtz(v.x, v.y);
+    hi = __builtin_bit_cast(uint32_t, hh);
+    const f2 hf = {(float)hh[0], (float)hh[1]};
+    const f2 r = v - hf;
+    lo = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(r.x, r.y));
+  };
+  auto compute = [&](const Step& t) {
+    const f2 sd2 = {sd, sd}, sv2 = {sv, sv};
+    // A fragments [cout tile][b]: the even (b = 0) / odd (b = 1) columns of the lane's 16
+    h8 ah[2][2], al[2][2];
+#pragma unroll
+    for (int i = 0; i < (CI2 ? 1 : 2); ++i) {
+      float dv[16];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dv[4 * k + e] = t.d[i][k][e];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        uint32_t hs[4], ls[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f2 v = {dv[4 * q + b], dv[4 * q + 2 + b]};
+          split2(v * sd2, hs[q], ls[q]);
+        }
+        ah[i][b] = __builtin_bit_cast(h8, u4v{hs[0], hs[1], hs[2], hs[3]});
+        al[i][b] = __builtin_bit_cast(h8, u4v{ls[0], ls[1], ls[2], ls[3]});
+      }
+    }
+    // B: input columns c0 .. c0 + 9 -> 5 packed pairs; shift s in {0, 1, 2} = b + rx
+    uint32_t ph[2][5], pl[2][5];
+#pragma unroll
+    for (int j = 0; j < (CI2 ? 2 : 1); ++j) {
+      float bv[10];
+      bv[0] = t.bl[j];
+      bv[9] = t.br[j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bv[1 + e] = t.b[j][0][e];
+        bv[5 + e] = t.b[j][1][e];
+      }
+#pragma unroll
+      for (int q = 0; q < 5; ++q) split2(f2{bv[2 * q], bv[2 * q + 1]} * sv2, ph[j][q], pl[j][q]);
+    }
+    auto frag = [&](int j, int sft, h8& fh, h8& fl) {
+      uint32_t fh4[4], fl4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (sft == 0) {
+          fh4[q] = ph[j][q];
+          fl4[q] = pl[j][q];
+        } else if (sft == 2) {
+          fh4[q] = ph[j][q + 1];
+          fl4[q] = pl[j][q + 1];
+        } else {
+          fh4[q] = __builtin_amdgcn_alignbit(ph[j][q + 1], ph[j][q], 16);
+          fl4[q] = __builtin_amdgcn_alignbit(pl[j][q + 1], pl[j][q], 16);
+        }
+      }
+      fh = __builtin_bit_cast(h8, u4v{fh4[0], fh4[1], fh4[2], fh4[3]});
+      fl = __builtin_bit_cast(h8, u4v{fl4[0], fl4[1], fl4[2], fl4[3]});
+    };
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int rx = 0; rx < 2; ++rx)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // cout tile (CI2: cin tile)
+          h8 fh, fl;
+          frag(CI2 ? i : 0, b + rx, fh, fl);
+          const h8 xh = ah[CI2 ? 0 : i][b], xl = al[CI2 ? 0 : i][b];
+          f32x16& c = acc[i][b * 2 + rx];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, fh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, fl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, fh, c, 0, 0, 0);
+        }
+  };
+
+  const int s0 = split * g.steps_per_split;
+  const int s1 = min(g.steps, s0 + g.steps_per_split);
+  {
+    const int r0 = s0 / wsteps;
+    lxs = s0 - r0 * wsteps;
+    ln = r0 / hin;
+    ly = r0 - ln * hin;
+  }
+  Step ring[PF];
+#pragma unroll
+  for (int k = 0; k < PF; ++k)
+    if (s0 + k < s1) load(ring[k]);
+  for (int s_ = s0; s_ < s1; s_ += PF) {
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      if (s_ + k < s1) {
+        compute(ring[k]);
+        if (s_ + k + PF < s1) load(ring[k]);
+      }
+    }
+  }
+  // partial [split][a*8 + ry*4 + b*2 + rx][co (cout32)][ci (cin32)], descaled (exact)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int orow = CI2 ? cot * 32 : cot * 64 + i * 32;
+      const int ocol = CI2 ? cit * 64 + i * 32 : cit * 32;
+      float* out = ws + (((size_t)split * 16 + a * 8 + ry * 4 + k) * g.cout32 + orow) * g.cin32 +
+                   ocol + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[(size_t)row * g.cin32] = acc[i][k][r] * descale;
+      }
+    }
+}
+
+// dW[co][ci][kh][kw] (+)= sum over splits, then over the 2 x 2 parity partials of the tap
+// (fixed order: split quarter by thread group, inside a split a-major, then b); 4 thread
+// groups per output as wgrad16_reduce4_kernel
+__global__ void __launch_bounds__(256)
+wgrad16up_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg16 g,
+                        int accumulate) {
+  __shared__ float part[4][64];
+  const int per = g.cout * g.cin, total = per * 9;
+  const int q = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s = 0.f;
+  int tap = 0, co = 0, ci = 0;
+  if (i < total) {
+    tap = i / per;
+    const int rem = i - tap * per;
+    co = rem / g.cin;
+    ci = rem - co * g.cin;
+    const int kh = tap / 3, kw = tap - 3 * kh;
+    // the partial planes of (kh, kw): (a, ry) with kh in K(a, ry), (b, rx) likewise
+    const int ar0 = kh == 0 ? 0 : 1, ar1 = kh == 2 ? 3 : 2;  // a*2+ry for a = 0 / a = 1
+    const int bc0 = kw == 0 ? 0 : 1, bc1 = kw == 2 ? 3 : 2;
+    int pl[4];
+    const int ars[2] = {ar0, ar1}, bcs[2] = {bc0, bc1};
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int aa = ars[u] >> 1, rr = ars[u] & 1, bb = bcs[v] >> 1, xx = bcs[v] & 1;
+        pl[u * 2 + v] = aa * 8 + rr * 4 + bb * 2 + xx;
+      }
+    const size_t plane = (size_t)g.cout32 * g.cin32, sstride = 16 * plane;
+    const float* src = ws + (size_t)co * g.cin32 + ci;
+    const int quarter = (g.nsplit + 3) / 4;
+    const int k0 = q * quarter, k1 = min(g.nsplit, k0 + quarter);
+    // four splits per iteration (16 loads in flight), four running sums per plane
+    float acc4[4][4] = {};
+    int k = k0;
+    for (; k + 3 < k1; k += 4) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const float* sp = src + (size_t)(k + m) * sstride;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc4[m][u] += sp[(size_t)pl[u] * plane];
+      }
+    }
+    for (int m = 0; k < k1; ++k, ++m) {
+      const float* sp = src + (size_t)k * sstride;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc4[m][u] += sp[(size_t)pl[u] * plane];
+    }
+    float t4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t4[u] = (acc4[0][u] + acc4[1][u]) + (acc4[2][u] + acc4[3][u]);
+    s = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+  }
+  part[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && i < total) {
+    const int j = threadIdx.x;
+    const float t = (part[0][j] + part[1][j]) + (part[2][j] + part[3][j]);
+    float* d = dw + ((size_t)co * g.cin + ci) * 9 + tap;
+    *d = accumulate ? *d + t : t;
+  }
+}
+
 // LDS-staged variant for the ITN's stride-1 layers with cout in {64, 128} and
 // cin % 64 == 0 (the residual convs 128 -> 128, the up convs 128 -> 64): a block
 // owns (all couts, 64 cins, kh) over a K split and steps through 16-pixel rows.
@@ -656,6 +923,7 @@ static Wg16Kernel wg16_kernel(const Wg16& g) {
 #endif
     return up ? wgrad16_lds_kernel<4, true, 3> : wgrad16_lds_kernel<4, false, 3>;
   }
+  if (g.mode == WG16_UPP) return g.ci2 ? wgrad16up_kernel<2, true> : wgrad16up_kernel<2, false>;
   if (g.ci2) return wgrad16_kernel<4, false, true>;
   if (g.mode == WG16_S2) return wgrad16_kernel<4, true>;
 #ifdef STX_AB
@@ -722,6 +990,13 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   g.steps = n * hv * (wv / 16);
   g.lds = wg16_lds_on() && (cout == 128 || (cout == 64 && lds_on_64())) && cin % 64 == 0 &&
           (in_mode == STX_IN_RAW || in_mode == STX_IN_RELU || in_mode == STX_IN_UPSAMPLE2);
+  // the upsampled input as parity classes (4 instead of 9 MACs per output; STX_WG16_UPP=0:
+  // the upsampled-row kernels): 32-column steps over the output rows of one row parity
+  static const bool upp_on = STX_KNOB("STX_WG16_UPP", 1) != 0;
+  if (upp_on && in_mode == STX_IN_UPSAMPLE2 && !g.lds && wv % 32 == 0 && hv % 2 == 0) {
+    g.mode = WG16_UPP;
+    g.steps = n * (hv / 2) * (wv / 32);
+  }
   if (g.lds) {  // blocks of (all couts x 64 cins x kh) x K split: ~512 blocks
     g.ncot = 1;
     g.ncit = cout == 64 && cin % 128 == 0 ? cin / 128 : cin / 64;  // CIB
@@ -734,7 +1009,9 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   static const int rounds = std::max(1, STX_KNOB("STX_WG16_ROUNDS", 1));
   const int slots = rounds * wg16_slots(wg16_kernel(g));
   // blocks per split: (kh x cin tiles) for the LDS kernel; 4 units (waves) per block
-  int ns = g.lds ? slots / (3 * g.ncit) : slots * 4 / (3 * g.ncot * g.ncit);
+  // (parity classes: 4 (ry, a) units per cout / cin tile pair instead of 3 kh)
+  const int kq = g.mode == WG16_UPP ? 4 : 3;
+  int ns = g.lds ? slots / (3 * g.ncit) : slots * 4 / (kq * g.ncot * g.ncit);
   ns = std::max(1, std::min(ns, cdiv(g.steps, 8)));  // >= 8 steps per split
   g.steps_per_split = cdiv(g.steps, ns);
   g.nsplit = cdiv(g.steps, g.steps_per_split);
@@ -748,7 +1025,7 @@ using namespace stx;
 extern "C" size_t stx_conv2d_wgrad16_ws(int n, int cin, int cout, int in_mode, int hv, int wv) {
   Wg16 g;
   if (!wg16_plan(n, cin, cout, in_mode, hv, wv, g)) return 0;
-  return (size_t)g.nsplit * 9 * g.cout32 * g.cin32 * sizeof(float);
+  return (size_t)g.nsplit * (g.mode == WG16_UPP ? 16 : 9) * g.cout32 * g.cin32 * sizeof(float);
 }
 
 extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, int accumulate,
@@ -778,11 +1055,16 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
     return STX_E_WORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
-  const int units = g.nsplit * 3 * g.ncot * g.ncit;
+  const int units = g.nsplit * (g.mode == WG16_UPP ? 4 : 3) * g.ncot * g.ncit;
   const int blocks = g.lds ? g.nsplit * 3 * g.ncit : cdiv(units, 4);
   hipLaunchKernelGGL(wg16_kernel(g), dim3(blocks), dim3(256), 0, st, x, dy, (float*)ws, x_amax,
                      dy_amax, g);
   const long long total = (long long)cout * cin * 9;
+  if (g.mode == WG16_UPP) {
+    hipLaunchKernelGGL(wgrad16up_reduce_kernel, dim3((int)((total + 63) / 64)), dim3(256), 0, st,
+                       (const float*)ws, dw, g, accumulate);
+    return check_launch("stx_conv2d_wgrad16 (parity classes)");
+  }
   const int rblocks = (int)std::min<long long>((total + 255) / 256, 4096);
   if (rblocks < 512 && g.nsplit >= 32)
     hipLaunchKernelGGL(wgrad16_reduce4_kernel, dim3((int)((total + 63) / 64)), dim3(256), 0, st,

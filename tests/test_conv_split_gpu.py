@@ -637,7 +637,13 @@ def test_split_gram_bwd_window_ties(dev, c):
                                   (1, 64, 128, 3, 16, N.STX_IN_RAW),
                                   # cout 64, cin % 128 == 0: 128 cins per block
                                   (2, 256, 64, 6, 16, N.STX_IN_RAW),
-                                  (1, 128, 64, 5, 32, N.STX_IN_RELU)])
+                                  (1, 128, 64, 5, 32, N.STX_IN_RELU),
+                                  # upsampled input as parity classes (wgrad16up_kernel):
+                                  # the ITN up convs, ragged cin / cout tiles, CI2
+                                  (2, 128, 64, 32, 32, N.STX_IN_UPSAMPLE2),
+                                  (2, 64, 32, 48, 64, N.STX_IN_UPSAMPLE2),
+                                  (1, 48, 40, 7, 16, N.STX_IN_UPSAMPLE2),
+                                  (3, 24, 20, 5, 48, N.STX_IN_UPSAMPLE2)])
 def test_split_wgrad(dev, case):
     """3x3 weight gradient on the split MFMA vs fp64 (and the fp32 MFMA kernel)."""
     n, cin, cout, h, w, mode = case
