@@ -440,7 +440,7 @@ wgrad16_reduce4_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg1
 // step is 32 output columns of one row: the lane's 16 dY pixels split into the b = 0 / 1
 // halves (evens / odds: two A fragments) and its 10 input pixels give the three shifted B
 // fragments, shift b + rx (the kw fragments of the plain kernel).  Partials
-// [split][a*8 + ry*4 + b*2 + rx][co][ci].
+// [split][a*6 + ry*3 + kw][co][ci] (the column taps assembled in registers).
 constexpr int WG16_UPP = 17;  // private mode: the parity-class form of STX_IN_UPSAMPLE2
 
 template <int PF, bool CI2>
@@ -614,26 +614,29 @@ wgrad16up_kernel(const float* __restrict__ x, const float* __restrict__ dy, floa
       }
     }
   }
-  // partial [split][a*8 + ry*4 + b*2 + rx][co (cout32)][ci (cin32)], descaled (exact)
+  // the column taps assembled here (kw = 0: (b, rx) = (0,0) + (1,0); 1: (0,1) + (1,0);
+  // 2: (0,1) + (1,1)), so the partial is [split][a*6 + ry*3 + kw][co (cout32)][ci (cin32)],
+  // descaled (exact)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int kw = 0; kw < 3; ++kw) {
       const int orow = CI2 ? cot * 32 : cot * 64 + i * 32;
       const int ocol = CI2 ? cit * 64 + i * 32 : cit * 32;
-      float* out = ws + (((size_t)split * 16 + a * 8 + ry * 4 + k) * g.cout32 + orow) * g.cin32 +
+      const int k0 = kw == 0 ? 0 : 1, k1 = kw == 2 ? 3 : 2;
+      float* out = ws + (((size_t)split * 12 + a * 6 + ry * 3 + kw) * g.cout32 + orow) * g.cin32 +
                    ocol + l32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        out[(size_t)row * g.cin32] = acc[i][k][r] * descale;
+        out[(size_t)row * g.cin32] = (acc[i][k0][r] + acc[i][k1][r]) * descale;
       }
     }
 }
 
-// dW[co][ci][kh][kw] (+)= sum over splits, then over the 2 x 2 parity partials of the tap
-// (fixed order: split quarter by thread group, inside a split a-major, then b); 4 thread
-// groups per output as wgrad16_reduce4_kernel
+// dW[co][ci][kh][kw] (+)= sum over splits of the tap's two row-parity partials (fixed
+// order: split quarters by thread group, a = 0 and a = 1 sums added last); 4 thread groups
+// per output as wgrad16_reduce4_kernel
 __global__ void __launch_bounds__(256)
 wgrad16up_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg16 g,
                         int accumulate) {
@@ -649,42 +652,20 @@ wgrad16up_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg
     co = rem / g.cin;
     ci = rem - co * g.cin;
     const int kh = tap / 3, kw = tap - 3 * kh;
-    // the partial planes of (kh, kw): (a, ry) with kh in K(a, ry), (b, rx) likewise
-    const int ar0 = kh == 0 ? 0 : 1, ar1 = kh == 2 ? 3 : 2;  // a*2+ry for a = 0 / a = 1
-    const int bc0 = kw == 0 ? 0 : 1, bc1 = kw == 2 ? 3 : 2;
-    int pl[4];
-    const int ars[2] = {ar0, ar1}, bcs[2] = {bc0, bc1};
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        const int aa = ars[u] >> 1, rr = ars[u] & 1, bb = bcs[v] >> 1, xx = bcs[v] & 1;
-        pl[u * 2 + v] = aa * 8 + rr * 4 + bb * 2 + xx;
-      }
-    const size_t plane = (size_t)g.cout32 * g.cin32, sstride = 16 * plane;
+    // the two row partials of (kh, kw): (a = 0, ry = kh > 0) and (a = 1, ry = kh == 2)
+    const size_t plane = (size_t)g.cout32 * g.cin32, sstride = 12 * plane;
+    const size_t p0 = (size_t)((kh == 0 ? 0 : 1) * 3 + kw) * plane;
+    const size_t p1 = (size_t)(6 + (kh == 2 ? 1 : 0) * 3 + kw) * plane;
     const float* src = ws + (size_t)co * g.cin32 + ci;
     const int quarter = (g.nsplit + 3) / 4;
     const int k0 = q * quarter, k1 = min(g.nsplit, k0 + quarter);
-    // four splits per iteration (16 loads in flight), four running sums per plane
-    float acc4[4][4] = {};
-    int k = k0;
-    for (; k + 3 < k1; k += 4) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const float* sp = src + (size_t)(k + m) * sstride;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc4[m][u] += sp[(size_t)pl[u] * plane];
-      }
-    }
-    for (int m = 0; k < k1; ++k, ++m) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int k = k0; k < k1; ++k) {
       const float* sp = src + (size_t)k * sstride;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc4[m][u] += sp[(size_t)pl[u] * plane];
+      s0 += sp[p0];
+      s1 += sp[p1];
     }
-    float t4[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) t4[u] = (acc4[0][u] + acc4[1][u]) + (acc4[2][u] + acc4[3][u]);
-    s = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+    s = s0 + s1;
   }
   part[q][threadIdx.x & 63] = s;
   __syncthreads();
@@ -1025,7 +1006,7 @@ using namespace stx;
 extern "C" size_t stx_conv2d_wgrad16_ws(int n, int cin, int cout, int in_mode, int hv, int wv) {
   Wg16 g;
   if (!wg16_plan(n, cin, cout, in_mode, hv, wv, g)) return 0;
-  return (size_t)g.nsplit * (g.mode == WG16_UPP ? 16 : 9) * g.cout32 * g.cin32 * sizeof(float);
+  return (size_t)g.nsplit * (g.mode == WG16_UPP ? 12 : 9) * g.cout32 * g.cin32 * sizeof(float);
 }
 
 extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, int accumulate,

@@ -162,3 +162,31 @@ def test_itn_instnorm_layers_vs_fp64(records, dev):
                                  ("dbeta", bt.grad, bc.grad, db64)):
             worst.append((_check(f"{name} {tag}", got, r32, t)[0], name, tag))
     print("worst IN-layer errors vs fp64:", sorted(worst)[-4:])
+
+
+@pytest.mark.parametrize("shape", [(2, 4, 256, 256), (1, 3, 128, 256), (1, 2, 256, 512)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_instnorm_large_planes_vs_fp64(dev, shape, relu):
+    """InstanceNorm(+ReLU) forward / backward on large planes (the ITN's 256^2 layers take
+    the segmented two-pass backward: per-4096-float segment sums, merged in segment order)
+    vs torch fp64; the parameter gradients through the deferred-partials path agree."""
+    g = torch.Generator().manual_seed(7)
+    x64 = torch.randn(*shape, generator=g, dtype=torch.float64) * 3 + 1
+    dy64 = torch.randn(*shape, generator=g, dtype=torch.float64)
+    c = shape[1]
+    g64 = torch.rand(c, generator=g, dtype=torch.float64) + 0.5
+    b64 = torch.randn(c, generator=g, dtype=torch.float64)
+    x = x64.float().to(dev).requires_grad_()
+    gm = g64.float().to(dev).requires_grad_()
+    bt = b64.float().to(dev).requires_grad_()
+    y = A.instance_norm(x, gm, bt, eps=1e-5, relu=relu)
+    y.backward(dy64.float().to(dev))
+    xr = x64.clone().requires_grad_()
+    gr, br = g64.clone().requires_grad_(), b64.clone().requires_grad_()
+    yr = F.instance_norm(xr, weight=gr, bias=br, eps=1e-5)
+    yr = F.relu(yr) if relu else yr
+    yr.backward(dy64)
+    for tag, got, ref in (("y", y.detach(), yr.detach()), ("dx", x.grad, xr.grad),
+                          ("dgamma", gm.grad, gr.grad), ("dbeta", bt.grad, br.grad)):
+        e = float((got.double().cpu() - ref).norm() / ref.norm())
+        assert e < 2e-5, (tag, e)
