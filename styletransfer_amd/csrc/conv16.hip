@@ -692,6 +692,10 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
   const int nchunks = cdiv(p.cin, 16);
   const int nsteps = KS * nchunks;
+  // the parity-class forms with cout <= 32 in this block (the ITN's 32-channel layers:
+  // the up conv to 32 channels, the first down conv's data gradient): the second 32-row
+  // MFMA tile would only multiply the slab's zero padding
+  const bool half_m = (PAR || UPP) && co0 + 32 >= p.cout;
   const int ex = amax_exp(read_amax(p.in_amax));
   const int ew = amax_exp(read_amax(p.w_amax)) + (UPP ? 2 : 0);  // (UPP: |W'| <= 4 max|w|)
   const float sx = __builtin_ldexpf(1.f, 15 - ex);
@@ -906,6 +910,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
                   *reinterpret_cast<const f16x8*>(bbase[j] + (C::NITEM + k * C::RW + rx) * 16);
 #pragma unroll
               for (int i = 0; i < 2; ++i) {
+                if (i == 1 && half_m) break;  // (rows past cout: nothing to compute)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh, acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, acc[i][j], 0, 0, 0);
@@ -944,6 +949,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
                   *reinterpret_cast<const f16x8*>(bbase[jt] + (C::NITEM + k * C::RW + tl) * 16);
 #pragma unroll
               for (int i = 0; i < 2; ++i) {
+                if (i == 1 && half_m) break;  // (rows past cout: nothing to compute)
                 acc[i][jt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh, acc[i][jt], 0, 0, 0);
                 acc[i][jt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl, acc[i][jt], 0, 0, 0);
                 acc[i][jt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh, acc[i][jt], 0, 0, 0);
