@@ -109,6 +109,8 @@ def test_split_conv_stride2(dev, case):
                                   (8, 64, 32, 128, 128, False),   # ITN up-conv 2
                                   (2, 32, 48, 20, 45, True),      # ragged tiles, relu_out
                                   (1, 16, 20, 17, 33, False),     # wo = 66, odd bands
+                                  (2, 20, 40, 9, 40, True),       # ragged chunk, cout 40
+                                  (1, 40, 72, 12, 24, False),     # cout > 64: two blocks
                                   (1, 128, 64, 270, 480, False)])  # video 1080p / 4
 def test_split_conv_upsample_parity(dev, case):
     """The upsampled-input conv as four output-parity 2x2 convs over the input
