@@ -194,3 +194,40 @@ def test_loader_workers_per_rank(monkeypatch):
         assert D.default_workers(lw) == max(0, min(16, n // lw - 1))
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
     assert D.default_workers() == max(0, min(16, n // 4 - 1))
+
+
+def test_parity_and_gram128_host_contracts():
+    """Round-5 host logic without a GPU: the 128-channel fused Gram's slab geometry and its
+    single-round gate, the parity-class upsampling slab size, the trained network's slab
+    jobs (the two up convs get a parity-class job), and the new stx_conv2d contracts
+    (wt16_up only on an upsampled-input split conv; mse_ref only with a 128-channel
+    fused Gram) refused before any launch."""
+    import ctypes as C
+    import torch
+    from styletransfer_amd import _native as N
+    from styletransfer_amd import network, ops
+    assert [ops.gram_tile_units(c) for c in (3, 64, 128, 256)] == [1, 1, 3, 10]
+    # conv2_2 at Gatys 512^2 (256 tiles: one round) vs fast_st's B = 8 (512 blocks)
+    assert ops.conv_gram_tiles(128, 128, 256, 256, n=1, in_mode=N.STX_IN_RELU) == 256
+    assert ops.conv_gram_tiles(64, 128, 256, 256, n=1, in_mode=N.STX_IN_RAW) == 256
+    assert ops.conv_gram_tiles(128, 128, 128, 128, n=8, in_mode=N.STX_IN_RELU) == 0
+    assert ops.conv_gram_tiles(128, 128, 256, 256, n=1, in_mode=N.STX_IN_UPSAMPLE2) == 0
+    L = N.lib()
+    # [a][cin16][ry][b, rx][hi, lo][cout64] fp16
+    assert L.stx_conv_weight16up_bytes(64, 32) == 2 * 64 * 2 * 4 * 2 * 64 * 2
+    assert L.stx_conv_weight16up_bytes(20, 40) == 2 * 32 * 2 * 4 * 2 * 64 * 2
+    net = network.ImageTransformNet(torch.rand(3, 8, 8), batch_size=1).to("cpu")
+    convs = [m for m in net.modules() if isinstance(m, network.Conv2d)]
+    ups = [c for c in convs if c._up_input]
+    assert [tuple(c.weight.shape[:2]) for c in ups] == [(64, 128), (32, 64)]
+    slabs = ops.TrainedSlabs(convs)
+    kinds = [slabs._jobs[i].kind for i in range(slabs._njobs)]
+    assert kinds.count(N.STX_WPREP_F16UP) == 2
+    assert sum(s[5] is not None for s in slabs.slabs) == 2
+    base = dict(x=16, y=32, n=1, cin=64, h=32, w=32, cout=64, ks=3, stride=1, pad=1,
+                cin_pad=64, cout_pad=64, wt16=48, w_amax=64, in_amax=80)
+    p = N.ConvParams(in_mode=N.STX_IN_RAW, hv=32, wv=32, ho=32, wo=32, wt16_up=96, **base)
+    assert L.stx_conv2d(C.byref(p), None) == 1001 and b"wt16_up" in L.stx_last_error_string()
+    p = N.ConvParams(in_mode=N.STX_IN_RAW, hv=32, wv=64, ho=32, wo=64, gram_part=112,
+                     mse_ref=128, mse_parts=144, **dict(base, w=64))
+    assert L.stx_conv2d(C.byref(p), None) == 1001 and b"mse_ref" in L.stx_last_error_string()
