@@ -564,20 +564,21 @@ static bool gram_tri_on(int c, int hw) {
   return on && (c == 128 || (all && c == 256)) && hw % 64 == 0;
 }
 
-// grid (ntu * FSUB, B), 1024 threads: 64 tile elements (16 lanes x float4, one 256-B
-// row segment of every partial) x 64 split-lanes.  Split-lane kl sums partials kl,
-// kl + 64, ... (four float4 accumulators, so each lane keeps several loads in flight);
-// the 64 lane sums of an element are added through LDS in split-lane order, so the
-// result is bit-reproducible.  (16-element x 16-lane blocks reading 64-B segments
-// left the reduction latency-bound: 11.8 us for the 16.8 MB of C=64 @ 512^2 partials.)
-constexpr int FEL = 64, FKL = 64, FNT = FEL / 4 * FKL;  // elements, split-lanes, threads
+// grid (ntu * FSUB, B), 512 threads: 64 tile elements (16 lanes x float4, one 256-B
+// row segment of every partial) x 32 split-lanes.  Split-lane kl sums partials kl,
+// kl + 32, ... (four float4 accumulators, so each lane keeps several loads in flight);
+// the 32 lane sums of an element are added through LDS in split-lane order, so the
+// result is bit-reproducible.  (64 split-lanes in 1024-thread blocks left each lane 4
+// partials at fast_st's batch: the batched launch 57.2 -> 52.5 us there, Gatys 17.3 ->
+// 15.4 us with 32; 16 lanes: 50.2 / 18.1 us; 16-element x 16-lane blocks reading 64-B
+// segments were latency-bound: 11.8 us for the 16.8 MB of C=64 @ 512^2 partials.)
+constexpr int FEL = 64, FKL = 32, FNT = FEL / 4 * FKL;  // elements, split-lanes, threads
 constexpr int FSUB = GT * GT / FEL;   // 64-element sub-tiles per tile (loss partials)
 // Few partials per tile (the 128 / 256-channel taps at small HW and large batch: a handful
-// of splits) would leave most of a block's 64 split-lanes idle and pay the 64-deep LDS
-// sum per element anyway, in thousands of blocks: such a block takes G = 2 or 4 sub-tiles
-// with 64 / G split-lanes each (G from nsplit, so every caller of a tap picks the same
-// order and the same bits).
-__host__ __device__ inline int fin_groups(int nsplit) { return nsplit <= 16 ? 4 : nsplit <= 32 ? 2 : 1; }
+// of splits) would leave most of a block's split-lanes idle: such a block takes G = 2 or 4
+// sub-tiles with 32 / G split-lanes each (G from nsplit, so every caller of a tap picks
+// the same order and the same bits).
+__host__ __device__ inline int fin_groups(int nsplit) { return nsplit <= 8 ? 4 : nsplit <= 16 ? 2 : 1; }
 __host__ __device__ inline int fin_blocks_per_tile(int nsplit) { return FSUB / fin_groups(nsplit); }
 
 // block (bx, by) of a finalize over grid (ntu * fin_blocks_per_tile(nsplit), b)
