@@ -540,6 +540,19 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
   // max|v| over the valid outputs: a per-lane mask (pixel inside the image) ANDed
   // into the IEEE bits; rows past cout exist only in a ragged last 64-row tile, where
   // a per-row mask is added
+  // the skip gradient of every element first: a load issued after one of this loop's
+  // stores waits for that store (vmcnt counts both), which serialised the loop into 32 / 64
+  // load -> store round trips
+  float auxv[AUX ? NI : 1][2][16];
+  if constexpr (AUX) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          auxv[j][i][r] = buf_ld(raux, vo[j] + (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * pb);
+  }
   const bool rows_full = rows >= 64;
   uint32_t lmask[NI];
 #pragma unroll
@@ -553,7 +566,7 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
       for (int r = 0; r < 16; ++r) {
         const int row = i * 32 + (r & 3) + 8 * (r >> 2);
         float v = fmaf(acc[i][j][r], scale, bias_r[i][r]);
-        if (AUX) v += p.aux_scale * buf_ld(raux, vo[j] + (uint32_t)row * pb);
+        if (AUX) v += p.aux_scale * auxv[j][i][r];
         if (RELU) v = fmaxf(v, 0.f);
         if constexpr (!POOLSUM && !PAR) buf_st(ry, vo[j] + (uint32_t)row * pb, v);
         acc[i][j][r] = v;  // kept for the fused pooled output (PAR: for the paired stores)
@@ -850,8 +863,12 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][NI], const stx_co
   const size_t wofs = ((size_t)n * p.cout + co_w) * plane;
   const uint32_t pb = (uint32_t)plane * 4u;
   const auto ry = make_srd(p.y + wofs, rows * pb);
-  const auto rmask = make_srd(p.mask ? p.mask + wofs : p.y, rows * pb);
-  const auto raux = make_srd(p.aux ? p.aux + wofs : p.y, rows * pb);
+  // (absent operands: zero-size descriptors, so every load below is issued unconditionally
+  // -- a load inside a per-element branch gets its own vmcnt(0) wait)
+  const bool has_mask = !mask_done && p.mask, has_aux = p.aux, has_acc = p.accumulate;
+  const auto rmask = make_srd(has_mask ? p.mask + wofs : p.y, has_mask ? rows * pb : 0u);
+  const auto raux = make_srd(has_aux ? p.aux + wofs : p.y, has_aux ? rows * pb : 0u);
+  const auto racc = make_srd(p.y + wofs, has_acc ? rows * pb : 0u);
   uint32_t vo[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -861,29 +878,36 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][NI], const stx_co
     vo[j] = (oy < p.ho && ox < p.wo) ? (uint32_t)(4 * h * (int)plane + oy * p.wo + ox) * 4u
                                      : BUF_OOB;
   }
-  float bias_r[2][16];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = co_w + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      bias_r[i][r] = (p.bias && co < p.cout) ? p.bias[co] : 0.f;
-    }
+  const auto rbias = make_srd(p.bias ? p.bias + co_w : p.y, p.bias ? rows * 4u : 0u);
   const float sc = (!mask_done && p.acc_scale) ? *p.acc_scale : 1.f;
+  // per group of EG elements of one (j, i) register tile: the group's loads first, then
+  // its stores -- a load issued after a store waits for it (vmcnt counts both), which
+  // serialised an element-at-a-time pass into a load -> store round trip per element
+  constexpr int EG = 8;
   uint32_t vmax_u = 0u;  // max |v| as IEEE bits: NaN (above inf) propagates
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+    for (int r0 = 0; r0 < 16; r0 += EG) {
+      float mv[16], av[16], yv[16], bv[16];
+#pragma unroll
+      for (int r = r0; r < r0 + EG; ++r) {
         const uint32_t o = vo[j] + (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * pb;
+        bv[r] = buf_ld(rbias, (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 4u);
+        mv[r] = buf_ld(rmask, o);
+        av[r] = buf_ld(raux, o);
+        yv[r] = buf_ld(racc, o);
+      }
+#pragma unroll
+      for (int r = r0; r < r0 + EG; ++r) {
         float v = acc[i][j][r];
         if (!mask_done) {
           v *= sc;
-          if (p.mask) v = buf_ld(rmask, o) > 0.f ? v : 0.f;
+          v = (!has_mask || mv[r] > 0.f) ? v : 0.f;
         }
-        v += bias_r[i][r];
+        v += bv[r];
         if (ROWPAIR) {
           if ((dsel[j] >> (i * 16 + r)) & 1u) v += dpv[i][r];
         } else if (p.up_dp) {
@@ -911,14 +935,20 @@ __device__ __forceinline__ void conv_epilogue(f32x16 (&acc)[2][NI], const stx_co
             }
           }
         }
-        if (p.aux) v += p.aux_scale * buf_ld(raux, o);
-        if (p.accumulate) v += buf_ld(ry, o);
+        v = has_aux ? v + p.aux_scale * av[r] : v;
+        v = has_acc ? v + yv[r] : v;
         if (p.relu_out) v = fmaxf(v, 0.f);
+        acc[i][j][r] = v;  // (kept for the fused pooled output)
+      }
+#pragma unroll
+      for (int r = r0; r < r0 + EG; ++r) {
+        const uint32_t o = vo[j] + (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * pb;
+        const float v = acc[i][j][r];
         buf_st(ry, o, v);
-        if (ROWPAIR) acc[i][j][r] = v;  // kept for the fused pooled output
         // elements outside the output (dropped stores) must not count
         if (o < rows * pb) vmax_u = max(vmax_u, __float_as_uint(v) & 0x7fffffffu);
       }
+    }
     }
   }
   const float vmax = __uint_as_float(vmax_u);
