@@ -690,8 +690,9 @@ wgrad16up_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg
 // instead of 8 waves), so the split-K slab the reduce kernel reads is half as big.
 // CIB = cins per block (64; 128 for cout = 64, so each wave still owns two 32 x 32
 // (co, ci) tiles: 18 MFMAs per barrier instead of 9)
-template <int WCO, bool UP, int PF, int CIB = 64>  // WCO = couts / 32; UP: nearest x2
-__global__ void __launch_bounds__(256, 1)  // upsampled input; PF + 1 steps of loads in flight
+// RL: ReLU input (compile time: no per-element select)
+template <int WCO, bool UP, int PF, int CIB = 64, bool RL = false>  // WCO = couts / 32; UP:
+__global__ void __launch_bounds__(256, 1)  // nearest x2 upsampled input; PF + 1 steps in flight
 wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                    float* __restrict__ ws, const float* __restrict__ x_amax,
                    const float* __restrict__ dy_amax, Wg16 g) {
@@ -709,7 +710,7 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   const float sv = __builtin_ldexpf(1.f, 15 - ex), sd = __builtin_ldexpf(1.f, 15 - ed);
   const float descale = __builtin_ldexpf(1.f, ex + ed - 30);
   const int H = g.hv, W = g.wv, wsteps = W / 16;
-  const bool relu = g.mode == STX_IN_RELU;
+  constexpr bool relu = RL;
   // this wave's (co tile, ci tile) pairs: WCO = 4 -> co tile = wave, ci tiles 0, 1;
   // WCO = 2 -> co tile = wave & 1, ci tile(s) (wave >> 1) * NCI + 0 .. NCI - 1
   const int cot = WCO == 4 ? wave : (wave & 1);
@@ -719,6 +720,14 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   const int ci_g = cit * CIB + sci;        // (+ 64 r for row r < NCI)
   const auto rdy = make_srd(dy, (uint32_t)((size_t)g.n * g.cout * H * W * 4u));
   const auto rx = make_srd(x, (uint32_t)((size_t)g.n * g.cin * g.h * g.w * 4u));
+  // byte offsets = a per-lane part (channel row, pixel within the step) + a per-step
+  // uniform part (image, row, column step) -- 32-bit: the plan bounds every tensor < 2 GB
+  const uint32_t la = (uint32_t)(co * H * W + 8 * h) * 4u;
+  uint32_t lb[NCI];
+#pragma unroll
+  for (int r = 0; r < NCI; ++r)
+    lb[r] = (uint32_t)((ci_g + 64 * r) * g.h * g.w + (UP ? 2 * q : 4 * q)) * 4u;
+  const bool lft = q > 0;  // (x0 + 4q > 0 when x0 == 0)
   struct Ld {
     f32x4 a0, a1;        // dY[co][y][x0 + 8h .. +7]
     f32x4 v[NCI];        // V[ci][vy][x0 + 4q .. +3] (upsample: x[.][vy/2][(x0+4q)/2 .. +1] in v.xy)
@@ -738,26 +747,28 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
         ++ln;
       }
     }
-    const uint32_t oa = (uint32_t)((((size_t)n * g.cout + co) * H + y) * W + x0 + 8 * h) * 4u;
+    const uint32_t oa = (uint32_t)(((n * g.cout) * H + y) * W + x0) * 4u + la;
     t.a0 = buf_ld4(rdy, live ? oa : BUF_OOB);
     t.a1 = buf_ld4(rdy, live ? oa + 16u : BUF_OOB);
-    const int vy = y + kh - 1, px = x0 + 4 * q;
+    const int vy = y + kh - 1;
     const bool rok = live && vy >= 0 && vy < H;
+    const bool lok = rok && (x0 > 0 || lft);             // V[x0 + 4q - 1] exists
+    const bool rgt = rok && x0 + 4 * q + 4 < W;          // V[x0 + 4q + 4] exists
+    // (UP: V[vy][vx] = x[vy/2][vx/2]; x0 + 4q is even)
+    const uint32_t sb = UP ? (uint32_t)(((n * g.cin) * g.h + (vy >> 1)) * g.w + (x0 >> 1)) * 4u
+                           : (uint32_t)(((n * g.cin) * g.h + vy) * g.w + x0) * 4u;
 #pragma unroll
     for (int r = 0; r < NCI; ++r) {
-      const size_t cig = (size_t)ci_g + 64 * r;
+      const uint32_t ob = sb + lb[r];
       if constexpr (!UP) {
-        const uint32_t ob = (uint32_t)((((size_t)n * g.cin + cig) * g.h + vy) * g.w + px) * 4u;
         t.v[r] = buf_ld4(rx, rok ? ob : BUF_OOB);
-        t.vl[r] = buf_ld(rx, (rok && px > 0) ? ob - 4u : BUF_OOB);
-        t.vr[r] = buf_ld(rx, (rok && px + 4 < W) ? ob + 16u : BUF_OOB);
-      } else {  // V[vy][vx] = x[vy/2][vx/2]; px is a multiple of 4
-        const uint32_t ob =
-            (uint32_t)((((size_t)n * g.cin + cig) * g.h + (vy >> 1)) * g.w + (px >> 1)) * 4u;
+        t.vl[r] = buf_ld(rx, lok ? ob - 4u : BUF_OOB);
+        t.vr[r] = buf_ld(rx, rgt ? ob + 16u : BUF_OOB);
+      } else {
         t.v[r].x = buf_ld(rx, rok ? ob : BUF_OOB);
         t.v[r].y = buf_ld(rx, rok ? ob + 4u : BUF_OOB);
-        t.vl[r] = buf_ld(rx, (rok && px > 0) ? ob - 4u : BUF_OOB);
-        t.vr[r] = buf_ld(rx, (rok && px + 4 < W) ? ob + 8u : BUF_OOB);
+        t.vl[r] = buf_ld(rx, lok ? ob - 4u : BUF_OOB);
+        t.vr[r] = buf_ld(rx, rgt ? ob + 8u : BUF_OOB);
       }
     }
   };
@@ -893,6 +904,8 @@ static Wg16Kernel wg16_kernel(const Wg16& g) {
   if (g.lds) {
     const bool up = g.mode == STX_IN_UPSAMPLE2;
 #ifdef STX_AB  // measured variants (not in the product build): load-ring depths, cout 64
+    if (g.mode == STX_IN_RELU && g.cout != 128)
+      return wgrad16_lds_kernel<2, false, 3, 64, true>;
     static const int lpf = STX_KNOB("STX_WG16_LPF", 3);
     if (g.cout == 128 && !up && lpf >= 5)
       return lpf >= 7 ? wgrad16_lds_kernel<4, false, 7> : wgrad16_lds_kernel<4, false, 5>;
@@ -902,6 +915,7 @@ static Wg16Kernel wg16_kernel(const Wg16& g) {
       return up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>;
     }
 #endif
+    if (g.mode == STX_IN_RELU) return wgrad16_lds_kernel<4, false, 3, 64, true>;
     return up ? wgrad16_lds_kernel<4, true, 3> : wgrad16_lds_kernel<4, false, 3>;
   }
   if (g.mode == WG16_UPP) return g.ci2 ? wgrad16up_kernel<2, true> : wgrad16up_kernel<2, false>;
