@@ -753,7 +753,7 @@ __global__ void __launch_bounds__(256, 2) conv_fewout3_kernel(stx_conv_params p,
 // cycles).  The weights' scale is block-local (max over the 27 x 64 slab entries).
 // A lane's B fragment is 8 channels 16t + 8h + e of its pixel, loaded straight from
 // global memory and split in registers.
-template <int CIN>
+template <int CIN, bool RELU_IN = false>  // RELU_IN: ReLU input (compile time)
 __global__ void __launch_bounds__(256, 2) conv_fewout16_kernel(stx_conv_params p, int tiles_x) {
   constexpr int KST = CIN / 16;
   __shared__ float dt[27 * FO_RH * FO_RWP];
@@ -769,7 +769,7 @@ __global__ void __launch_bounds__(256, 2) conv_fewout16_kernel(stx_conv_params p
   const int oy0 = ty * FO_TH, ox0 = tx * FO_TW;
   const int plane_in = p.h * p.w;
   const float* __restrict__ xn = p.x + (size_t)n * CIN * plane_in;
-  const bool relu_in = p.in_mode == STX_IN_RELU;
+  constexpr bool relu_in = RELU_IN;
   // A: row m = co*9 + tap (rows >= 9*cout are 0), channel c = 16t + 8h + e
   const int m = l32, mco = m / 9, mt = m - mco * 9;
   const int mcl = min(mco, p.cout - 1);
@@ -905,9 +905,14 @@ int conv2d_fewout(const stx_conv_params& p, hipStream_t st) {
                   !p.out_amax && p.wt_batch_stride == 0 && p.wt && p.hv == p.h && p.wv == p.w;
   if (!ok) return -1;
   const int tiles_x = (p.wo + FO_TW - 1) / FO_TW, tiles_y = (p.ho + FO_TH - 1) / FO_TH;
-  if (p.in_amax && few16_on())
-    hipLaunchKernelGGL((conv_fewout16_kernel<64>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0,
-                       st, p, tiles_x);
+  if (p.in_amax && few16_on()) {
+    if (p.in_mode == STX_IN_RELU)
+      hipLaunchKernelGGL((conv_fewout16_kernel<64, true>), dim3(tiles_x * tiles_y, 1, p.n),
+                         dim3(256), 0, st, p, tiles_x);
+    else
+      hipLaunchKernelGGL((conv_fewout16_kernel<64>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256),
+                         0, st, p, tiles_x);
+  }
   else
     hipLaunchKernelGGL((conv_fewout3_kernel<64>), dim3(tiles_x * tiles_y, 1, p.n), dim3(256), 0,
                        st, p, tiles_x);
