@@ -293,7 +293,7 @@ def gatys_leg(args, world, rank, dev):
     loss = float(eng.total)
     # the kernel instance that launch takes (conv16.hip launch16v2): P2 = 3 the split
     # phase, 1 the fp32-MFMA phase
-    p2 = 1 if ca is None or os.environ.get("STX_P2_SPLIT", "1") == "0" else 3
+    p2 = 1 if ca is None or N.knob("STX_P2_SPLIT", "1") == "0" else 3
     return dict(rate=rate, dt=dt, loss=loss, run=run, kernel=dict(fwd_ms=fwd_ms, gflop=gf,
                                                          dg_kernel=DG_KERNEL.format(p2),
                                                          gflop_conv=gf_conv, tflops=achieved,
@@ -388,7 +388,7 @@ def fast_st_leg(args, world, rank, dev, B=None, steps=None):
     tr = FastStTrainer(itn, style, world_size=world)
     batch = torch.from_numpy(W.synthetic_image(4000 + rank, (B, 3, 256, 256))).to(dev)
     steps = steps or args.fast_steps
-    graph = not args.no_graph and os.environ.get("STX_FAST_GRAPH", "1") != "0"
+    graph = not args.no_graph and N.knob("STX_FAST_GRAPH", "1") != "0"
     if graph:  # hipGraph replays per training step (FastStTrainer.capture)
         replay, static, _ = tr.capture(batch, warmup=max(1, min(args.warmup, 2)))
         replay()

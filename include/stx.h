@@ -185,7 +185,10 @@ int stx_conv_weight_prep16(const float* w, void* wt16, float* w_amax, int cout, 
  * then dP4 = conv3_1^T(dZ5); stransfer/network.py:92-123 StyleLoss backward through
  * :264-314 the conv3_1 piece):  conv^T_w(A . z) = conv^T_{w'}(z) with
  *   w'[c][ci][kh][kw] = s * sum_co A[c*pitch + co] * w[co][ci][kh][kw]   (s = *scale or 1)
- * so the data gradient reads z directly and dZ = A z is never formed.  A is one image's
+ * so the data gradient reads z directly and dZ = A z is never formed.  The identity as
+ * written needs A symmetric, which the Gram-backward operator is (coef = c (G - T) with
+ * the diagonal alpha term; G and T symmetric); for a general A the launch computes
+ * conv^T_w(A^T . z).  A is one image's
  * [cout][pitch] operator (pitch >= cout; stx_style_loss's coef), a_amax an amax group
  * >= max|A| (the finalize's coef_amax), w [cout][cin][3][3] with w_amax >= max|w|.  One
  * launch writes the transposed split slab wtT16 (stx_conv_weight16_bytes(cin, cout, 3, 1)

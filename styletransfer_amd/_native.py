@@ -18,6 +18,16 @@ STX_IN_RAW, STX_IN_RELU, STX_IN_RELU_POOL2, STX_IN_UPSAMPLE2, STX_IN_DILATE2 = r
 STX_AMAX_SLOTS = 32  # an "amax" is a group of 32 floats whose max is the value (stx.h)
 STX_GRAM_GROUP = 8  # fused Gram partials per in-kernel group sum (stx_conv_params.gram_cnt)
 
+
+def knob(name: str, default: str) -> str:
+    """A measurement-only A/B switch of the Python host path: read from the environment
+    only when STX_AB=1 (tools/ab_engine.py and the other same-box A/B scripts), otherwise
+    the product default -- the product path is environment-independent, like the
+    library's compile-time STX_KNOBs (common.h; only `make AB=1` builds read those)."""
+    if os.environ.get("STX_AB") != "1":
+        return default
+    return os.environ.get(name, default)
+
 vp = C.c_void_p
 i32 = C.c_int
 i64 = C.c_longlong

@@ -16,18 +16,18 @@ def _c(t):
 
 def _split_on():
     import os
-    return os.environ.get("STX_CONV_SPLIT", "1") != "0"
+    return N.knob("STX_CONV_SPLIT", "1") != "0"
 
 
 def _upsample_fuse_on():
     import os
-    return os.environ.get("STX_UPSAMPLE_FUSE", "1") != "0"
+    return N.knob("STX_UPSAMPLE_FUSE", "1") != "0"
 
 
 def _upar_on():
     """STX_UPAR=0: upsampled-input convs over the upsampled halo (no parity classes; A/B)."""
     import os
-    return os.environ.get("STX_UPAR", "1") != "0"
+    return N.knob("STX_UPAR", "1") != "0"
 
 
 def _grad_into(param, g, accumulate_fn):

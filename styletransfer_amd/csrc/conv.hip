@@ -707,10 +707,11 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   if (p.wt16_up &&
       (p.in_mode != STX_IN_UPSAMPLE2 || !p.wt16 || p.wt16 == (const void*)1 || p.ks != 3 ||
        p.pad != 1 || p.stride != 1 || p.cin < 16 || p.cout <= 4 || p.wo <= 32 ||
+       p.hv != 2 * p.h || p.wv != 2 * p.w ||  // (the 2x2 parity taps assume the full x2 image)
        p.wt_batch_stride || p.mask || p.aux || p.accumulate || p.acc_scale || p.up_dp ||
        p.p2_z || p.pool_out || p.pool_sum || p.gram_part)) {
-    set_error("stx_conv2d: wt16_up needs an upsampled-input split conv (3x3 stride 1, wo > 32) "
-              "with the plain epilogue (bias / relu_out / out_amax)");
+    set_error("stx_conv2d: wt16_up needs an upsampled-input split conv (3x3 stride 1, wo > 32, "
+              "virtual size exactly 2h x 2w) with the plain epilogue (bias / relu_out / out_amax)");
     return STX_E_INVALID;
   }
   if ((p.mse_ref || p.mse_parts) && (!p.mse_ref || !p.mse_parts || !p.gram_part || p.cout != 128)) {

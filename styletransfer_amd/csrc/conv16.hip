@@ -230,41 +230,42 @@ __device__ __forceinline__ void phase2_f16(f32x16 (&acc)[2][2], const stx_conv_p
 // Split Gram-backward phase of the v2 data-gradient conv (P2 = 3): acc -- de-scaled,
 // *acc_scale, ReLU-masked and brought to the power-of-two scale S = 2^ls by `prologue`,
 // which runs once chunk 0's loads are issued -- gets + S * s2 * A[n] . z2 on the fp16
-// hi/lo MFMA with every scale precomputed: z2 by
-// its amax group (p2_amax: sz = 2^(15 - ez)), A' = s2 * A by the batch max the Gram
-// finalize wrote (p2_wt_amax: sa = S / sz <= 2^(15 - ea)).  No in-kernel reductions: the
-// round-3 port of phase2_f16 paid two block-wide max passes and a re-read of A for its
-// scales, and lost to the fp32 MFMA.  Per 16-channel chunk: z2 -> LDS [P][cg][256 px]
-// (16-B units of 8 channels, hi / lo planes); A' straight from memory into each lane's
-// fragment registers (no LDS round trip); 3 MFMAs per 32 x 32 tile (the fp32 phase:
-// 8 x 32x32x2 f32, 5x the MFMA cycles); the next chunk's loads are in flight during the
-// MFMAs.
+// hi/lo MFMA with every scale precomputed: z2 by its amax group (p2_amax: sz =
+// 2^(15 - ez)), A' = s2 * A by the batch max the Gram finalize wrote (p2_wt_amax: sa =
+// S / sz <= 2^(15 - ea)).  No in-kernel reductions: the round-3 port of phase2_f16 paid
+// two block-wide max passes and a re-read of A for its scales, and lost to the fp32 MFMA.
+// Per 16-channel chunk, into one of two LDS buffers (one barrier per chunk: chunk c+1 is
+// split and written while chunk c's MFMAs run):
+//   z2 -> [P][cg][256 px] 16-B units: thread t owns tile pixel t and writes its two
+//         channel groups' hi and lo units (lane-consecutive 16-B stores, conflict-free;
+//         the round-5 form wrote 8-B halves at a 64-B lane stride: 896 bank-conflict
+//         cycles per chunk and block) from 16 lane-coalesced dword loads;
+//   A' -> [P][cg][64 co] 16-B units, split once per block by waves 0-1 (each of the four
+//         waves split its own register copy of all 64 couts before);
+// then 3 MFMAs per 32 x 32 tile from conflict-free ds_read_b128s.
 template <int TW, bool RP, class Prologue>
 __device__ __forceinline__ void phase2_pre(f32x16 (&acc)[2][2], const stx_conv_params& p,
                                            const EpiTile& t, int ls, int ez, char* smem,
                                            Prologue&& prologue) {
-  constexpr int NPIX = 256;
-  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  constexpr int NPIX = 256, BM = 64;
+  constexpr int ZB = 4 * NPIX * 16, AB_ = 4 * BM * 16, BUF = ZB + AB_;  // 20 KB per buffer
   const int tid = threadIdx.x, h = t.h, l32 = t.l32;
   const size_t plane = (size_t)p.ho * p.wo;
   const int C2 = p.p2_c;
   const float s2 = p.p2_scale ? *p.p2_scale : 1.f;
   const float sz = __builtin_ldexpf(1.f, 15 - ez);
   const float sa = __builtin_ldexpf(s2, ls - (15 - ez));
-  char* lz = smem;                  // [P][cg][256 px] x 16 B = 16 KB
-  // z2: thread -> pixel quad (4 consecutive pixels of a tile row) x channel quad cq
-  const int q = tid & 63, cq = tid >> 6;
-  const int qp = 4 * q, qrow = qp / TW, qcol = qp - qrow * TW;
-  const int qy = t.ty0 + qrow, qx = t.tx0 + qcol;
-  const bool vec = (p.wo & 3) == 0;  // rows 16-B aligned: a quad is all in or all out
-  const uint32_t zq_off = (qy < p.ho && qx < p.wo) ? (uint32_t)(qy * p.wo + qx) * 4u : BUF_OOB;
+  // z2: thread -> tile pixel tid (row tid / TW), all 16 channels of the chunk
+  const int zy = t.ty0 + tid / TW, zx = t.tx0 + tid % TW;
+  const uint32_t z_off = (zy < p.ho && zx < p.wo) ? (uint32_t)(zy * p.wo + zx) * 4u : BUF_OOB;
   const uint32_t pb = (uint32_t)plane * 4u;
   const float* __restrict__ z2 = p.p2_z + (size_t)t.n * C2 * plane;
-  // A' fragments straight from memory (small, L2 resident): lane (h, l32) of tile i
-  // holds A[c0 + 8h + e][co0 + 32 i + l32], e < 8 (32 consecutive couts per load)
+  // A': threads 0..127 -> (channel group acg, cout aco): 8 channels of one cout
+  const bool a_thr = tid < 128;  // (waves 0 and 1: wave-uniform)
+  const int acg = (tid >> 6) & 1, aco = tid & 63;
   const auto ra = make_srd(p.p2_wt + (size_t)t.n * p.p2_wt_batch_stride,
                            (uint32_t)C2 * (uint32_t)p.cout_pad * 4u);
-  const uint32_t a_off = (uint32_t)((8 * h) * p.cout_pad + t.co0 + l32) * 4u;
+  const uint32_t a_off = (uint32_t)((8 * acg) * p.cout_pad + t.co0 + aco) * 4u;
   const uint32_t a_row = (uint32_t)p.cout_pad * 4u;
   int bpix[2];
 #pragma unroll
@@ -274,77 +275,76 @@ __device__ __forceinline__ void phase2_pre(f32x16 (&acc)[2][2], const stx_conv_p
     bpix[j] = ty * TW + tx;
   }
   struct Stage {
-    f32x4 z[4];  // [channel e of the quad] x 4 pixels
-    float a[2][8];
+    float z[16];  // channel e of the chunk at this thread's pixel
+    float a[8];   // channel 8 acg + e at cout aco
   };
   auto fetch = [&](int c0, Stage& g) {
+    // channels past C2 read 0 (descriptor range)
     const auto rz = make_srd(z2 + (size_t)c0 * plane, (uint32_t)max(0, C2 - c0) * pb);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t o = zq_off + (uint32_t)(4 * cq + e) * pb;
-      if (vec) {
-        g.z[e] = buf_ld4(rz, o);
-      } else {  // ragged width: per-pixel loads, pixels past the row end read 0
+    for (int e = 0; e < 16; ++e) g.z[e] = buf_ld(rz, z_off + (uint32_t)e * pb);
+    if (a_thr) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          g.z[e][k] = (qx + k < p.wo) ? buf_ld(rz, o + 4u * k) : 0.f;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 8; ++e)  // channels past C2 read 0 (descriptor range)
-        g.a[i][e] = buf_ld(ra, a_off + (uint32_t)(c0 + e) * a_row + (uint32_t)(128 * i));
-  };
-  auto stage = [&](const Stage& g) {
-    const int cg = cq >> 1, hf = cq & 1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      f16x4 hi, lo;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = g.z[e][k] * sz;
-        const _Float16 vh = (_Float16)v;
-        hi[e] = vh;
-        lo[e] = (_Float16)(v - (float)vh);
-      }
-      *reinterpret_cast<f16x4*>(lz + ((0 * 2 + cg) * NPIX + qp + k) * 16 + hf * 8) = hi;
-      *reinterpret_cast<f16x4*>(lz + ((1 * 2 + cg) * NPIX + qp + k) * 16 + hf * 8) = lo;
+      for (int e = 0; e < 8; ++e) g.a[e] = buf_ld(ra, a_off + (uint32_t)(c0 + e) * a_row);
     }
   };
-  auto split_a = [&](const Stage& g, f16x8 (&fa)[2][2]) {
+  auto split8 = [](const float* v, float s, f16x8& hi, f16x8& lo) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int e = 0; e < 8; ++e) {
+      const float x = v[e] * s;
+      const _Float16 xh = (_Float16)x;
+      hi[e] = xh;
+      lo[e] = (_Float16)(x - (float)xh);
+    }
+  };
+  auto stage = [&](const Stage& g, int b) {
+    char* lz = smem + b * BUF;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = g.a[i][e] * sa;
-        const _Float16 vh = (_Float16)v;
-        fa[i][0][e] = vh;
-        fa[i][1][e] = (_Float16)(v - (float)vh);
-      }
+    for (int cg = 0; cg < 2; ++cg) {
+      f16x8 hi, lo;
+      split8(g.z + 8 * cg, sz, hi, lo);
+      *reinterpret_cast<f16x8*>(lz + ((0 * 2 + cg) * NPIX + tid) * 16) = hi;
+      *reinterpret_cast<f16x8*>(lz + ((1 * 2 + cg) * NPIX + tid) * 16) = lo;
+    }
+    if (a_thr) {
+      char* la = lz + ZB;
+      f16x8 hi, lo;
+      split8(g.a, sa, hi, lo);
+      *reinterpret_cast<f16x8*>(la + ((0 * 2 + acg) * BM + aco) * 16) = hi;
+      *reinterpret_cast<f16x8*>(la + ((1 * 2 + acg) * BM + aco) * 16) = lo;
+    }
   };
   Stage g;
   fetch(0, g);
   prologue();  // the caller's scaling and mask, with chunk 0's loads in flight
-  for (int c0 = 0; c0 < C2; c0 += 16) {
-    __syncthreads();  // the previous chunk's (or the main loop's) LDS reads done
-    stage(g);
-    f16x8 fa[2][2];
-    split_a(g, fa);
-    __syncthreads();
-    if (c0 + 16 < C2) fetch(c0 + 16, g);
+  __syncthreads();  // the main loop's LDS reads done
+  stage(g, 0);
+  if (16 < C2) fetch(16, g);
+  int b = 0;
+  for (int c0 = 0; c0 < C2; c0 += 16, b ^= 1) {
+    __syncthreads();  // buffer b complete; buffer b^1's reads (chunk c0 - 16) done
+    const char* lz = smem + b * BUF;
+    const char* la = lz + ZB;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      f16x8 fa[2];
+#pragma unroll
+      for (int P = 0; P < 2; ++P)
+        fa[P] = *reinterpret_cast<const f16x8*>(la + ((P * 2 + h) * BM + i * 32 + l32) * 16);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f16x8 fb[2];
 #pragma unroll
         for (int P = 0; P < 2; ++P)
           fb[P] = *reinterpret_cast<const f16x8*>(lz + ((P * 2 + h) * NPIX + bpix[j]) * 16);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][0], fb[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][0], fb[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][1], fb[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0], fb[1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1], fb[0], acc[i][j], 0, 0, 0);
       }
+    }
+    if (c0 + 16 < C2) {  // the next chunk -> the other buffer, its successor's loads
+      stage(g, b ^ 1);
+      if (c0 + 32 < C2) fetch(c0 + 32, g);
     }
   }
   __syncthreads();  // LDS handed back to the epilogue
@@ -1049,6 +1049,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] *= up;
       };
+      static_assert(2 * (4 * 256 * 16 + 4 * 64 * 16) <= C::LDS_BYTES, "phase-2 buffers fit");
       phase2_pre<TW, RP>(acc, p, et, ls, ez, smem, prologue);
       conv_epilogue_plain_body<TW, NI, RP, false>(acc, p, et, __builtin_ldexpf(1.f, -ls), smem);
     } else if constexpr (P2 == 1) {

@@ -95,7 +95,7 @@ class SideStream:
 
     def begin(self, device):
         import os
-        if os.environ.get("STX_WGRAD_SIDE", "0") != "1":
+        if N.knob("STX_WGRAD_SIDE", "0") != "1":
             return
         key = torch.device(device).index or 0
         if key not in self.streams:
@@ -334,7 +334,7 @@ class TrainedSlabs:
         self._build()
 
     def _build(self):
-        split = os.environ.get("STX_CONV_SPLIT", "1") != "0"
+        split = N.knob("STX_CONV_SPLIT", "1") != "0"
         L = lib()
         jobs = []
         if self.slabs is not None:
@@ -370,7 +370,7 @@ class TrainedSlabs:
                     out.append((slab, None))
             up = None
             if f16 and stride == 1 and ks == 3 and getattr(conv, "_up_input", False) and \
-                    os.environ.get("STX_UPAR", "1") != "0":
+                    N.knob("STX_UPAR", "1") != "0":
                 up = torch.empty(L.stx_conv_weight16up_bytes(cin, cout), device=dev,
                                  dtype=torch.uint8)
                 jobs.append(N.WprepJob(w.data_ptr(), up.data_ptr(), am.data_ptr(),
@@ -399,7 +399,7 @@ class TrainedSlabs:
                               None if up is None else (up, wt16[1]))
 
 
-_S2_FWD = os.environ.get("STX_S2_FWD", "1") != "0"
+_S2_FWD = N.knob("STX_S2_FWD", "1") != "0"
 
 
 def split_eligible(cin, cout, ks, stride=1):
@@ -500,7 +500,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
             in_amax = amax(x)
         p.wt16, p.w_amax, p.in_amax = wt16[0].data_ptr(), wt16[1].data_ptr(), in_amax.data_ptr()
         if wt16_up is not None and in_mode == N.STX_IN_UPSAMPLE2 and ks == 3 and stride == 1 \
-                and pad == 1 and wo > 32 and not any(
+                and pad == 1 and wo > 32 and (hv, wv) == (2 * h, 2 * w) and not any(
                     v is not None for v in (mask, aux, acc_scale, p2_z, up_dp, pool_out,
                                             gram_part)) and not accumulate:
             p.wt16_up, p.w_amax = wt16_up[0].data_ptr(), wt16_up[1].data_ptr()
@@ -586,7 +586,7 @@ def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW,
         dw = torch.empty((cout, cin, ks, ks), device=x.device, dtype=torch.float32)
     L = lib()
     import os
-    split = split and os.environ.get("STX_CONV_SPLIT", "1") != "0"
+    split = split and N.knob("STX_CONV_SPLIT", "1") != "0"
     if split and ks == 9 and stride == 1 and pad == 4 and in_mode == N.STX_IN_RAW:
         # ITN conv0 / conv22: the 3-channel side expanded per tap row (wgrad9.hip)
         need9 = L.stx_conv2d_wgrad_few16_ws(n, cin, cout, ks, h, w)
@@ -612,7 +612,7 @@ def conv2d_wgrad(x, dy, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW,
                   "stx_conv2d_wgrad16")
             return dw
     if split and ks == 3 and stride == 2 and pad == 1 and in_mode == N.STX_IN_RAW \
-            and os.environ.get("STX_WG16_S2", "1") != "0" \
+            and N.knob("STX_WG16_S2", "1") != "0" \
             and h == 2 * ho and w == 2 * wo:
         need16 = L.stx_conv2d_wgrad16_s2_ws(n, cin, cout, ho, wo)
         if need16:

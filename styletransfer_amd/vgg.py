@@ -84,7 +84,7 @@ class VGGFeatures:
             self.b.append(bt)
             self.wt.append(ops.conv_weight_prep(wt))
             self.wtT.append(ops.conv_weight_prep(wt, transpose=True))
-            split = os.environ.get("STX_CONV_SPLIT", "1") != "0"
+            split = N.knob("STX_CONV_SPLIT", "1") != "0"
             self.wt16.append(ops.conv_weight_prep16(wt) if split and
                              ops.split_eligible(cin, cout, 3) else None)
             self.wtT16.append(ops.conv_weight_prep16(wt, transpose=True) if split and
@@ -115,7 +115,7 @@ class VGGFeatures:
         """Fused Gram partials per image conv l emits in a batch of n (0: not fusable)."""
         cout, cin = VGG_CONV_SHAPES[l]
         # conv1_1 (3 input channels) runs on convfew.hip's split kernel without a slab
-        if (cin >= 16 and self.wt16[l] is None) or os.environ.get("STX_GRAM_FUSE", "1") == "0":
+        if (cin >= 16 and self.wt16[l] is None) or N.knob("STX_GRAM_FUSE", "1") == "0":
             return 0
         return ops.conv_gram_tiles(cin, cout, ho, wo, n=n, in_mode=self._run_mode(l, wo))
 
@@ -132,7 +132,7 @@ class VGGFeatures:
         unless STX_GRAM_GROUPED=1: the in-launch reduction (ticket counter + sc1 hand-off)
         adds ~4.6 us to each producing conv, more than the smaller finalize saves (same-
         process A/B: Gatys 512^2 695 -> 703 us, fast_st B8 4478 -> 4469 us)."""
-        if os.environ.get("STX_GRAM_GROUPED", "0") != "1" or not self.gram_tiles(l, ho, wo, n):
+        if N.knob("STX_GRAM_GROUPED", "0") != "1" or not self.gram_tiles(l, ho, wo, n):
             return 0
         cout, cin = VGG_CONV_SHAPES[l]
         return ops.conv_gram_groups(cin, cout, ho, wo, n=n, in_mode=self._run_mode(l, wo))
@@ -245,8 +245,8 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         alpha = float(folded_weights[1]) * 2.0 / (B * 128 * (H // 2) * (W // 2))
     st.alpha = alpha
     st.c4 = c4
-    split = os.environ.get("STX_GRAM_SPLIT", "1") != "0"
-    overlap = os.environ.get("STX_LOSS_STREAM", "0") != "0"  # measured slower (A/B)
+    split = N.knob("STX_GRAM_SPLIT", "1") != "0"
+    overlap = N.knob("STX_LOSS_STREAM", "0") != "0"  # measured slower (A/B)
     main = torch.cuda.current_stream(dev)
     side = _side_stream(dev) if overlap else main
     capturing = False
@@ -280,7 +280,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
             st.grams[l] = torch.empty(B * ops.gram_tile_units(VGG_CONV_SHAPES[l][0]) * nt * 4096,
                                       device=dev, dtype=torch.float32)
 
-    fuse_content = os.environ.get("STX_CONTENT_FUSE", "1") != "0"
+    fuse_content = N.knob("STX_CONTENT_FUSE", "1") != "0"
     # the content tap's Gram in its conv epilogue: the content / feature MSE sums too
     content = None
     if st.grams[CONTENT_CONV] is not None and fuse_content:
@@ -292,7 +292,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
     # finalize launch per tap, right after its partials)
     # (with the loss stream the jobs are recorded on the side stream's calls and the one
     # finalize launch runs on main after the join)
-    fin = ops.FinalizeBatch() if os.environ.get("STX_FIN_BATCH", "1") != "0" else None
+    fin = ops.FinalizeBatch() if N.knob("STX_FIN_BATCH", "1") != "0" else None
 
     def tap_loss(i, l, z, b_, c_, fuse_mse):
         if fuse_mse:  # style loss + content/feature/feature-mse in one pass over z
@@ -344,8 +344,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
                 st.lws[i] = torch.empty(need, device=dev, dtype=torch.uint8)
             njobs = len(fin.jobs) if fin is not None else 0
             tap_loss(i, l, z, b_, c_, fuse_mse)
-            if i in COEF_AMAX_SLOT and fin is not None and len(fin.jobs) == njobs + 1 and \
-                    os.environ.get("STX_P2_SPLIT", "1") != "0":
+            if i in COEF_AMAX_SLOT and fin is not None and len(fin.jobs) == njobs + 1:
                 # the batched finalize also writes max|A| of the taps whose Gram backward
                 # runs inside a data-gradient conv: that phase's split-MFMA A scale
                 st.coef_amax[i] = slot(st.amax, COEF_AMAX_SLOT[i])
@@ -433,7 +432,7 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
     # (STX_COMPOSE=0: the Gram backward of conv3_1 as its own 1x1 pass, dZ5 = A5 Z5; A/B)
     ca = st.coef_amax if st.coef_amax else [None] * 5
     if sp and B == 1 and feat.wtT16[4] is not None and ca[4] is not None and \
-            os.environ.get("STX_COMPOSE", "1") != "0":
+            N.knob("STX_COMPOSE", "1") != "0":
         # conv3_1's output feeds only its style loss, so dP2 = conv3_1^T(A5 Z5) =
         # conv^T_{A5 W}(Z5): A5 folded into the data-gradient weights (one small GEMM
         # launch that writes the split slab), dZ5 never formed.  One operator per image:

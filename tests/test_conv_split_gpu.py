@@ -168,12 +168,15 @@ def test_split_conv_dgrad(dev, case):
 
 
 @pytest.mark.parametrize("case", [(2, 32, 64, 33, 30), (8, 32, 64, 128, 128), (2, 32, 64, 50, 98),
-                                  (8, 32, 64, 256, 256), (4, 64, 128, 128, 128)])
+                                  (8, 32, 64, 256, 256), (4, 64, 128, 128, 128),
+                                  (1, 32, 64, 34, 65), (2, 32, 64, 37, 99)])
 def test_split_conv_dilate(dev, case):
     """stride-2 data gradient as a stride-1 conv over the zero-dilated input: widths > 32
     on the 64 x 4 parity-class tiles (only the taps that meet non-zero dilated positions
     run), incl. ragged tiles and the ImageTransformNet's two shapes at B = 8; narrow
-    widths on the generic tiles."""
+    widths on the generic tiles.  Odd widths > 32 (65, 99): rows whose start is only 4-B
+    aligned, so the epilogue's paired 8-B stores and its 4-B right-edge fallback both run
+    (ADVICE r5)."""
     n, cin, cout, h, w = case
     x = rnd(n, cin, h, w, dev=dev, seed=14).double().cpu().requires_grad_()
     wgt = rnd(cout, cin, 3, 3, dev=dev, seed=15, scale=0.2, shift=-0.1)

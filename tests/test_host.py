@@ -228,6 +228,13 @@ def test_parity_and_gram128_host_contracts():
                 cin_pad=64, cout_pad=64, wt16=48, w_amax=64, in_amax=80)
     p = N.ConvParams(in_mode=N.STX_IN_RAW, hv=32, wv=32, ho=32, wo=32, wt16_up=96, **base)
     assert L.stx_conv2d(C.byref(p), None) == 1001 and b"wt16_up" in L.stx_last_error_string()
+    # the parity-class taps assume the full x2 image: a truncated virtual size (hv < 2h or
+    # wv < 2w, which UPSAMPLE2 otherwise accepts) is refused, not computed with the wrong
+    # border
+    for hv, wv in ((64, 63), (63, 64), (62, 64)):
+        p = N.ConvParams(in_mode=N.STX_IN_UPSAMPLE2, hv=hv, wv=wv, ho=hv, wo=wv, wt16_up=96,
+                         **base)
+        assert L.stx_conv2d(C.byref(p), None) == 1001 and b"wt16_up" in L.stx_last_error_string()
     p = N.ConvParams(in_mode=N.STX_IN_RAW, hv=32, wv=64, ho=32, wo=64, gram_part=112,
                      mse_ref=128, mse_parts=144, **dict(base, w=64))
     assert L.stx_conv2d(C.byref(p), None) == 1001 and b"mse_ref" in L.stx_last_error_string()

@@ -17,8 +17,9 @@ pytestmark = pytest.mark.gpu
 
 def _run(side, dev, H, B, steps=3):
     from styletransfer_amd.train import FastStTrainer
-    old = os.environ.get("STX_WGRAD_SIDE")
+    old = os.environ.get("STX_WGRAD_SIDE"), os.environ.get("STX_AB")
     os.environ["STX_WGRAD_SIDE"] = "1" if side else "0"
+    os.environ["STX_AB"] = "1"  # (a measurement-only switch: N.knob reads it under STX_AB)
     try:
         style = torch.from_numpy(W.synthetic_image(21, (1, 3, H, H))).to(dev)
         batches = [torch.from_numpy(W.synthetic_image(900 + k, (B, 3, H, H))).to(dev)
@@ -32,10 +33,11 @@ def _run(side, dev, H, B, steps=3):
         torch.cuda.synchronize()
         return tr.flat.detach().cpu().clone(), tr.flat_grad.detach().cpu().clone(), losses
     finally:
-        if old is None:
-            os.environ.pop("STX_WGRAD_SIDE", None)
-        else:
-            os.environ["STX_WGRAD_SIDE"] = old
+        for k, v in zip(("STX_WGRAD_SIDE", "STX_AB"), old):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 @pytest.mark.parametrize("H,B", [(64, 2), (256, 8)])

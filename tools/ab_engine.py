@@ -33,7 +33,8 @@ def ev(fn, reps):
 
 class Env:
     def __init__(self, spec):
-        self.kv = dict(x.split("=", 1) for x in spec.split(",") if x)
+        # STX_AB=1: the host path's A/B switches read the environment only then (N.knob)
+        self.kv = dict([("STX_AB", "1")] + [x.split("=", 1) for x in spec.split(",") if x])
         self.old = {}
 
     def __enter__(self):

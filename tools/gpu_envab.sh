@@ -1,5 +1,6 @@
 # environment A/B on one box (separate processes, alternating): bench.py Gatys + fast_st legs
 # with VAR=a vs VAR=b, after the given tests.   gpurun -- 'bash tools/gpu_envab.sh <tag> VAR a b "<tests>"'
+export STX_AB=1  # (the host path reads its A/B switches only under STX_AB=1: N.knob)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 tag=$1; var=$2; va=$3; vb=$4; T=${5:-}
 if [ -n "$T" ]; then

@@ -1,6 +1,7 @@
 # rocprofv3 kernel traces of the Gatys leg under VAR=a and VAR=b, per-iteration breakdowns
 #   gpurun -- 'bash tools/gpu_prof_env.sh <tag> VAR a b'
 cd /tmp && export TMPDIR=/tmp
+export STX_AB=1  # (the host path reads its A/B switches only under STX_AB=1: N.knob)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 tag=$1; var=$2
 for v in $3 $4; do

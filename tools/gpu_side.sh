@@ -1,5 +1,6 @@
 # weight-gradient side stream: the trainer tests, then the same-process A/B of the fast_st step
 set -o pipefail
+export STX_AB=1  # (the host path reads its A/B switches only under STX_AB=1: N.knob)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 tag=${1:-side}
 timeout -k 10 500 python -u -m pytest tests/test_side_stream_gpu.py tests/test_conv9_gpu.py tests/test_itn_masks_gpu.py tests/test_dp_gpu.py tests/test_video_gpu.py tests/test_parity_gpu.py tests/test_workflows_gpu.py -x -q -rf --timeout 120 --timeout-method thread > gpurun_out/${tag}_t.log 2>&1

@@ -3,6 +3,7 @@
 #   gpurun -- 'bash tools/prof_iter.sh tag "STX_COMPOSE=0" "STX_COMPOSE=1"'
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
+export STX_AB=1  # (the host path reads its A/B switches only under STX_AB=1: N.knob)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 tag=$1; shift
 i=0

@@ -3,6 +3,7 @@
 #   gpurun -- 'bash tools/prof_libs.sh <tag> fast|gatys'
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
+export STX_AB=1  # (the host path reads its A/B switches only under STX_AB=1: N.knob)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 tag=$1; leg=${2:-fast}
 if [ "$leg" = fast ]; then ARGS="--fast-only --steps 20 --warmup 2"; else ARGS="--steps 30 --warmup 3 --skip-cpu --skip-fast --skip-infer --lbfgs-steps 0 --gatys-run-iters 0"; fi
