@@ -501,7 +501,18 @@ def case_gatys512(N, H=512, iters=3):
         x64.append(O.to_np(x).copy())
     c0 = content.numpy().astype(np.float64)
     nproj = lambda a: np.concatenate([[np.linalg.norm(a)], proj32(a)])  # noqa: E731
+    # flip-aware form of the image after 3 steps (Adam steps ~lr*sign(g): a pixel whose |g|
+    # is at rounding level steps either way in any fp32 run): the fp64 run's update in full,
+    # and the fp32 reference's own flip fraction (|du - du64| > lr / 2) and relative error
+    # on its non-flipped pixels -- the bar a HIP run is held to
+    lr = 1e-3
+    u64, ur = x64[2] - c0, xs[2].astype(np.float64) - c0
+    rflip = np.abs(ur - u64) > 0.5 * lr
+    keep = ~rflip
+    ref_keep_rel = float(np.linalg.norm(ur[keep] - u64[keep]) / np.linalg.norm(u64[keep]))
     return {"size": np.array(H), "style_seed": np.array(1000), "content_seed": np.array(2000),
+            "upd3_64": u64.astype(np.float32), "upd3_ref_flip_frac": np.array(rflip.mean()),
+            "upd3_ref_keep_rel": np.array(ref_keep_rel),
             "losses": tot, "losses_it1": per,
             "dx1_proj": nproj(grads[0]), "dx3_proj": nproj(grads[2]),
             "upd3_proj": nproj(xs[2] - c0),

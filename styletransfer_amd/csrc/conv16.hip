@@ -785,6 +785,23 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   auto st_halo = [&](int buf, int r) {
     const int idx = tid + r * NT;
     if (r + 1 < C::NIT || C::NITEM % NT == 0 || idx < C::NITEM) {
+      char* hb = smem + buf * C::HB;
+#ifdef STX_DIAG_NOSPLIT
+      // timing-only diagnostic build (make DIAG=1, numerically meaningless): the loader's
+      // values stored as raw fp32 bits in the two planes -- no scale, no fp16 conversion
+      f32x4 a, b;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        a[c] = hv[r][c];
+        b[c] = hv[r][c + 4];
+        if (LM == STX_IN_RELU || LM == STX_IN_RELU_POOL2) {
+          a[c] = fmaxf(a[c], 0.f);
+          b[c] = fmaxf(b[c], 0.f);
+        }
+      }
+      *reinterpret_cast<f32x4*>(hb + idx * 16) = a;
+      *reinterpret_cast<f32x4*>(hb + (C::NITEM + idx) * 16) = b;
+#else
       f16x8 hi, lo;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -795,9 +812,9 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
         hi[c] = vh;
         lo[c] = (_Float16)(v - (float)vh);
       }
-      char* hb = smem + buf * C::HB;
       *reinterpret_cast<f16x8*>(hb + idx * 16) = hi;
       *reinterpret_cast<f16x8*>(hb + (C::NITEM + idx) * 16) = lo;
+#endif
     }
   };
   auto ld_w = [&](int step) {  // step = chunk * KS + kh (UPP: ry)

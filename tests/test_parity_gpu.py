@@ -192,8 +192,9 @@ def test_gatys_config2_512_engine_golden(dev):
     the first update ~lr*sign(g) agrees in sign except on a negligible fraction of
     pixels (|g| ~ rounding).  At this size the fp32 reference's image gradient is itself
     ~1.1e-3 from the fp64 run's (elements within rounding of a ReLU / argmax kink), so
-    gradients and the image after 3 steps are compared three-way: HIP's distance from
-    the fp64 run <= 2.5x the fp32 reference's (32 projections + norm)."""
+    gradients are compared three-way: HIP's distance from the fp64 run <= 2.5x (4x after
+    two steps) the fp32 reference's (32 projections + norm); the image after 3 steps
+    pixel by pixel, its sign-flipped pixels bounded separately (flip-aware)."""
     d = g("gatys512")
     H = int(d["size"])
     style = T(W.synthetic_image(int(d["style_seed"]), (1, 3, H, H)), dev)
@@ -218,13 +219,25 @@ def test_gatys_config2_512_engine_golden(dev):
     errs = {}
     # iteration 1's gradient: 2.5x; after two Adam steps (~lr*sign(g) per pixel, so a pixel
     # whose |g| is at rounding level steps either way in any fp32 run) the trajectories of
-    # fp32 runs fan out from the fp64 one by their own sign flips: the gradient 4x, the
-    # image (whole +-lr steps on those pixels; measured 4.9x) 6x.  The loss trajectory
-    # above is held to 1e-4.
-    for k, v, f in (("dx1", dx1, 2.5), ("dx3", dx3, 4.0), ("upd3", x3 - c0, 6.0)):
+    # fp32 runs fan out from the fp64 one by their own sign flips: the gradient 4x.  The
+    # loss trajectory above is held to 1e-4.
+    for k, v, f in (("dx1", dx1, 2.5), ("dx3", dx3, 4.0)):
         e, r = rel(nproj(v), d[f"{k}_proj_64"]), rel(d[f"{k}_proj"], d[f"{k}_proj_64"])
         errs[k] = (e, r)
         assert e <= max(f * r, 1e-5), (k, e, r)
+    # the image after 3 steps, flip-aware against the fp64 run's full update: pixels that
+    # stepped the other way (|du - du64| > lr / 2: a whole +-lr step where |g| is at rounding
+    # level) are counted and bounded on their own; every other pixel's update is held to
+    # 2.5x the fp32 reference's own error on its non-flipped pixels (gatys512.npz)
+    lr = 1e-3
+    u, u64 = x3 - c0, d["upd3_64"].astype(np.float64)
+    flip = np.abs(u - u64) > 0.5 * lr
+    keep_rel = rel(u[~flip], u64[~flip])
+    ref_flip, ref_keep = float(d["upd3_ref_flip_frac"]), float(d["upd3_ref_keep_rel"])
+    errs["upd3"] = dict(flip_frac=float(flip.mean()), ref_flip_frac=ref_flip,
+                        keep_rel=keep_rel, ref_keep_rel=ref_keep)
+    assert flip.mean() <= 1e-4, errs["upd3"]
+    assert keep_rel <= 2.5 * ref_keep, errs["upd3"]
     s_hip = (x1 - c0).ravel() > 0
     s_ref = np.unpackbits(d["upd1_sign"])[:s_hip.size].astype(bool)
     flips = float(np.mean(s_hip != s_ref))

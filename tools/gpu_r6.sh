@@ -38,11 +38,12 @@ if [ -n "${AB:-}" ]; then
   tail -12 gpurun_out/${tag}_ab.log
 fi
 if [ -n "${MICRO:-}" ]; then
-  # MICRO_AB=1: the same script under libstx_prev.so as well (same box)
-  for v in new ${MICRO_AB:+prev}; do
-    L=$PWD/styletransfer_amd/libstx.so; [ $v = prev ] && L=$PWD/styletransfer_amd/libstx_prev.so
+  # MICRO_AB=1: the same script under libstx_prev.so as well (same box); MICRO_LIBS: the
+  # library variants to run it under (default libstx.so [libstx_prev.so])
+  for v in ${MICRO_LIBS:-libstx.so ${MICRO_AB:+libstx_prev.so}}; do
+    L=$PWD/styletransfer_amd/$v
     echo "== micro $MICRO ($v)"
-    STX_LIB_PARTIAL=1 STX_LIB=$L timeout -k 10 300 python $MICRO > gpurun_out/${tag}_micro_$v.log 2>&1 || { tail -20 gpurun_out/${tag}_micro_$v.log; exit 1; }
+    STX_LIB_PARTIAL=1 STX_LIB=$L timeout -k 10 300 python $MICRO ${MICRO_ARGS:-} > gpurun_out/${tag}_micro_$v.log 2>&1 || { tail -20 gpurun_out/${tag}_micro_$v.log; exit 1; }
     tail -40 gpurun_out/${tag}_micro_$v.log
   done
 fi
