@@ -78,7 +78,7 @@ def main():
         nt = ops.conv_gram_tiles(cin, cout, ho, wo) if s == 1 and mode in (
             N.STX_IN_RAW, N.STX_IN_RELU) else 0
         if nt and not args.no_split and (cin == 3 or ops.split_eligible(cin, cout, ks, s)):
-            gp = torch.empty(n * nt * 4096, device=dev)
+            gp = torch.empty(n * ops.gram_tile_units(cout) * nt * 4096, device=dev)
             kw16 = {}
             if cin != 3:
                 kw16 = dict(wt16=ops.conv_weight_prep16(wraw), in_amax=ops.amax(x))
