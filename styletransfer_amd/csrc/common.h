@@ -51,6 +51,22 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // one per-chunk descriptor and mark padding/out-of-tile elements with BUF_OOB, so
 // the fetch is straight-line code (no per-element exec branches, no serialising
 // vmcnt(0) per load) and channel padding past the tensor end reads as zero.
+// ReLU on the IEEE bit pattern: max(bits, 0) as signed ints keeps every non-negative float
+// and maps every negative one (sign bit set) to +0 -- one v_max_i32, where fmaxf(x, 0.f)
+// of a loaded x is two v_max_f32 (operand canonicalisation first)
+__device__ __forceinline__ float relu_bits(float x) {
+  return __int_as_float(max(__float_as_int(x), 0));
+}
+// relu(max of a 2x2 window) = the integer max of the four bit patterns and 0 (non-negative
+// floats order like their bits; a negative float loses to 0 either way): two v_max3_i32.
+// Exactly relu_bits(max_pool(x)); the bare int max of four floats is NOT their float max
+// when all are negative, which is why the 0 is part of it.
+__device__ __forceinline__ float pool4_bits(float a, float b, float c, float d) {
+  const int m = max(max(__float_as_int(a), __float_as_int(b)),
+                    max(max(__float_as_int(c), __float_as_int(d)), 0));
+  return __int_as_float(m);
+}
+
 constexpr uint32_t BUF_OOB = 0x80000000u;  // callers keep byte counts below this
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const float* base, uint32_t bytes) {

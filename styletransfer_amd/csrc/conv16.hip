@@ -456,8 +456,8 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
       for (int c = 0; c < 8; ++c) {
         const uint32_t o = hoff[r] + (uint32_t)c * pb;
         if (LM == STX_IN_RELU_POOL2)
-          hv[r][c] = fmaxf(fmaxf(buf_ld(rs, o), buf_ld(rs, o + 4)),
-                           fmaxf(buf_ld(rs, o + wb), buf_ld(rs, o + wb + 4)));
+          hv[r][c] = pool4_bits(buf_ld(rs, o), buf_ld(rs, o + 4), buf_ld(rs, o + wb),
+                                buf_ld(rs, o + wb + 4));
         else
           hv[r][c] = buf_ld(rs, o);
       }
@@ -473,7 +473,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         float v = hv[r][c];
-        if (LM == STX_IN_RELU || LM == STX_IN_RELU_POOL2) v = fmaxf(v, 0.f);
+        if (LM == STX_IN_RELU) v = relu_bits(v);  // (POOL2: pool4_bits applied the ReLU)
         v *= sx;
         const _Float16 vh = (_Float16)v;
         hi[c] = vh;
@@ -776,8 +776,8 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     for (int c = 0; c < 8; ++c) {
       const uint32_t o = hoff[r] + (uint32_t)c * pb;
       if (LM == STX_IN_RELU_POOL2)
-        hv[r][c] = fmaxf(fmaxf(buf_ld(rs, o), buf_ld(rs, o + 4)),
-                         fmaxf(buf_ld(rs, o + wrow), buf_ld(rs, o + wrow + 4)));
+        hv[r][c] = pool4_bits(buf_ld(rs, o), buf_ld(rs, o + 4), buf_ld(rs, o + wrow),
+                              buf_ld(rs, o + wrow + 4));
       else
         hv[r][c] = buf_ld(rs, o);
     }
@@ -805,8 +805,11 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
       f16x8 hi, lo;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
+        // ReLU as an integer max of the bit pattern (negative floats are negative ints):
+        // one v_max_i32 -- fmaxf of a loaded value costs two v_max_f32 (the first
+        // canonicalises the operand)
         float v = hv[r][c];
-        if (LM == STX_IN_RELU || LM == STX_IN_RELU_POOL2) v = fmaxf(v, 0.f);
+        if (LM == STX_IN_RELU) v = relu_bits(v);  // (POOL2: pool4_bits applied the ReLU)
         v *= sx;
         const _Float16 vh = (_Float16)v;
         hi[c] = vh;

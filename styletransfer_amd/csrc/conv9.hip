@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(64 * W, 8 / W) conv9_in3_kernel(stx_conv_param
     for (int k = 0; k < NB_R; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        if (relu_in) bv[k][e] = fmaxf(bv[k][e], 0.f);
+        if (relu_in) bv[k][e] = relu_bits(bv[k][e]);
         mx = fmaxf(mx, fabsf(bv[k][e]));
       }
     const int ex = exp_of(block_max<W>(mx, red));
@@ -394,7 +394,7 @@ __global__ void __launch_bounds__(NT, 1) conv9_out3_kernel(stx_conv_params p, in
     for (int k = 0; k < NB_R; ++k) {
       if (relu_in)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) hs[k][e] = fmaxf(hs[k][e], 0.f);
+        for (int e = 0; e < 8; ++e) hs[k][e] = relu_bits(hs[k][e]);
       f16x8 hi, lo;
       split8(hs[k], sx, hi, lo);
       const int i = tid + NT * k;

@@ -698,7 +698,7 @@ __global__ void __launch_bounds__(256, 2) conv_fewout3_kernel(stx_conv_params p,
     for (int s = 0; s < NST; ++s) {
       const float v = __builtin_bit_cast(
           float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, (uint32_t)(2 * s) * plane_in * 4u, 0));
-      buf[s] = relu_in ? fmaxf(v, 0.f) : v;
+      buf[s] = relu_in ? relu_bits(v) : v;
     }
   };
   auto run_item = [&](int item, const float (&buf)[NST]) {
@@ -825,7 +825,7 @@ __global__ void __launch_bounds__(256, 2) conv_fewout16_kernel(stx_conv_params p
       for (int e = 0; e < 8; ++e) {
         const float v = __builtin_bit_cast(
             float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, (uint32_t)(16 * t + e) * plane_in * 4u, 0));
-        buf[t][e] = relu_in ? fmaxf(v, 0.f) : v;
+        buf[t][e] = relu_in ? relu_bits(v) : v;
       }
   };
   auto run_item = [&](int item, const float (&buf)[KST][8]) {

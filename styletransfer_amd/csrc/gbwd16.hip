@@ -182,8 +182,8 @@ gram_bwd16_v1_kernel(Gb16 p) {
             zb = lrow ? zo : zv;
           }
           const float pa = swap_pair(za), pb = swap_pair(zb);
-          const float z0 = fmaxf(par ? pa : za, 0.f), z1 = fmaxf(par ? za : pa, 0.f);
-          const float z2 = fmaxf(par ? pb : zb, 0.f), z3 = fmaxf(par ? zb : pb, 0.f);
+          const float z0 = relu_bits(par ? pa : za), z1 = relu_bits(par ? za : pa);
+          const float z2 = relu_bits(par ? pb : zb), z3 = relu_bits(par ? zb : pb);
           int bi = 0;
           float best = z0;
           if (z1 > best) { best = z1; bi = 1; }
@@ -438,8 +438,8 @@ gram_bwd16_kernel(Gb16 p) {
             zb = lrow ? zo : zv;
           }
           const float pa = swap_pair(za), pb = swap_pair(zb);
-          const float z0 = fmaxf(par ? pa : za, 0.f), z1 = fmaxf(par ? za : pa, 0.f);
-          const float z2 = fmaxf(par ? pb : zb, 0.f), z3 = fmaxf(par ? zb : pb, 0.f);
+          const float z0 = relu_bits(par ? pa : za), z1 = relu_bits(par ? za : pa);
+          const float z2 = relu_bits(par ? pb : zb), z3 = relu_bits(par ? zb : pb);
           int bi = 0;
           float best = z0;
           if (z1 > best) { best = z1; bi = 1; }

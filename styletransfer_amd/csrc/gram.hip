@@ -491,7 +491,7 @@ gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw,
         hi[k] = (_Float16)v;
         lo[k] = (_Float16)(v - (float)hi[k]);
         if constexpr (MSE) {  // out-of-range pixels read 0 on both sides: no contribution
-          const float d = ld[r][k] - lc[r][k], dr = fmaxf(ld[r][k], 0.f) - fmaxf(lc[r][k], 0.f);
+          const float d = ld[r][k] - lc[r][k], dr = relu_bits(ld[r][k]) - relu_bits(lc[r][k]);
           ms += d * d;
           msr += dr * dr;
         }

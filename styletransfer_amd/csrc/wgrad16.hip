@@ -265,8 +265,8 @@ wgrad16_kernel(const float* __restrict__ x, const float* __restrict__ dy, float*
       for (int q = 0; q < 5; ++q) {
         f2 v = {bv[2 * q], bv[2 * q + 1]};
         if (relu) {
-          v.x = fmaxf(v.x, 0.f);
-          v.y = fmaxf(v.y, 0.f);
+          v.x = relu_bits(v.x);
+          v.y = relu_bits(v.y);
         }
         split2(v * sv2, ph[q], pl[q]);
       }

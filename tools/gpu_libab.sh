@@ -8,7 +8,7 @@ if [ -n "$T" ]; then
   rc=$?; echo "T rc=$rc"; tail -1 gpurun_out/${tag}_t.log; grep -E "^(FAILED|ERROR)|^E  " gpurun_out/${tag}_t.log | head -10
   [ $rc -eq 0 ] || exit $rc
 fi
-for i in 1 2; do
+for i in ${ROUNDS:-1 2}; do
   for v in new prev ${EXTRA_VARIANT:-}; do
     if [ $v = prev ]; then L=$PWD/styletransfer_amd/libstx_prev.so; else L=$PWD/styletransfer_amd/libstx.so; fi; if [ $v = ppb2 ]; then export STX_IN_PPB=2; else unset STX_IN_PPB; fi
     STX_LIB=$L timeout -k 10 200 python bench.py --steps 50 --warmup 5 --skip-cpu --skip-infer --lbfgs-steps 0 --gatys-run-iters 0 --fast-b64-steps 0 > gpurun_out/${tag}_$v$i.json 2>gpurun_out/${tag}_$v$i.err || { tail -3 gpurun_out/${tag}_$v$i.err; exit 1; }
