@@ -60,12 +60,12 @@ PEAK_HBM_GBS = 8000.0
 
 # the roofline kernel instance and its per-launch HBM traffic (rocprofv3 FETCH_SIZE /
 # WRITE_SIZE passes of tools/pmc_r3.sh over an eager Gatys iteration, calibrated on
-# kernels of known byte count: tools/pmc_r3_summary.py -> profiles/r5_pmc.json, the
+# kernels of known byte count: tools/pmc_r3_summary.py -> profiles/r6_pmc.json, the
 # passes over the current build)
 DG_KERNEL = "conv3x3_f16x3_v2_kernel<64, 0, {}, 2, 1>"
 ROOFLINE_KERNEL = "conv3x3_f16x3_v2_kernel<64, 1, 0, 2, 1>"
 ROOFLINE_MATCH = ROOFLINE_KERNEL
-PMC_FILE = os.path.join(REPO, "profiles", "r5_pmc.json")
+PMC_FILE = os.path.join(REPO, "profiles", "r6_pmc.json")
 # algorithmic bytes of conv1_2 fwd @512^2 as the iteration launches it: Z1 in, Z2 and the
 # fused relu+pool output P2 out, weights + bias, and the fused Gram partials (1024 tiles
 # x 64 x 64 fp32)
