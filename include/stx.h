@@ -160,6 +160,11 @@ int stx_version(void);
  * their struct mirrors against it. */
 int stx_abi_layout(long long* out, int n);
 const char* stx_last_error_string(void);
+/* The ABI revision of this header (STX_ABI_VERSION): a host binding refuses a library of
+ * another revision rather than pass arguments whose meaning changed (round 6:
+ * stx_instnorm_bwd's second argument is beta, not y). */
+#define STX_ABI_VERSION 6
+int stx_abi_version(void);
 
 /* Padded GEMM dims the conv kernels expect for a (cin, cout, ks) conv. */
 int stx_conv_weight_dims(int cin, int cout, int ks, int* cin_pad, int* cout_pad);
@@ -488,14 +493,17 @@ int stx_adam_step_clear(float* p, const float* g, float* m, float* v, long long 
                         float* clear, int clear_n, void* stream);
 
 /* InstanceNorm2d(affine) forward, per (n,c) plane over hw (biased var, eps):
- *   u = x (+ res);  y = (u-mean)*rstd*gamma + beta;  y = max(y,0) if relu.
+ *   u = x (+ res);  y = (u-mean)*rstd*gamma + beta, formed as fma(u, gsc, sh) with
+ *   gsc = gamma rstd, sh = fma(-mean, gsc, beta);  y = max(y,0) if relu.
  * mean/rstd [n*c] saved for the backward (may be NULL).  out_amax (amax group, zeroed
  * by the caller, may be NULL) receives max|y| -- the next split conv's input scale. */
 int stx_instnorm_fwd(const float* x, const float* res, const float* gamma, const float* beta,
                      float* y, float* mean, float* rstd, int n, int c, int hw, float eps,
                      int relu, float* out_amax, void* stream);
-/* backward: dy = grad wrt y; y needed when relu (mask).  du = grad wrt u (= grad of x
- * and of res).  dgamma/dbeta (may be NULL) (+)= sums over n (fixed order).  dbias_in
+/* backward: dy = grad wrt y; beta = the forward's beta (NULL if none).  With relu the
+ * mask y > 0 is recomputed from u = x (+ res), mean, rstd, gamma and beta exactly as the
+ * forward formed y (y = fma(u, gsc, sh), gsc = gamma rstd, sh = fma(-mean, gsc, beta):
+ * the same bits), so y itself is not read.  du = grad wrt u (= grad of x and of res).  dgamma/dbeta (may be NULL) (+)= sums over n (fixed order).  dbias_in
  * (may be NULL) (+)= sum_{n,p} du: the bias gradient of the conv that produced x
  * (stransfer/network.py:471-611, every Conv2d followed by InstanceNorm2d), so that
  * conv needs no separate bias-gradient pass.  out_amax (amax group or NULL) receives
@@ -516,7 +524,7 @@ typedef struct stx_in_pgrad_job {
   int n, c, accumulate, pad_;
 } stx_in_pgrad_job;
 int stx_instnorm_param_grads(const stx_in_pgrad_job* jobs, int njobs, void* stream);
-int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
+int stx_instnorm_bwd(const float* dy, const float* beta, const float* x, const float* res,
                      const float* gamma, const float* mean, const float* rstd, float* du,
                      float* dgamma, float* dbeta, float* dbias_in, int n, int c, int hw, int relu,
                      int accumulate_params, float* out_amax, void* ws, size_t ws_bytes,

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("STX_LIB", os.path.join(_HERE, "libstx.so"))
 STX_IN_RAW, STX_IN_RELU, STX_IN_RELU_POOL2, STX_IN_UPSAMPLE2, STX_IN_DILATE2 = range(5)
 STX_AMAX_SLOTS = 32  # an "amax" is a group of 32 floats whose max is the value (stx.h)
 STX_GRAM_GROUP = 8  # fused Gram partials per in-kernel group sum (stx_conv_params.gram_cnt)
+STX_ABI_VERSION = 6  # include/stx.h: the library must report the same revision
 
 
 def knob(name: str, default: str) -> str:
@@ -99,6 +100,7 @@ SIGNATURES = {
     "stx_version": (i32, []),
     "stx_abi_layout": (i32, [vp, i32]),
     "stx_last_error_string": (C.c_char_p, []),
+    "stx_abi_version": (i32, []),
     "stx_conv_weight_dims": (i32, [i32, i32, i32, C.POINTER(i32), C.POINTER(i32)]),
     "stx_conv_weight_prep": (i32, [vp, vp, i32, i32, i32, i32, vp]),
     "stx_conv2d": (i32, [C.POINTER(ConvParams), vp]),
@@ -212,8 +214,15 @@ def lib():
                 L = C.CDLL(LIB_PATH)
             except OSError as e:  # pragma: no cover
                 raise NativeError(f"failed to load {LIB_PATH}: {e}") from e
-            # STX_LIB_PARTIAL=1: an older library build for same-box A/B timing
-            # (tools/ab_conv.sh) may lack newer entry points
+            # the ABI revision must match, whatever else: an older library whose entry
+            # points read an argument differently would be driven out of bounds (a
+            # round-5 libstx_prev.so read stx_instnorm_bwd's beta as a whole y plane)
+            abi = L.stx_abi_version() if hasattr(L, "stx_abi_version") else None
+            if abi != STX_ABI_VERSION:
+                raise NativeError(f"{LIB_PATH}: ABI revision {abi}, this binding needs "
+                                  f"{STX_ABI_VERSION} (include/stx.h STX_ABI_VERSION)")
+            # STX_LIB_PARTIAL=1: an older build of the same ABI revision for same-box A/B
+            # timing may lack newer entry points
             partial = os.environ.get("STX_LIB_PARTIAL") == "1"
             for name, (res, args) in SIGNATURES.items():
                 if partial and not hasattr(L, name):

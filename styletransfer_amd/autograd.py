@@ -260,7 +260,7 @@ class InstanceNormFn(torch.autograd.Function):
                                          None if beta is None else beta.detach(), res=res,
                                          eps=eps, relu=relu, out_amax=g)
         ops.ARENA.annotate(y, g)
-        ctx.save_for_backward(x, res, gamma, y, mean, rstd)
+        ctx.save_for_backward(x, res, gamma, mean, rstd)  # (the ReLU mask is recomputed)
         ctx.beta_ref = beta
         ctx.cb_ref = conv_bias
         ctx.relu = relu
@@ -270,7 +270,7 @@ class InstanceNormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, res, gamma, y, mean, rstd = ctx.saved_tensors
+        x, res, gamma, mean, rstd = ctx.saved_tensors
         c = x.shape[1]
         cb = ctx.cb_ref if ctx.needs_input_grad[6] else None
         params = (gamma, ctx.beta_ref if gamma is not None else None, cb)
@@ -280,7 +280,9 @@ class InstanceNormFn(torch.autograd.Function):
         bufs = [None if p is None else (p.grad if acc else torch.empty(c, device=x.device))
                 for p in params]
         ga = ops.ARENA.take(x.device)
-        du = ops.instnorm_bwd(_c(dy), y, x, res, None if gamma is None else gamma.detach(),
+        beta = ctx.beta_ref
+        du = ops.instnorm_bwd(_c(dy), None if beta is None else beta.detach(), x, res,
+                              None if gamma is None else gamma.detach(),
                               mean, rstd, relu=ctx.relu, dgamma=bufs[0], dbeta=bufs[1],
                               dbias_in=bufs[2], accumulate=acc, out_amax=ga)
         ops.ARENA.annotate(du, ga)

@@ -30,6 +30,7 @@ int check_launch(const char* what) {
 
 extern "C" int stx_version(void) { return 1; }
 extern "C" const char* stx_last_error_string(void) { return stx::g_err; }
+extern "C" int stx_abi_version(void) { return STX_ABI_VERSION; }
 
 // sizeof and the offset of the last member of each ABI struct (include/stx.h order), for
 // bindings to check their struct mirrors against: a member added on one side only moves

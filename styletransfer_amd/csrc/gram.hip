@@ -549,6 +549,206 @@ gram_tri_f16_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw,
   }
 }
 
+// C = 256 (VGG conv3_1's tap): the whole upper triangle of G per block, on 8 waves.  A
+// block takes one image's pixel range and ALL 36 upper-triangle 32 x 32 blocks (row panels
+// w and 7 - w to waves 2 (w % 4) .. +1, four or five blocks each, so a wave's blocks share
+// their A fragments), z read once from HBM and split once into fp16 hi/lo.  Per chunk of
+// 32 pixels the 256 x 32 slab goes to LDS as 16-B fragment units (8 pixels of one channel)
+// at unit c * 4 + (g ^ ((c >> 2) & 3)) (g = 8-pixel group): the swizzle keeps both the
+// staging stores (4 lanes per channel) and the fragment reads (32 lanes over 32
+// channels) conflict-free.  Double-buffered chunks, one barrier per chunk, the next
+// chunk's loads in flight during the MFMAs.  The 64 x 64-tile kernel it replaces read
+// every 64-row panel (nt + 1) / 2 times and split it once per tile (640 blocks, 19 us at
+// 128^2); the 4-wave triangle kernel (1 wave per SIMD, 9 accumulator blocks per wave)
+// was slower still.  Partials: the 64 x 64-tile layout gram_finalize reads.
+constexpr int T256_PX = 32;  // pixels per chunk
+template <bool STAGED>
+__global__ void __launch_bounds__(512, 1)
+gram_tri256_kernel(const float* __restrict__ z, float* __restrict__ ws, int hw, int nsplit,
+                   int split_len, const float* __restrict__ z_amax) {
+  constexpr int C = 256, NB = 8, NT = C / GT, NTU = NT * (NT + 1) / 2;
+  constexpr int UNITS = C * T256_PX / 8;       // 16-B units per plane per chunk (1024)
+  constexpr int PLANE = UNITS * 16;            // bytes (16 KB)
+  constexpr int BUF = 2 * PLANE;               // hi + lo
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int split = blockIdx.x, b = blockIdx.z;
+  const int p0 = split * split_len, p1 = min(hw, p0 + split_len);
+  const auto rz = make_srd(z + (size_t)b * C * hw, (uint32_t)C * (uint32_t)hw * 4u);
+  const int e = gram_amax_exp(read_amax(z_amax));
+  const float sx = __builtin_ldexpf(1.f, 15 - e), inv2 = __builtin_ldexpf(1.f, 2 * e - 30);
+  // this wave's blocks: the 9 blocks of row panels (w, 7 - w), w = wave / 2, in order
+  // (panel w: bj = w .. 7, then panel 7 - w: bj = 7 - w .. 7); the even wave takes the
+  // first five, the odd wave the other four
+  constexpr int PER = 5;
+  int bi[PER], bj[PER];
+  bool uA[PER];  // block q's A panel is 7 - pw (else pw)
+  const int pw = wave >> 1, first = (wave & 1) ? 5 : 0, cnt = (wave & 1) ? 4 : 5;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    int t = min(first + q, first + cnt - 1);  // (slot past cnt: a copy, not stored)
+    const int n0 = NB - pw;                   // blocks in panel pw
+    uA[q] = t >= n0;
+    if (t < n0) {
+      bi[q] = pw;
+      bj[q] = pw + t;
+    } else {
+      bi[q] = NB - 1 - pw;
+      bj[q] = NB - 1 - pw + (t - n0);
+    }
+  }
+  f32x16 acc[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+  // staging: unit u = tid + 512 r (r = 0, 1) -> channel u >> 2, 8-pixel group u & 3
+  f32x4 ld[2][2];
+  uint32_t ch_off[2];
+  int slot[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int u = tid + 512 * r, c = u >> 2, g = u & 3;
+    ch_off[r] = (uint32_t)(c * hw + 8 * g) * 4u;
+    slot[r] = (c * 4 + (g ^ ((c >> 2) & 3))) * 16;
+  }
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int g = (tid + 512 * r) & 3;
+      const uint32_t o = c0 + 8 * g < p1 ? ch_off[r] + (uint32_t)c0 * 4u : BUF_OOB;
+      ld[r][0] = buf_ld4(rz, o);
+      ld[r][1] = buf_ld4(rz, o + 16u);
+    }
+  };
+  auto stage = [&](int buf) {
+    char* base = lds + buf * BUF;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      f16x8_t hi, lo;
+      split8(ld[r][0], ld[r][1], sx, hi, lo);
+      *reinterpret_cast<f16x8_t*>(base + slot[r]) = hi;
+      *reinterpret_cast<f16x8_t*>(base + PLANE + slot[r]) = lo;
+    }
+  };
+  // fragment unit of (block row panel, k-step s) for this lane: channel 32 panel + l32,
+  // group 2 s + h
+  auto frag_off = [&](int panel, int s) {
+    const int c = 32 * panel + l32, g = 2 * s + h;
+    return (c * 4 + (g ^ ((c >> 2) & 3))) * 16;
+  };
+  int buf = 0;
+  if (p0 < p1) {
+    fetch(p0);
+    stage(0);
+    if (p0 + T256_PX < p1) fetch(p0 + T256_PX);
+  }
+  for (int c0 = p0; c0 < p1; c0 += T256_PX, buf ^= 1) {
+    __syncthreads();  // buffer buf complete; the other buffer's reads (chunk c0 - 32) done
+    const char* base = lds + buf * BUF;
+    // per k-step every fragment first (A panels pw and 7 - pw -- uA[q]: which one block q
+    // uses, wave-uniform -- and one B panel per block; a diagonal block reads its A panel
+    // again), then the step's MFMAs
+#pragma unroll
+    for (int st = 0; st < T256_PX / 16; ++st) {
+      f16x8_t fa[2][2], fb[PER][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int oa = frag_off(a ? NB - 1 - pw : pw, st);
+        fa[a][0] = *reinterpret_cast<const f16x8_t*>(base + oa);
+        fa[a][1] = *reinterpret_cast<const f16x8_t*>(base + PLANE + oa);
+      }
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        if (q >= cnt) break;
+        const int ob = frag_off(bj[q], st);
+        fb[q][0] = *reinterpret_cast<const f16x8_t*>(base + ob);
+        fb[q][1] = *reinterpret_cast<const f16x8_t*>(base + PLANE + ob);
+      }
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        if (q >= cnt) break;
+        const int a = uA[q] ? 1 : 0;
+        if (a) {
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1][0], fb[q][0], acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1][0], fb[q][1], acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[1][1], fb[q][0], acc[q], 0, 0, 0);
+        } else {
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0][0], fb[q][0], acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0][0], fb[q][1], acc[q], 0, 0, 0);
+          acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[0][1], fb[q][0], acc[q], 0, 0, 0);
+        }
+      }
+    }
+    if (c0 + T256_PX < p1) {  // the next chunk -> the other buffer, its successor's loads
+      stage(buf ^ 1);
+      if (c0 + 2 * T256_PX < p1) fetch(c0 + 2 * T256_PX);
+    }
+  }
+  // partials in the 64 x 64-tile layout [b][tile][split][64][64] (diagonal tiles with the
+  // mirrored lower-left quadrant)
+  if constexpr (STAGED) {
+    // each wave's 32 x 32 block through its own LDS region (pitch 40 floats: the two lane
+    // halves' rows land 32 banks apart), then 16-B stores: 8 rows x 128 B per store
+    // instruction instead of 2 x 128 B
+    constexpr int PITCH = 40;
+    float* reg = reinterpret_cast<float*>(lds) + wave * 32 * PITCH;
+    __syncthreads();  // the last chunk's fragment reads are done
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      if (q >= cnt) break;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        reg[((r & 3) + 8 * (r >> 2) + 4 * h) * PITCH + l32] = acc[q][r] * inv2;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS stores landed
+      const int I = bi[q] >> 1, J = bj[q] >> 1, qi = bi[q] & 1, qj = bj[q] & 1;
+      float* out = ws + (((size_t)b * NTU + tile_index(I, J, NT)) * nsplit + split) * (GT * GT);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int row = (lane >> 3) + 8 * k, c4 = lane & 7;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(reg + row * PITCH + 4 * c4);
+        *reinterpret_cast<f32x4*>(out + (qi * 32 + row) * GT + qj * 32 + 4 * c4) = v;
+        if (I == J && qi != qj) {  // mirror: row `row` of the transposed block
+          f32x4 m;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) m[e] = reg[(4 * c4 + e) * PITCH + row];
+          *reinterpret_cast<f32x4*>(out + (qj * 32 + row) * GT + qi * 32 + 4 * c4) = m;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next stores
+    }
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (q >= cnt) break;
+    const int I = bi[q] >> 1, J = bj[q] >> 1, qi = bi[q] & 1, qj = bj[q] & 1;
+    float* out = ws + (((size_t)b * NTU + tile_index(I, J, NT)) * nsplit + split) * (GT * GT);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float v = acc[q][r] * inv2;
+      out[(qi * 32 + row) * GT + qj * 32 + l32] = v;
+      if (I == J && qi != qj) out[(qj * 32 + l32) * GT + qi * 32 + row] = v;  // mirror
+    }
+  }
+}
+
+// splits per image of gram_tri256_kernel: ~256 blocks over the batch, at least 128 pixels
+// (4 chunks) per block, a multiple of 8 splits
+static int gram_tri256_splits(int hw, int b) {
+  static const int target = std::max(8, STX_KNOB("STX_GRAM256_BLOCKS", 256));
+  int want = std::max(1, target / std::max(1, b));
+  want = std::min(want, std::max(1, hw / 128));
+  return want;
+}
+
+static bool gram_tri256_on(int c, int hw) {
+  static const bool on = STX_KNOB("STX_GRAM_TRI256", 1) != 0;
+  return on && c == 256 && hw % 32 == 0;
+}
+
 static int gram_tri_splits(int c, int hw, int b) {
   // C = 128 @ 256^2: 256 > 128 > 64 blocks (A/B)
   static const int target = std::max(8, STX_KNOB("STX_GRAM_TRI_BLOCKS", 256));
@@ -803,6 +1003,7 @@ static size_t gram_parts_offset(int b, int c, int hw, int* nparts) {
   gram_geometry16(c, hw, b, ns16, sl16, ntu);
   nsplit = std::max(nsplit, ns16);
   if (gram_tri_on(c, hw)) nsplit = std::max(nsplit, gram_tri_splits(c, hw, b));
+  if (gram_tri256_on(c, hw)) nsplit = std::max(nsplit, gram_tri256_splits(hw, b));
   if (nparts) *nparts = b * ntu * FSUB;
   return (size_t)b * ntu * nsplit * GT * GT * sizeof(float);
 }
@@ -888,6 +1089,16 @@ static int gram_run(const float* z, int b, int c, int hw, float scale, float* g_
       hipLaunchKernelGGL(gram_tri_f16_kernel<256>, dim3(nsplit, 1, b), dim3(256), 0, st, z, slabs,
                          hw, nsplit, split_len, z_amax);
 #endif
+  } else if (f16 && gram_tri256_on(c, hw)) {
+    nsplit = gram_tri256_splits(hw, b);
+    split_len = rup(cdiv(hw, nsplit), T256_PX);
+    nsplit = cdiv(hw, split_len);
+    if (STX_KNOB("STX_GRAM256_STAGE", 1))
+      hipLaunchKernelGGL(gram_tri256_kernel<true>, dim3(nsplit, 1, b), dim3(512), 0, st, z, slabs,
+                         hw, nsplit, split_len, z_amax);
+    else
+      hipLaunchKernelGGL(gram_tri256_kernel<false>, dim3(nsplit, 1, b), dim3(512), 0, st, z, slabs,
+                         hw, nsplit, split_len, z_amax);
   } else if (f16) {
     hipLaunchKernelGGL(gram_partial_f16_kernel, dim3(nsplit * ntu, 1, b), dim3(256), 0, st, z,
                        slabs, c, hw, nsplit, split_len, z_amax);

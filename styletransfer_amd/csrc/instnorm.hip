@@ -18,6 +18,16 @@ namespace stx {
 
 constexpr int NB = 256;
 
+// y = fma(u, gsc, sh) with gsc = gamma rstd, sh = fma(-mean, gsc, beta): every forward
+// kernel forms the output this way, with explicit fmas (no contraction left to the
+// compiler), so a backward recomputes the ReLU decision y > 0 from u = x (+ res) and the
+// saved mean / rstd bit for bit instead of reading y (one plane-read fewer per element)
+__device__ __forceinline__ void in_coefs(const float* gamma, const float* beta, int ch,
+                                         float mean, float rstd, float& gsc, float& sh) {
+  gsc = gamma ? gamma[ch] * rstd : rstd;
+  sh = __builtin_fmaf(-mean, gsc, beta ? beta[ch] : 0.f);
+}
+
 __global__ void __launch_bounds__(NB)
 instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
                     const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -57,8 +67,8 @@ instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
   }
   const float var = block_sum<NB>(q, red) / (float)hw;
   const float rstd = 1.f / sqrtf(var + eps);
-  const float gsc = gamma ? gamma[ch] * rstd : rstd;
-  const float sh = (beta ? beta[ch] : 0.f) - mean * gsc;
+  float gsc, sh;
+  in_coefs(gamma, beta, ch, mean, rstd, gsc, sh);
   float* yp = y + base;
   uint32_t om = 0u;  // max |y| as IEEE bits (NaN sorts above inf)
   if (vec) {
@@ -68,7 +78,7 @@ instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
       f32x4 o;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        o[k] = v[k] * gsc + sh;
+        o[k] = __builtin_fmaf(v[k], gsc, sh);
         if (relu) o[k] = fmaxf(o[k], 0.f);
         om = max(om, __float_as_uint(o[k]) & 0x7fffffffu);
       }
@@ -76,7 +86,7 @@ instnorm_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
     }
   } else {
     for (int i = threadIdx.x; i < hw; i += NB) {
-      float o = (xp[i] + (rp ? rp[i] : 0.f)) * gsc + sh;
+      float o = __builtin_fmaf(xp[i] + (rp ? rp[i] : 0.f), gsc, sh);
       o = relu ? fmaxf(o, 0.f) : o;
       yp[i] = o;
       om = max(om, __float_as_uint(o) & 0x7fffffffu);
@@ -110,7 +120,7 @@ __device__ __forceinline__ void block_max_to_nt(float* group, uint32_t mu, float
 
 template <int NBT>
 __global__ void __launch_bounds__(NBT)
-instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ beta,
                     const float* __restrict__ x, const float* __restrict__ res,
                     const float* __restrict__ gamma, const float* __restrict__ mean,
                     const float* __restrict__ rstd, float* __restrict__ du,
@@ -120,15 +130,15 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
   const size_t base = (size_t)blockIdx.x * hw;
   const int ch = blockIdx.x % c;
   const float mu = mean[blockIdx.x], rs = rstd[blockIdx.x];
+  float gsc, sh;  // the forward's y = fma(u, gsc, sh): the ReLU decision recomputed
+  in_coefs(gamma, beta, ch, mu, rs, gsc, sh);
   const float* dyp = dy + base;
-  const float* yp = y ? y + base : nullptr;
   const float* xp = x + base;
   const float* rp = res ? res + base : nullptr;
   float sg = 0.f, sgx = 0.f;
   const bool vec = ((hw & 3) == 0) &&
-                   ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(y) |
-                     reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) |
-                     reinterpret_cast<uintptr_t>(du)) & 15) == 0;
+                   ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) |
+                     reinterpret_cast<uintptr_t>(res) | reinterpret_cast<uintptr_t>(du)) & 15) == 0;
   // float4 path (16-B aligned planes): 4x fewer loads, two float4 groups per trip so
   // each thread keeps 8 loads in flight
   auto ld4 = [](const float* p, int i) { return *reinterpret_cast<const f32x4*>(p + i); };
@@ -137,11 +147,11 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
       const f32x4 d4 = ld4(dyp, i);
       const f32x4 x4 = ld4(xp, i);
       const f32x4 r4 = rp ? ld4(rp, i) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 y4 = relu ? ld4(yp, i) : f32x4{1.f, 1.f, 1.f, 1.f};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float g = (relu && !(y4[e] > 0.f)) ? 0.f : d4[e];
-        const float xh = (x4[e] + r4[e] - mu) * rs;
+        const float u = x4[e] + r4[e];
+        const float g = (relu && !(__builtin_fmaf(u, gsc, sh) > 0.f)) ? 0.f : d4[e];
+        const float xh = (u - mu) * rs;
         sg += g;
         sgx += g * xh;
       }
@@ -149,8 +159,9 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
   } else {
     for (int i = threadIdx.x; i < hw; i += NBT) {
       float g = dyp[i];
-      if (relu && !(yp[i] > 0.f)) g = 0.f;
-      const float xh = (xp[i] + (rp ? rp[i] : 0.f) - mu) * rs;
+      const float u = xp[i] + (rp ? rp[i] : 0.f);
+      if (relu && !(__builtin_fmaf(u, gsc, sh) > 0.f)) g = 0.f;
+      const float xh = (u - mu) * rs;
       sg += g;
       sgx += g * xh;
     }
@@ -167,12 +178,12 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
       const f32x4 d4 = ld4(dyp, i);
       const f32x4 x4 = ld4(xp, i);
       const f32x4 r4 = rp ? ld4(rp, i) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 y4 = relu ? ld4(yp, i) : f32x4{1.f, 1.f, 1.f, 1.f};
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float g = (relu && !(y4[e] > 0.f)) ? 0.f : d4[e];
-        const float xh = (x4[e] + r4[e] - mu) * rs;
+        const float u = x4[e] + r4[e];
+        const float g = (relu && !(__builtin_fmaf(u, gsc, sh) > 0.f)) ? 0.f : d4[e];
+        const float xh = (u - mu) * rs;
         o[e] = k * ((float)hw * g - sg - xh * sgx);
         om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
         sdu += o[e];
@@ -182,8 +193,9 @@ instnorm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
   } else {
     for (int i = threadIdx.x; i < hw; i += NBT) {
       float g = dyp[i];
-      if (relu && !(yp[i] > 0.f)) g = 0.f;
-      const float xh = (xp[i] + (rp ? rp[i] : 0.f) - mu) * rs;
+      const float u = xp[i] + (rp ? rp[i] : 0.f);
+      if (relu && !(__builtin_fmaf(u, gsc, sh) > 0.f)) g = 0.f;
+      const float xh = (u - mu) * rs;
       const float o = k * ((float)hw * g - sg - xh * sgx);
       dup[i] = o;
       om = max(om, __float_as_uint(o) & 0x7fffffffu);
@@ -251,8 +263,8 @@ instnorm_fwd_reg_kernel(const float* __restrict__ x, const float* __restrict__ r
   }
   const float var = block_sum_nt<NT>(q, red) / (float)hw;
   const float rstd = 1.f / sqrtf(var + eps);
-  const float gsc = gamma ? gamma[ch] * rstd : rstd;
-  const float sh = (beta ? beta[ch] : 0.f) - mean * gsc;
+  float gsc, sh;
+  in_coefs(gamma, beta, ch, mean, rstd, gsc, sh);
   f32x4* yp = reinterpret_cast<f32x4*>(y + base);
   uint32_t om = 0u;
 #pragma unroll
@@ -262,7 +274,7 @@ instnorm_fwd_reg_kernel(const float* __restrict__ x, const float* __restrict__ r
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        o[e] = u[k][e] * gsc + sh;
+        o[e] = __builtin_fmaf(u[k][e], gsc, sh);
         if (relu) o[e] = fmaxf(o[e], 0.f);
         om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
       }
@@ -291,7 +303,7 @@ instnorm_fwd_reg_kernel(const float* __restrict__ x, const float* __restrict__ r
 
 template <int NT, int R4>
 __global__ void __launch_bounds__(NT)
-instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ beta,
                         const float* __restrict__ x, const float* __restrict__ res,
                         const float* __restrict__ gamma, const float* __restrict__ mean,
                         const float* __restrict__ rstd, float* __restrict__ du,
@@ -301,9 +313,10 @@ instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ 
   const size_t base = (size_t)blockIdx.x * hw;
   const int ch = blockIdx.x % c;
   const float mu = mean[blockIdx.x], rs = rstd[blockIdx.x];
+  float gsc, sh;  // the forward's y = fma(u, gsc, sh): the ReLU decision recomputed
+  in_coefs(gamma, beta, ch, mu, rs, gsc, sh);
   const int n4 = hw >> 2;
   const f32x4* dyp = reinterpret_cast<const f32x4*>(dy + base);
-  const f32x4* yp = relu ? reinterpret_cast<const f32x4*>(y + base) : nullptr;
   const f32x4* xp = reinterpret_cast<const f32x4*>(x + base);
   const f32x4* rp = res ? reinterpret_cast<const f32x4*>(res + base) : nullptr;
   f32x4 g[R4], xh[R4];
@@ -316,10 +329,9 @@ instnorm_bwd_reg_kernel(const float* __restrict__ dy, const float* __restrict__ 
     const f32x4 d4 = in ? dyp[i] : z4;
     f32x4 u4 = in ? xp[i] : z4;
     if (rp && in) u4 += rp[i];
-    const f32x4 y4 = (relu && in) ? yp[i] : f32x4{1.f, 1.f, 1.f, 1.f};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      g[k][e] = (relu && !(y4[e] > 0.f)) ? 0.f : d4[e];
+      g[k][e] = (relu && !(__builtin_fmaf(u4[e], gsc, sh) > 0.f)) ? 0.f : d4[e];
       xh[k][e] = in ? (u4[e] - mu) * rs : 0.f;
     }
   }
@@ -426,15 +438,15 @@ instnorm_fwd_pipe_kernel(const float* __restrict__ x, const float* __restrict__ 
     const float var = block_sum_nt<NT>(q, red) / (float)HW;
     const float rstd = 1.f / sqrtf(var + eps);
     const int ch = plane % c;
-    const float gsc = gamma ? gamma[ch] * rstd : rstd;
-    const float sh = (beta ? beta[ch] : 0.f) - mean * gsc;
+    float gsc, sh;
+    in_coefs(gamma, beta, ch, mean, rstd, gsc, sh);
     f32x4* yp = reinterpret_cast<f32x4*>(y + (size_t)plane * HW);
 #pragma unroll
     for (int k = 0; k < R4; ++k) {
       f32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        o[e] = u[k][e] * gsc + sh;
+        o[e] = __builtin_fmaf(u[k][e], gsc, sh);
         if (relu) o[e] = fmaxf(o[e], 0.f);
         om = max(om, __float_as_uint(o[e]) & 0x7fffffffu);
       }
@@ -463,7 +475,7 @@ instnorm_fwd_pipe_kernel(const float* __restrict__ x, const float* __restrict__ 
 
 template <int NT, int R4, int PPB, bool RELU, bool RES>
 __global__ void __launch_bounds__(NT)
-instnorm_bwd_pipe_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+instnorm_bwd_pipe_kernel(const float* __restrict__ dy, const float* __restrict__ beta,
                          const float* __restrict__ x, const float* __restrict__ res,
                          const float* __restrict__ gamma, const float* __restrict__ mean,
                          const float* __restrict__ rstd, float* __restrict__ du,
@@ -471,14 +483,13 @@ instnorm_bwd_pipe_kernel(const float* __restrict__ dy, const float* __restrict__
   constexpr int HW = 4 * NT * R4;
   __shared__ float red[NT / 64];
   const int p0 = blockIdx.x * PPB;
-  f32x4 db[2][R4], yb[2][R4], xb[2][R4], rb[2][R4];
+  f32x4 db[2][R4], xb[2][R4], rb[2][R4];
   auto load = [&](int b, int plane) {
     const size_t base = (size_t)plane * HW;
 #pragma unroll
     for (int k = 0; k < R4; ++k) {
       const int i = threadIdx.x + k * NT;
       db[b][k] = reinterpret_cast<const f32x4*>(dy + base)[i];
-      if constexpr (RELU) yb[b][k] = reinterpret_cast<const f32x4*>(y + base)[i];
       xb[b][k] = reinterpret_cast<const f32x4*>(x + base)[i];
       if constexpr (RES) rb[b][k] = reinterpret_cast<const f32x4*>(res + base)[i];
     }
@@ -490,6 +501,8 @@ instnorm_bwd_pipe_kernel(const float* __restrict__ dy, const float* __restrict__
     const int b = j & 1, plane = p0 + j;
     if (j + 1 < PPB) load(b ^ 1, plane + 1);
     const float mu = mean[plane], rs = rstd[plane];
+    float gsc, sh;  // the forward's y = fma(u, gsc, sh): the ReLU decision recomputed
+    in_coefs(gamma, beta, plane % c, mu, rs, gsc, sh);
     f32x4 g[R4], xh[R4];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
@@ -498,7 +511,7 @@ instnorm_bwd_pipe_kernel(const float* __restrict__ dy, const float* __restrict__
       if constexpr (RES) u4 += rb[b][k];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if constexpr (RELU) g[k][e] = !(yb[b][k][e] > 0.f) ? 0.f : db[b][k][e];
+        if constexpr (RELU) g[k][e] = !(__builtin_fmaf(u4[e], gsc, sh) > 0.f) ? 0.f : db[b][k][e];
         else g[k][e] = db[b][k][e];
         xh[k][e] = (u4[e] - mu) * rs;
       }
@@ -565,7 +578,7 @@ static int in_ppb() {  // planes per block of the pipelined 64^2 kernels (1: one
 // of dy and y than the two-pass loop kernel.  Same arithmetic as instnorm_bwd_reg_kernel.
 template <int NT, int R4, bool RELU, bool RES>
 __global__ void __launch_bounds__(NT)
-instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__ beta,
                          const float* __restrict__ x, const float* __restrict__ res,
                          const float* __restrict__ gamma, const float* __restrict__ mean,
                          const float* __restrict__ rstd, float* __restrict__ du,
@@ -578,9 +591,10 @@ instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__
   // per-plane buffer descriptors: one lane offset, the per-k step in the scalar offset
   // (64-bit addresses per k would take 2 VGPRs each and spill); elements past the
   // plane read 0 and their stores are dropped by the range check
+  float gsc, sh;  // the forward's y = fma(u, gsc, sh): the ReLU decision recomputed
+  in_coefs(gamma, beta, ch, mu, rs, gsc, sh);
   const uint32_t pbytes = (uint32_t)hw * 4u;
   const auto rdy = make_srd(dy + base, pbytes);
-  const auto ry = make_srd(RELU ? y + base : dy + base, pbytes);
   const auto rx = make_srd(x + base, pbytes);
   const auto rr = make_srd(RES ? res + base : x + base, pbytes);
   const auto rdu = make_srd(du + base, pbytes);
@@ -595,12 +609,10 @@ instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__
         f32x4, __builtin_amdgcn_raw_buffer_load_b128(rdy, lo, k * KSTEP, 0));
     f32x4 u4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, lo, k * KSTEP, 0));
     if (RES) u4 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, lo, k * KSTEP, 0));
-    f32x4 y4 = {1.f, 1.f, 1.f, 1.f};
-    if (RELU) y4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry, lo, k * KSTEP, 0));
     const bool in = (int)threadIdx.x + k * NT < n4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      g[k][e] = (RELU && !(y4[e] > 0.f)) ? 0.f : d4[e];
+      g[k][e] = (RELU && !(__builtin_fmaf(u4[e], gsc, sh) > 0.f)) ? 0.f : d4[e];
       const float xh = in ? (u4[e] - mu) * rs : 0.f;
       sg += g[k][e];
       sgx += g[k][e] * xh;
@@ -777,12 +789,13 @@ extern "C" size_t stx_instnorm_bwd_ws(int n, int c) {
   return (size_t)3 * n * c * sizeof(float) + 64;
 }
 
-extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x, const float* res,
-                                const float* gamma, const float* mean, const float* rstd,
+extern "C" int stx_instnorm_bwd(const float* dy, const float* beta, const float* x,
+                                const float* res, const float* gamma, const float* mean,
+                                const float* rstd,
                                 float* du, float* dgamma, float* dbeta, float* dbias_in, int n,
                                 int c, int hw, int relu, int accumulate_params, float* out_amax,
                                 void* ws, size_t ws_bytes, void* stream) {
-  if (n <= 0 || c <= 0 || hw <= 0 || !dy || !x || !du || !mean || !rstd || (relu && !y)) {
+  if (n <= 0 || c <= 0 || hw <= 0 || !dy || !x || !du || !mean || !rstd) {
     set_error("stx_instnorm_bwd: invalid args");
     return STX_E_INVALID;
   }
@@ -791,14 +804,14 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
     return STX_E_WORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
-  const bool al = ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(y) |
-                    reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(res) |
-                    reinterpret_cast<uintptr_t>(du)) & 15) == 0 && hw % 4 == 0;
+  const bool al = ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) |
+                    reinterpret_cast<uintptr_t>(res) | reinterpret_cast<uintptr_t>(du)) & 15) == 0 &&
+                  hw % 4 == 0;
   // block shape of the 64^2 kernels, as stx_instnorm_fwd
   static const int cfg = STX_KNOB("STX_IN_CFG", 2);
 #ifdef STX_AB
   if (cfg == 1 && al && hw <= 4 * 128 * 8)
-    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, dy, y, x,
+    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<128, 8>), dim3(n * c), dim3(128), 0, st, dy, beta, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else
 #endif
@@ -807,7 +820,7 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
     const int ppb = in_ppb();
     const dim3 grid(n * c / ppb);
 #define STX_IN_BWD_PIPE(P, RL, R)                                                               \
-  hipLaunchKernelGGL((instnorm_bwd_pipe_kernel<512, 2, P, RL, R>), grid, dim3(512), 0, st, dy, y, \
+  hipLaunchKernelGGL((instnorm_bwd_pipe_kernel<512, 2, P, RL, R>), grid, dim3(512), 0, st, dy, beta, \
                      x, res, gamma, mean, rstd, du, (float*)ws, c, out_amax)
     if (ppb == 4) {
       if (relu) { if (res) STX_IN_BWD_PIPE(4, true, true); else STX_IN_BWD_PIPE(4, true, false); }
@@ -818,23 +831,23 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* y, const float* x,
     }
 #undef STX_IN_BWD_PIPE
   } else if (cfg == 2 && al && hw <= 4 * 512 * 2)
-    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<512, 2>), dim3(n * c), dim3(512), 0, st, dy, y, x,
+    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<512, 2>), dim3(n * c), dim3(512), 0, st, dy, beta, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else if (al && hw <= 4 * 256 * 4)
-    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 4>), dim3(n * c), dim3(256), 0, st, dy, y, x,
+    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 4>), dim3(n * c), dim3(256), 0, st, dy, beta, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else if (al && hw <= 4 * 256 * 16)
-    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 16>), dim3(n * c), dim3(256), 0, st, dy, y,
+    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 16>), dim3(n * c), dim3(256), 0, st, dy, beta,
                        x, res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else if (al && hw <= 4 * 1024 * 16 && relu && !res && greg_on())  // 256^2 IN + ReLU
     hipLaunchKernelGGL((instnorm_bwd_greg_kernel<1024, 16, true, false>), dim3(n * c),
-                       dim3(1024), 0, st, dy, y, x, res, gamma, mean, rstd, du, (float*)ws, c,
+                       dim3(1024), 0, st, dy, beta, x, res, gamma, mean, rstd, du, (float*)ws, c,
                        hw, relu, out_amax);
   else if (hw >= 4 * 1024 * 4)  // big planes (256^2): 16 waves per plane
-    hipLaunchKernelGGL(instnorm_bwd_kernel<1024>, dim3(n * c), dim3(1024), 0, st, dy, y, x, res,
+    hipLaunchKernelGGL(instnorm_bwd_kernel<1024>, dim3(n * c), dim3(1024), 0, st, dy, beta, x, res,
                        gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else
-    hipLaunchKernelGGL(instnorm_bwd_kernel<NB>, dim3(n * c), dim3(NB), 0, st, dy, y, x, res, gamma,
+    hipLaunchKernelGGL(instnorm_bwd_kernel<NB>, dim3(n * c), dim3(NB), 0, st, dy, beta, x, res, gamma,
                        mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   if (dgamma || dbeta || dbias_in)
     hipLaunchKernelGGL(instnorm_param_grad_kernel, dim3(cdiv(c, 256)), dim3(256), 0, st,

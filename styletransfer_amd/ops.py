@@ -968,10 +968,12 @@ def instnorm_fwd(x, gamma, beta, res=None, eps=1e-5, relu=False, out=None, out_a
     return out, mean, rstd
 
 
-def instnorm_bwd(dy, y, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbeta=None,
+def instnorm_bwd(dy, beta, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbeta=None,
                  accumulate=False, out_amax=None, dbias_in=None):
     """du of y = [relu](IN(x (+res))*gamma + beta); dgamma / dbeta / dbias_in (the bias
-    gradient of the conv that produced x, sum du) written or accumulated when given."""
+    gradient of the conv that produced x, sum du) written or accumulated when given.
+    beta: the forward's beta (None if it had none): with relu the kernel recomputes the
+    forward's y > 0 from x (+ res), mean, rstd, gamma, beta bit for bit (include/stx.h)."""
     n, c = x.shape[:2]
     hw = x[0, 0].numel()
     du = torch.empty_like(x)
@@ -989,7 +991,7 @@ def instnorm_bwd(dy, y, x, res, gamma, mean, rstd, relu=False, dgamma=None, dbet
         dgamma = dbeta = dbias_in = None
     else:
         wp, wn = WS.get(need, x.device)
-    check(L.stx_instnorm_bwd(dy.data_ptr(), _p(y), x.data_ptr(), _p(res), _p(gamma),
+    check(L.stx_instnorm_bwd(dy.data_ptr(), _p(beta), x.data_ptr(), _p(res), _p(gamma),
                              mean.data_ptr(), rstd.data_ptr(), du.data_ptr(), _p(dgamma),
                              _p(dbeta), _p(dbias_in), n, c, hw, int(relu), int(accumulate),
                              _p(out_amax), wp,

@@ -343,7 +343,12 @@ def test_vgg_fused_pool_matches_unfused(dev):
 
 
 @pytest.mark.parametrize("shape", [(1, 64, 64, 64), (2, 128, 24, 40), (1, 256, 16, 16),
-                                   (1, 96, 9, 24), (3, 64, 8, 7), (1, 64, 512, 512)])
+                                   (1, 96, 9, 24), (3, 64, 8, 7), (1, 64, 512, 512),
+                                   # C = 256 on the whole-triangle 8-wave kernel: the Gatys
+                                   # conv3_1 tap (128 splits), fast_st's B = 8 at 64^2, a
+                                   # ragged last split (960 px), and hw % 32 != 0 (fallback)
+                                   (1, 256, 128, 128), (8, 256, 64, 64), (2, 256, 24, 40),
+                                   (1, 256, 12, 10)])
 def test_split_gram(dev, shape):
     """fp16 hi/lo split Gram partials (z_amax given) vs fp64, and the style loss /
     backward coefficients they feed vs the fp32 MFMA path."""

@@ -23,6 +23,10 @@ def test_library_exports_header_symbols():
     assert len(decl) >= 30
     assert decl <= syms, decl - syms
     assert decl == set(N.SIGNATURES), decl ^ set(N.SIGNATURES)
+    # the ABI revision the binding checks at load (a library of another revision is
+    # refused, never driven with arguments whose meaning changed)
+    rev = re.search(r"#define STX_ABI_VERSION (\d+)", hdr).group(1)
+    assert L.stx_abi_version() == N.STX_ABI_VERSION == int(rev)
 
 
 def test_struct_mirrors_match_the_library():

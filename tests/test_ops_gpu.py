@@ -225,17 +225,28 @@ def test_adam_step_clear(dev):
         assert torch.equal(st[0][0], st[1][0]) and int(st[1][3].item()) == 2
 
 
-@pytest.mark.parametrize("relu,res,hw", [(False, False, (12, 20)), (True, False, (12, 20)),
-                                         (False, True, (12, 20)), (True, True, (64, 64)),
-                                         (True, False, (128, 128)), (False, True, (256, 256)),
-                                         (True, False, (7, 9))])
-def test_instnorm(dev, relu, res, hw):
+@pytest.mark.parametrize("relu,res,hw,nc", [(False, False, (12, 20), None),
+                                            (True, False, (12, 20), None),
+                                            (False, True, (12, 20), None),
+                                            (True, True, (64, 64), None),
+                                            (True, False, (128, 128), None),
+                                            (False, True, (256, 256), None),
+                                            (True, False, (7, 9), None),
+                                            # the 256^2 ReLU backward (greg kernel), and the
+                                            # pipelined 64^2 kernels (>= 1024 planes, B = 8)
+                                            (True, False, (256, 256), None),
+                                            (True, False, (64, 64), (8, 128)),
+                                            (True, True, (64, 64), (8, 128))])
+def test_instnorm(dev, relu, res, hw, nc):
     """InstanceNorm (+res, +ReLU) forward/backward on every kernel variant (register-
     resident planes up to 64^2 / 128^2 / 256^2, the loop kernels otherwise) and the
-    max|.| annotations of y and du."""
-    c = 32 if hw == (12, 20) else 4
-    x = rnd(2, c, *hw, dev=dev, seed=71, scale=3, shift=-1).requires_grad_()
-    r = rnd(2, c, *hw, dev=dev, seed=72).requires_grad_() if res else None
+    max|.| annotations of y and du.  The backward recomputes the ReLU decision from x
+    (+ res) and the saved statistics (stx_instnorm_bwd takes beta, not y): du must equal
+    the fp64 backward through the mask of the HIP forward's own y (a decision that differs
+    from y > 0 anywhere would be an O(1) error there)."""
+    n, c = nc if nc else (2, 32 if hw == (12, 20) else 4)
+    x = rnd(n, c, *hw, dev=dev, seed=71, scale=3, shift=-1).requires_grad_()
+    r = rnd(n, c, *hw, dev=dev, seed=72).requires_grad_() if res else None
     gamma = rnd(c, dev=dev, seed=73, shift=0.5).requires_grad_()
     beta = rnd(c, dev=dev, seed=74).requires_grad_()
     u = x + r if res else x
@@ -252,12 +263,23 @@ def test_instnorm(dev, relu, res, hw):
     dg = torch.empty(c, device=dev)
     db = torch.empty(c, device=dev)
     da = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
-    du = ops.instnorm_bwd(dy, y, x.detach(), r.detach() if res else None, gamma.detach(), mean,
-                          rstd, relu=relu, dgamma=dg, dbeta=db, out_amax=da)
+    du = ops.instnorm_bwd(dy, beta.detach(), x.detach(), r.detach() if res else None,
+                          gamma.detach(), mean, rstd, relu=relu, dgamma=dg, dbeta=db, out_amax=da)
     assert rel(du, grads[0]) < 1e-4
     assert rel(dg, grads[1]) < 1e-5
     assert rel(db, grads[2]) < 1e-5
     assert float(da.max()) == float(du.abs().max())
+    # the same backward in fp64 through the HIP forward's own ReLU decisions (y > 0)
+    u64 = (x + r if res else x).detach().double().cpu()
+    hw_ = u64[0, 0].numel()
+    mu64 = u64.mean(dim=(2, 3), keepdim=True)
+    rs64 = 1.0 / torch.sqrt(u64.var(dim=(2, 3), unbiased=False, keepdim=True) + 1e-5)
+    xh = (u64 - mu64) * rs64
+    g64 = dy.double().cpu() * ((y.cpu() > 0).double() if relu else 1.0)
+    gm = gamma.detach().double().cpu().view(1, -1, 1, 1)
+    du64 = gm * rs64 / hw_ * (hw_ * g64 - g64.sum(dim=(2, 3), keepdim=True)
+                              - xh * (g64 * xh).sum(dim=(2, 3), keepdim=True))
+    assert rel(du.cpu(), du64) < 1e-5, rel(du.cpu(), du64)
 
 
 def test_upsample_tv(dev):
