@@ -572,11 +572,13 @@ static int in_ppb() {  // planes per block of the pipelined 64^2 kernels (1: one
   return v;
 }
 
-// Large planes (the ITN's 256^2 layers: 64 K floats, 1024 threads x 16 float4): only g
-// stays in registers (64 VGPRs -- g and x-hat together would not fit 16 waves per CU);
-// the second pass re-reads u = x (+ res) instead of dy, y and u, one plane-read fewer
-// of dy and y than the two-pass loop kernel.  Same arithmetic as instnorm_bwd_reg_kernel.
-template <int NT, int R4, bool RELU, bool RES>
+// Large planes (the ITN's 256^2 layers: 64 K floats, 1024 threads x 16 float4): g stays
+// in registers (64 VGPRs) and u = x (+ res) is kept too -- its first XL float4s per thread
+// in registers, the rest in LDS (XL = 8: 32 VGPRs + 128 KB of LDS, one block per CU) -- so
+// the plane is read once: dy and u in, du out (the round-5 form re-read u in its second
+// pass: 4 plane-reads + 1 write instead of 2 + 1).  The ReLU decision is recomputed from u.
+// Same arithmetic as instnorm_bwd_reg_kernel.
+template <int NT, int R4, bool RELU, bool RES, int XL>
 __global__ void __launch_bounds__(NT)
 instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__ beta,
                          const float* __restrict__ x, const float* __restrict__ res,
@@ -585,14 +587,16 @@ instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__
                          float* __restrict__ parts, int c, int hw, int relu,
                          float* __restrict__ out_amax) {
   __shared__ float red[NT / 64];
+  // u of steps XL .. R4-1 ([step][thread]); XL < 0: u not kept, re-read in the second pass
+  __shared__ f32x4 ul[XL < 0 ? 1 : (R4 - XL) * NT];
   const size_t base = (size_t)blockIdx.x * hw;
   const int ch = blockIdx.x % c;
   const float mu = mean[blockIdx.x], rs = rstd[blockIdx.x];
+  float gsc, sh;  // the forward's y = fma(u, gsc, sh): the ReLU decision recomputed
+  in_coefs(gamma, beta, ch, mu, rs, gsc, sh);
   // per-plane buffer descriptors: one lane offset, the per-k step in the scalar offset
   // (64-bit addresses per k would take 2 VGPRs each and spill); elements past the
   // plane read 0 and their stores are dropped by the range check
-  float gsc, sh;  // the forward's y = fma(u, gsc, sh): the ReLU decision recomputed
-  in_coefs(gamma, beta, ch, mu, rs, gsc, sh);
   const uint32_t pbytes = (uint32_t)hw * 4u;
   const auto rdy = make_srd(dy + base, pbytes);
   const auto rx = make_srd(x + base, pbytes);
@@ -601,7 +605,7 @@ instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__
   const uint32_t lo = threadIdx.x * 16u;
   constexpr uint32_t KSTEP = NT * 16u;
   const int n4 = hw >> 2;
-  f32x4 g[R4];
+  f32x4 g[R4], ur[XL > 0 ? XL : 1];
   float sg = 0.f, sgx = 0.f;
 #pragma unroll
   for (int k = 0; k < R4; ++k) {
@@ -617,10 +621,17 @@ instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__
       sg += g[k][e];
       sgx += g[k][e] * xh;
     }
-    // at most 4 steps of loads in flight (the scheduler would hoist all 16 and spill)
-    if ((k & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (XL >= 0) {
+      if (k < XL)
+        ur[k < XL ? k : 0] = u4;
+      else
+        ul[(k - XL) * NT + threadIdx.x] = u4;
+    }
+    // at most 2 steps of loads in flight (g and u take 96 VGPRs; the scheduler would
+    // hoist more loads and spill)
+    if ((k & 1) == 1) __builtin_amdgcn_sched_barrier(0);
   }
-  sg = block_sum_nt<NT>(sg, red);
+  sg = block_sum_nt<NT>(sg, red);   // (its barriers also order the LDS stores of u)
   sgx = block_sum_nt<NT>(sgx, red);
   const float gm = gamma ? gamma[ch] : 1.f;
   const float kk = gm * rs / (float)hw;
@@ -628,9 +639,14 @@ instnorm_bwd_greg_kernel(const float* __restrict__ dy, const float* __restrict__
   float sdu = 0.f;
 #pragma unroll
   for (int k = 0; k < R4; ++k) {
-    if ((k & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-    f32x4 u4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, lo, k * KSTEP, 0));
-    if (RES) u4 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, lo, k * KSTEP, 0));
+    f32x4 u4;
+    if constexpr (XL < 0) {
+      if ((k & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+      u4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, lo, k * KSTEP, 0));
+      if (RES) u4 += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, lo, k * KSTEP, 0));
+    } else {
+      u4 = k < XL ? ur[k < XL ? k : 0] : ul[(k - XL) * NT + threadIdx.x];
+    }
     const bool in = (int)threadIdx.x + k * NT < n4;
     f32x4 o;
 #pragma unroll
@@ -840,9 +856,24 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* beta, const float*
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 16>), dim3(n * c), dim3(256), 0, st, dy, beta,
                        x, res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else if (al && hw <= 4 * 1024 * 16 && relu && !res && greg_on())  // 256^2 IN + ReLU
-    hipLaunchKernelGGL((instnorm_bwd_greg_kernel<1024, 16, true, false>), dim3(n * c),
-                       dim3(1024), 0, st, dy, beta, x, res, gamma, mean, rstd, du, (float*)ws, c,
-                       hw, relu, out_amax);
+  {
+    // u kept in registers + LDS at 512 threads per plane (STX_GREG_FORM A/B, B8 x 32 planes
+    // of 256^2, same box: 0 = u re-read in the second pass at 1024 threads 51.0 us, 1 = u
+    // kept at 1024 threads 44.1 us (spills 24 VGPRs), 2 = this 40.1 us)
+    static const int form = STX_KNOB("STX_GREG_FORM", 2);
+    if (form == 0)
+      hipLaunchKernelGGL((instnorm_bwd_greg_kernel<1024, 16, true, false, -1>), dim3(n * c),
+                         dim3(1024), 0, st, dy, beta, x, res, gamma, mean, rstd, du, (float*)ws,
+                         c, hw, relu, out_amax);
+    else if (form == 2)
+      hipLaunchKernelGGL((instnorm_bwd_greg_kernel<512, 32, true, false, 14>), dim3(n * c),
+                         dim3(512), 0, st, dy, beta, x, res, gamma, mean, rstd, du, (float*)ws,
+                         c, hw, relu, out_amax);
+    else
+      hipLaunchKernelGGL((instnorm_bwd_greg_kernel<1024, 16, true, false, 7>), dim3(n * c),
+                         dim3(1024), 0, st, dy, beta, x, res, gamma, mean, rstd, du, (float*)ws,
+                         c, hw, relu, out_amax);
+  }
   else if (hw >= 4 * 1024 * 4)  // big planes (256^2): 16 waves per plane
     hipLaunchKernelGGL(instnorm_bwd_kernel<1024>, dim3(n * c), dim3(1024), 0, st, dy, beta, x, res,
                        gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
