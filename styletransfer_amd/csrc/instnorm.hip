@@ -563,6 +563,16 @@ instnorm_bwd_pipe_kernel(const float* __restrict__ dy, const float* __restrict__
   }
 }
 
+// block shape of the planes between 4 x 256 x 4 and 4 x 1024 x 4 floats (the ITN's 128^2
+// layers: 512 planes at B = 8): 0 = 256 x 16 float4 (2 blocks, 8 waves per CU), 1 = 1024 x
+// 4, 2 = 512 x 8, 3 = the pipelined kernels on two planes per 512-thread block (A/B:
+// STX_IN128; B8 x 64 @ 128^2 ReLU, same box: fwd / bwd 13.9 / 18.9, 13.7 / 21.7, 13.5 /
+// 18.0, 14.6 / 19.0 us -- none pays, 0 is kept)
+static int in128_form() {
+  static const int v = STX_KNOB("STX_IN128", 0);
+  return v;
+}
+
 static int in_ppb() {  // planes per block of the pipelined 64^2 kernels (1: one-plane kernels)
   // 1, 2 or 4 (the launches below instantiate these; anything else means 1)
   static const int v = [] {
@@ -784,6 +794,15 @@ extern "C" int stx_instnorm_fwd(const float* x, const float* res, const float* g
   else if (hw % 4 == 0 && hw <= 4 * 256 * 4)
     hipLaunchKernelGGL((instnorm_fwd_reg_kernel<256, 4>), dim3(n * c), dim3(256), 0, st, x, res,
                        gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
+  else if (in128_form() == 3 && hw == 4 * 512 * 8 && !res && (n * c) % 2 == 0 && n * c / 2 >= 256)
+    hipLaunchKernelGGL((instnorm_fwd_pipe_kernel<512, 8, 2, false>), dim3(n * c / 2), dim3(512), 0,
+                       st, x, res, gamma, beta, y, mean, rstd, c, eps, relu, out_amax);
+  else if (in128_form() == 1 && hw % 4 == 0 && hw <= 4 * 1024 * 4)
+    hipLaunchKernelGGL((instnorm_fwd_reg_kernel<1024, 4>), dim3(n * c), dim3(1024), 0, st, x,
+                       res, gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
+  else if (in128_form() == 2 && hw % 4 == 0 && hw <= 4 * 512 * 8)
+    hipLaunchKernelGGL((instnorm_fwd_reg_kernel<512, 8>), dim3(n * c), dim3(512), 0, st, x,
+                       res, gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
   else if (hw % 4 == 0 && hw <= 4 * 256 * 16)
     hipLaunchKernelGGL((instnorm_fwd_reg_kernel<256, 16>), dim3(n * c), dim3(256), 0, st, x, res,
                        gamma, beta, y, mean, rstd, c, hw, eps, relu, out_amax);
@@ -852,6 +871,17 @@ extern "C" int stx_instnorm_bwd(const float* dy, const float* beta, const float*
   else if (al && hw <= 4 * 256 * 4)
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 4>), dim3(n * c), dim3(256), 0, st, dy, beta, x,
                        res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
+  else if (in128_form() == 3 && al && hw == 4 * 512 * 8 && relu && !res && (n * c) % 2 == 0 &&
+           n * c / 2 >= 256)
+    hipLaunchKernelGGL((instnorm_bwd_pipe_kernel<512, 8, 2, true, false>), dim3(n * c / 2),
+                       dim3(512), 0, st, dy, beta, x, res, gamma, mean, rstd, du, (float*)ws, c,
+                       out_amax);
+  else if (in128_form() == 1 && al && hw <= 4 * 1024 * 4)
+    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<1024, 4>), dim3(n * c), dim3(1024), 0, st, dy,
+                       beta, x, res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
+  else if (in128_form() == 2 && al && hw <= 4 * 512 * 8)
+    hipLaunchKernelGGL((instnorm_bwd_reg_kernel<512, 8>), dim3(n * c), dim3(512), 0, st, dy,
+                       beta, x, res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
   else if (al && hw <= 4 * 256 * 16)
     hipLaunchKernelGGL((instnorm_bwd_reg_kernel<256, 16>), dim3(n * c), dim3(256), 0, st, dy, beta,
                        x, res, gamma, mean, rstd, du, (float*)ws, c, hw, relu, out_amax);
