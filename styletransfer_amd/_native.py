@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("STX_LIB", os.path.join(_HERE, "libstx.so"))
 STX_IN_RAW, STX_IN_RELU, STX_IN_RELU_POOL2, STX_IN_UPSAMPLE2, STX_IN_DILATE2 = range(5)
 STX_AMAX_SLOTS = 32  # an "amax" is a group of 32 floats whose max is the value (stx.h)
 STX_GRAM_GROUP = 8  # fused Gram partials per in-kernel group sum (stx_conv_params.gram_cnt)
-STX_ABI_VERSION = 6  # include/stx.h: the library must report the same revision
+STX_ABI_VERSION = 7  # include/stx.h: the library must report the same revision
 
 
 def knob(name: str, default: str) -> str:
@@ -50,7 +50,7 @@ class ConvParams(C.Structure):
         ("wt16", vp), ("w_amax", vp), ("in_amax", vp), ("out_amax", vp),
         ("pool_out", vp), ("p2_amax", vp), ("gram_part", vp), ("pool_sum", i32),
         ("gram_cnt", vp), ("p2_wt_amax", vp), ("mse_ref", vp), ("mse_parts", vp),
-        ("wt16_up", vp),
+        ("wt16_up", vp), ("unpool_out", i32),
     ]
 
 

@@ -37,7 +37,7 @@ extern "C" int stx_abi_version(void) { return STX_ABI_VERSION; }
 // one of these
 extern "C" int stx_abi_layout(long long* out, int n) {
   const long long v[] = {
-      (long long)sizeof(stx_conv_params),  (long long)offsetof(stx_conv_params, wt16_up),
+      (long long)sizeof(stx_conv_params),  (long long)offsetof(stx_conv_params, unpool_out),
       (long long)sizeof(stx_wprep_job),    (long long)offsetof(stx_wprep_job, pad_),
       (long long)sizeof(stx_loss_parts),   (long long)offsetof(stx_loss_parts, k),
       (long long)sizeof(stx_gram_fin_job), (long long)offsetof(stx_gram_fin_job, coef_amax),

@@ -51,6 +51,26 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // one per-chunk descriptor and mark padding/out-of-tile elements with BUF_OOB, so
 // the fetch is straight-line code (no per-element exec branches, no serialising
 // vmcnt(0) per load) and channel padding past the tensor end reads as zero.
+constexpr uint32_t BUF_OOB = 0x80000000u;  // callers keep byte counts below this
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const float* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_t buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f32x2_t, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
+}
+
 // ReLU on the IEEE bit pattern: max(bits, 0) as signed ints keeps every non-negative float
 // and maps every negative one (sign bit set) to +0 -- one v_max_i32, where fmaxf(x, 0.f)
 // of a loaded x is two v_max_f32 (operand canonicalisation first)
@@ -67,20 +87,6 @@ __device__ __forceinline__ float pool4_bits(float a, float b, float c, float d) 
   return __int_as_float(m);
 }
 
-constexpr uint32_t BUF_OOB = 0x80000000u;  // callers keep byte counts below this
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const float* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes,
-                                           0x00020000);
-}
-
-__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
-}
-
-__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
-}
 
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, 0);

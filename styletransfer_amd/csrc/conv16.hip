@@ -350,6 +350,182 @@ __device__ __forceinline__ void phase2_pre(f32x16 (&acc)[2][2], const stx_conv_p
   __syncthreads();  // LDS handed back to the epilogue
 }
 
+// P2 = 4 (stx_conv_params.unpool_out, include/stx.h): a pooled VGG tap's ReLU+MaxPool
+// backward and Gram backward in the epilogue of the data gradient that produces the pooled
+// gradient d (conv2_1^T: d = dP1, the output dZ2 = unpool(d) [Z2 > 0] + s A2 Z2).  The
+// block's 32 x 4 tile of d (wave wn: row ty0 + wn, lane l32: column tx0 + l32) covers the
+// full-resolution rows 2 ty0 .. +7, columns 2 tx0 .. +63 of z:
+//  1. per element of acc (co, d pixel): the window's four z values (two 8-B loads) give its
+//     first maximum of relu(z) (torch's max_pool2d backward index, as gram_bwd16) and the
+//     ReLU mask there -> one bit per element in sel[s] (s = 2 dy + dx, the window slot);
+//  2. per row parity dy: A . z over the region's 256 pixels of that parity on the fp16
+//     hi / lo MFMA, N-tile dx / lane l32 <-> pixel (2 (ty0 + wn) + dy, 2 (tx0 + l32) + dx),
+//     so the lane's N-tile element sits under its own element of d.  z in chunks of 16
+//     channels through double-buffered LDS ([P][cg][dx][row][32] 16-B units: the
+//     fragment reads are conflict-free), one barrier per chunk; A' straight from L2 into
+//     fragment registers (as phase2_pre); accumulators separate from acc, so each term
+//     keeps its own power-of-two scale;
+//  3. y = A.z + the routed d, written as 8-B (dx pair) stores; max|y| -> out_amax.
+template <int TW>
+__device__ __forceinline__ void epi_unpool_gram(f32x16 (&acc)[2][1], const stx_conv_params& p,
+                                                const EpiTile& t, float descale, char* smem) {
+  static_assert(TW == 32, "32 x 4 tiles of d");
+  constexpr int UNITS = 2 * 2 * 2 * 128;  // [P][cg][dx][4 rows x 32]: one 16 KB buffer
+  const int tid = threadIdx.x, h = t.h, l32 = t.l32, wn = t.wn;
+  const int H2 = 2 * p.ho, W2 = 2 * p.wo;
+  const uint32_t pb2 = (uint32_t)H2 * (uint32_t)W2 * 4u;
+  const auto rz = make_srd(p.up_z + (size_t)t.n * 64 * H2 * W2, 64u * pb2);
+  const auto ry = make_srd(p.y + (size_t)t.n * 64 * H2 * W2, 64u * pb2);
+  const int Y0 = 2 * (t.ty0 + wn), X0 = 2 * (t.tx0 + l32);
+  const uint32_t win = (uint32_t)(Y0 * W2 + X0) * 4u, wrow = (uint32_t)W2 * 4u;
+  auto corow = [&](int i, int r) { return i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
+  // 1. window first maximum and mask
+  uint32_t sel[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 1
+  for (int i = 0; i < 2; ++i) {
+    f32x2_t top[16], bot[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t o = (uint32_t)corow(i, r) * pb2 + win;
+      top[r] = buf_ld2(rz, o);
+      bot[r] = buf_ld2(rz, o + wrow);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float z0 = top[r].x, z1 = top[r].y, z2 = bot[r].x, z3 = bot[r].y;
+      const float r0 = relu_bits(z0), r1 = relu_bits(z1), r2 = relu_bits(z2), r3 = relu_bits(z3);
+      int bi = 0;
+      float best = r0;
+      if (r1 > best) { best = r1; bi = 1; }
+      if (r2 > best) { best = r2; bi = 2; }
+      if (r3 > best) { bi = 3; }
+      const float zs = bi == 0 ? z0 : bi == 1 ? z1 : bi == 2 ? z2 : z3;
+      const uint32_t bit = zs > 0.f ? 1u << (16 * i + r) : 0u;
+      sel[0] |= bi == 0 ? bit : 0u;
+      sel[1] |= bi == 1 ? bit : 0u;
+      sel[2] |= bi == 2 ? bit : 0u;
+      sel[3] |= bi == 3 ? bit : 0u;
+    }
+  }
+  // 2. scales: A' = s2 A 2^(15 - ea), z' = z 2^(15 - ez); A.z = acc2 2^(ea + ez - 30)
+  const float s2 = p.p2_scale ? *p.p2_scale : 1.f;
+  const int ea = amax_exp(read_amax(p.p2_wt_amax) * fabsf(s2));
+  const int ez = amax_exp(read_amax(p.p2_amax));
+  const float sa = __builtin_ldexpf(s2, 15 - ea), sz = __builtin_ldexpf(1.f, 15 - ez);
+  const float down = __builtin_ldexpf(1.f, ea + ez - 30);
+  // A' (64 x 64, both passes) split once into LDS after the z buffers: [chunk][P][cg][co]
+  // 16-B units (8 channels of one cout), 16 KB; thread t -> (chunk, cg, co) = the 512
+  // units' first / second half
+  char* la = smem + 2 * UNITS * 16;
+  {
+    const float* __restrict__ A = p.p2_wt + (size_t)t.n * p.p2_wt_batch_stride;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int u = tid + 256 * k, co = u & 63, cg8 = u >> 6;  // channel group of 8 (0..7)
+      float av[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[e] = A[(size_t)(8 * cg8 + e) * p.cout_pad + co];
+      f16x8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = av[e] * sa;
+        const _Float16 vh = (_Float16)v;
+        hi[e] = vh;
+        lo[e] = (_Float16)(v - (float)vh);
+      }
+      const int c = cg8 >> 1, cg = cg8 & 1;
+      *reinterpret_cast<f16x8*>(la + (((c * 2 + 0) * 2 + cg) * 64 + co) * 16) = hi;
+      *reinterpret_cast<f16x8*>(la + (((c * 2 + 1) * 2 + cg) * 64 + co) * 16) = lo;
+    }
+  }
+  // staging thread -> (cg, row wr, column tx): 8 channels x the pixel pair dx = 0, 1
+  const int scg = tid >> 7, swr = (tid >> 5) & 3, stx_ = tid & 31;
+  auto fetch = [&](int dy, int c0, f32x2_t (&g)[8]) {
+    const uint32_t po = (uint32_t)((2 * (t.ty0 + swr) + dy) * W2 + 2 * (t.tx0 + stx_)) * 4u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = buf_ld2(rz, (uint32_t)(c0 + 8 * scg + e) * pb2 + po);
+  };
+  auto stage = [&](const f32x2_t (&g)[8], int b) {
+    char* lz = smem + b * UNITS * 16;
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      f16x8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = (dx ? g[e].y : g[e].x) * sz;
+        const _Float16 vh = (_Float16)v;
+        hi[e] = vh;
+        lo[e] = (_Float16)(v - (float)vh);
+      }
+      const int u = ((scg * 2 + dx) * 4 + swr) * 32 + stx_;  // [cg][dx][row][32] in plane P
+      *reinterpret_cast<f16x8*>(lz + u * 16) = hi;
+      *reinterpret_cast<f16x8*>(lz + (UNITS / 2 + u) * 16) = lo;
+    }
+  };
+  uint32_t vmax_u = 0u;
+#pragma unroll 1
+  for (int dy = 0; dy < 2; ++dy) {
+    f32x16 acc2[2][2];  // [dx][i]
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[dx][i][r] = 0.f;
+    f32x2_t g[8];
+    fetch(dy, 0, g);
+    __syncthreads();  // the LDS is free (main loop / the previous pass's reads done)
+    stage(g, 0);
+    fetch(dy, 16, g);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int b = c & 1;
+      __syncthreads();  // buffer b (and A') complete; buffer b ^ 1's reads (chunk c - 1) done
+      const char* lz = smem + b * UNITS * 16;
+      f16x8 fa[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int P = 0; P < 2; ++P)
+          fa[i][P] = *reinterpret_cast<const f16x8*>(la + (((c * 2 + P) * 2 + h) * 64 + 32 * i + l32) * 16);
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int u = ((h * 2 + dx) * 4 + wn) * 32 + l32;
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(lz + u * 16);
+        const f16x8 bl = *reinterpret_cast<const f16x8*>(lz + (UNITS / 2 + u) * 16);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          acc2[dx][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][0], bh, acc2[dx][i], 0, 0, 0);
+          acc2[dx][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][0], bl, acc2[dx][i], 0, 0, 0);
+          acc2[dx][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][1], bh, acc2[dx][i], 0, 0, 0);
+        }
+      }
+      if (c + 1 < 4) {
+        stage(g, b ^ 1);
+        if (c + 2 < 4) fetch(dy, 16 * (c + 2), g);
+      }
+    }
+    // 3. y = A.z + the routed d (8-B stores of the dx pair)
+    const uint32_t sel0 = dy ? sel[2] : sel[0], sel1 = dy ? sel[3] : sel[1];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = acc[i][0][r] * descale;
+        const uint32_t bit = 1u << (16 * i + r);
+        const float v0 = acc2[0][i][r] * down + ((sel0 & bit) ? d : 0.f);
+        const float v1 = acc2[1][i][r] * down + ((sel1 & bit) ? d : 0.f);
+        vmax_u = max(vmax_u, max(__float_as_uint(v0) & 0x7fffffffu,
+                                 __float_as_uint(v1) & 0x7fffffffu));
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t dv = {__float_as_uint(v0), __float_as_uint(v1)};
+        __builtin_amdgcn_raw_buffer_store_b64(
+            dv, ry, (uint32_t)corow(i, r) * pb2 + win + (uint32_t)dy * wrow, 0, 0);
+      }
+  }
+  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
+}
+
 // S = 2: the stride-2 downsampling convs (raw input, loader mode LM_S2): the tile's
 // input window is (2 TH + 1) x (2 TW + 1) and output pixel (ty, tx) reads its taps at
 // window position (2 ty + kh, 2 tx + kw)
@@ -654,7 +830,7 @@ struct C16up {
 };
 
 template <int TW, int LM, int P2, int NI, int WM = 1>
-__global__ void __launch_bounds__(256 * WM, WM == 2 ? 1 : ((NI == 1 && TW <= 32) ? 3 : 2))
+__global__ void __launch_bounds__(256 * WM, WM == 2 ? 1 : ((NI == 1 && TW <= 32 && P2 == 0) ? 3 : 2))
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   // PAR: the zero-dilated data gradient (a stride-2 conv's input gradient) on 64 x 4 tiles
   // whose N-tiles are output parity classes: of the 9 taps x 3 kernel rows only those that
@@ -666,7 +842,9 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   constexpr int NT = C::NT;
   constexpr int KS = UPP ? 2 : 3;  // K steps per 16-channel chunk
   constexpr bool RP = TW == 64 && NI == 2 && !PAR && !UPP;  // row-pair tiles (pool / unpool)
-  static_assert(P2 == 0 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
+  static_assert(P2 == 0 || P2 == 4 || NI == 2, "the Gram-backward phase assumes 256-pixel tiles");
+  static_assert(P2 != 4 || (TW == 32 && NI == 1 && WM == 1 && LM == STX_IN_RAW),
+                "the unpool epilogue takes 32 x 4 tiles of a raw-input conv");
   static_assert(P2 != 2, "1x1 mode: v1 kernel");
   static_assert(WM == 1 || P2 == 0, "WM = 2: plain epilogue only");
   constexpr int BM = C::BM;
@@ -1042,6 +1220,10 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     } else if constexpr (WM == 2) {
       // (eligibility: launch16v2 / launch16_gram128)
       conv_epilogue_plain<TW, NI, RP, false, WM>(acc, p, et, descale, smem);
+    } else if constexpr (P2 == 4) {
+      // (eligibility: stx_conv2d -- stx_conv_params.unpool_out)
+      static_assert(2 * 2 * 2 * 2 * 128 * 16 + 16384 <= C::LDS_BYTES, "unpool epilogue buffers fit");
+      epi_unpool_gram<TW>(acc, p, et, descale, smem);
     } else if constexpr (P2 == 3) {
       // (eligibility: launch16v2 -- data gradient + mask + the phase, bias / out_amax only)
       const int ez = amax_exp(read_amax(p.p2_amax));
@@ -1585,7 +1767,16 @@ weight_compose16_kernel(const float* __restrict__ A, int pitch, const float* __r
   }
 }
 
+// stx_conv_params.unpool_out (validated by stx_conv2d): 32 x 4 tiles of d, 64 couts
+static int launch16_unpool(const stx_conv_params& p, hipStream_t st) {
+  const int tiles_x = p.wo / 32, ntiles = tiles_x * (p.ho / 4);
+  hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<32, STX_IN_RAW, 4, 1>), dim3(ntiles, 1, p.n),
+                     dim3(256), 0, st, p, tiles_x, ntiles);
+  return check_launch("stx_conv2d(f16x3 v2 + unpool / Gram-backward epilogue)");
+}
+
 int conv2d_f16x3(const stx_conv_params& p, hipStream_t st) {
+  if (p.unpool_out) return launch16_unpool(p, st);
   switch (p.stride == 2 ? LM_S2 : p.in_mode) {
     case STX_IN_RAW: return dispatch16_tw<STX_IN_RAW>(p, st);
     case STX_IN_RELU: return dispatch16_tw<STX_IN_RELU>(p, st);

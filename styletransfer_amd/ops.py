@@ -448,7 +448,8 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
            relu_out=False, wt_batch_stride=0, hv=None, wv=None, p2_z=None, p2_coef=None,
            p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
            pool_out=None, p2_amax=None, split_1x1=False, gram_part=None, pool_sum=False,
-           gram_cnt=None, p2_wt_amax=None, mse_ref=None, mse_parts=None, wt16_up=None):
+           gram_cnt=None, p2_wt_amax=None, mse_ref=None, mse_parts=None, wt16_up=None,
+           unpool_out=None):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
     up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
@@ -465,7 +466,11 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
     mse_ref/mse_parts (with gram_part, cout 128): the content target and the per-tile
     content / feature MSE sums of the output (stx_conv_params.mse_ref).
     wt16_up=(slab, w_amax) from conv_weight_prep16_up: an upsampled-input conv with the
-    plain epilogue runs as four output-parity 2x2 convs (stx_conv_params.wt16_up)."""
+    plain epilogue runs as four output-parity 2x2 convs (stx_conv_params.wt16_up).
+    unpool_out=(z, coef, coef_amax, z_amax, scale): the result d is the gradient of
+    maxpool2x2(relu(z)) and `out` [n][cout][2 ho][2 wo] receives unpool(d) [z > 0] +
+    scale * A[n] . z (stx_conv_params.unpool_out: a pooled tap's ReLU+MaxPool and Gram
+    backward in this data gradient's epilogue)."""
     _req(x, "x")
     n, c, h, w = x.shape
     assert c == cin, (c, cin)
@@ -476,6 +481,12 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
     if pool_sum:
         assert pool_out is not None and out is None, "pool_sum writes pool_out only"
         out = pool_out  # p.y must be set; the kernel never writes it with pool_sum
+    elif unpool_out is not None:
+        oshape = (n, cout, 2 * ho, 2 * wo)
+        if out is None:
+            out = torch.empty(oshape, device=x.device, dtype=torch.float32)
+        _req(out, "out")
+        assert out.shape == oshape, (out.shape, oshape)
     elif out is None:
         out = torch.empty((n, cout, ho, wo), device=x.device, dtype=torch.float32)
     else:
@@ -513,6 +524,16 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
         assert ks == 1 and wt_batch_stride and mask is None and p2_z is None
         p.wt16 = 1
         p.in_amax = (in_amax if in_amax is not None else amax(x)).data_ptr()
+    if unpool_out is not None:
+        uz, ucoef, ucoef_amax, uz_amax, uscale = unpool_out
+        _req(uz, "unpool z")
+        assert uz.shape == out.shape and ucoef.shape[-1] == op, (uz.shape, ucoef.shape, op)
+        p.unpool_out = 1
+        p.up_z, p.p2_wt, p.p2_scale = uz.data_ptr(), ucoef.data_ptr(), _p(uscale)
+        p.p2_c = uz.shape[1]
+        p.p2_wt_batch_stride = ucoef.shape[-1] * ucoef.shape[-2]
+        p.p2_amax = (uz_amax if uz_amax is not None else amax(uz)).data_ptr()
+        p.p2_wt_amax = ucoef_amax.data_ptr()
     if in_amax is not None and not p.in_amax:
         # the non-split kernels that take an input bound (convfew.hip's split 64->3
         # data gradient) read it too; the others ignore it

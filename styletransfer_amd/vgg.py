@@ -380,7 +380,8 @@ _SIDE = {}
 
 # amax groups of LossState.amax: 0..5 forward, 6..10 backward split-conv inputs, 11 / 12
 # max|A| of the taps whose Gram backward is a data-gradient conv's second phase
-COEF_AMAX_SLOT = {0: 11, 2: 12, 4: 14}  # max|A| per tap (split phase / composed weights)
+COEF_AMAX_SLOT = {0: 11, 1: 15, 2: 12, 4: 14}  # max|A| per tap (split phase / composed
+# weights / conv2_1^T's unpool epilogue)
 COMPOSE_AMAX_SLOT = 13  # max|A5 W| of the composed conv3_1 data-gradient weights
 
 
@@ -467,9 +468,17 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
                      p2_amax=slot(am, 3), p2_wt_amax=ca[2])
     # -> grad wrt pool(relu Z2)
     n2 = (B, 64, z[1].shape[2] // 2, z[1].shape[3] // 2)
-    dp1 = feat.dgrad(2, dz3, buf("dp1", n2), in_amax=slot(am, 8))
-    dz2 = ops.gram_bwd_fused(st.coef[1], z[1], out=buf("dz2", z[1].shape), acc_scale=s(1),
-                             up_dp=dp1, out_amax=slot(am, 9), z_amax=slot(am, 2) if sp else None)
+    if sp and ca[1] is not None and n2[3] % 32 == 0 and n2[2] % 4 == 0 and \
+            N.knob("STX_UNPOOL_FUSE", "1") != "0":
+        # dZ2 = unpool(dP1) [Z2 > 0] + A2 Z2 in conv2_1^T's epilogue: dP1 never reaches HBM
+        dz2 = feat.dgrad(2, dz3, buf("dz2", z[1].shape), in_amax=slot(am, 8),
+                         out_amax=slot(am, 9),
+                         unpool_out=(z[1], st.coef[1], ca[1], slot(am, 2), s(1)))
+    else:
+        dp1 = feat.dgrad(2, dz3, buf("dp1", n2), in_amax=slot(am, 8))
+        dz2 = ops.gram_bwd_fused(st.coef[1], z[1], out=buf("dz2", z[1].shape), acc_scale=s(1),
+                                 up_dp=dp1, out_amax=slot(am, 9),
+                                 z_amax=slot(am, 2) if sp else None)
     # dZ1 = conv1_2^T(dZ2)*[Z1>0] + A1 Z1
     dz1 = feat.dgrad(1, dz2, buf("dz1", z[0].shape), mask=z[0], p2_z=z[0],
                      p2_coef=st.coef[0], p2_scale=s(0), in_amax=slot(am, 9), p2_amax=slot(am, 1),

@@ -37,7 +37,7 @@ def test_struct_mirrors_match_the_library():
     from styletransfer_amd import _native as N
     out = (C.c_longlong * 12)()
     assert N.lib().stx_abi_layout(C.cast(out, C.c_void_p), 12) == 12
-    mirrors = [(N.ConvParams, "wt16_up"), (N.WprepJob, "pad_"), (N.LossParts, "k"),
+    mirrors = [(N.ConvParams, "unpool_out"), (N.WprepJob, "pad_"), (N.LossParts, "k"),
                (N.GramFinJob, "coef_amax"), (N.PGradJob, "pad_"), (N.ImageMeta, "tmp_offset")]
     for i, (S, last) in enumerate(mirrors):
         assert S._fields_[-1][0] == last, S
@@ -239,6 +239,9 @@ def test_parity_and_gram128_host_contracts():
         p = N.ConvParams(in_mode=N.STX_IN_UPSAMPLE2, hv=hv, wv=wv, ho=hv, wo=wv, wt16_up=96,
                          **base)
         assert L.stx_conv2d(C.byref(p), None) == 1001 and b"wt16_up" in L.stx_last_error_string()
+    # unpool_out: only a raw-input split data gradient with cout 64 and its operands
+    p = N.ConvParams(in_mode=N.STX_IN_RAW, hv=32, wv=32, ho=32, wo=32, unpool_out=1, **base)
+    assert L.stx_conv2d(C.byref(p), None) == 1001 and b"unpool_out" in L.stx_last_error_string()
     p = N.ConvParams(in_mode=N.STX_IN_RAW, hv=32, wv=64, ho=32, wo=64, gram_part=112,
                      mse_ref=128, mse_parts=144, **dict(base, w=64))
     assert L.stx_conv2d(C.byref(p), None) == 1001 and b"mse_ref" in L.stx_last_error_string()
