@@ -149,16 +149,19 @@ typedef struct stx_conv_params {
    * four output-parity 2x2 convs over the un-upsampled input (64 x 8 output tiles of one
    * row parity per block); plain epilogue only (bias, relu_out, out_amax), wo > 32. */
   const void* wt16_up;
-  /* unpool_out = 1 (split path, raw-input 3x3 stride-1 data gradient, cout 64, wo % 32 == 0,
-   * ho % 4 == 0): the conv's result d (the gradient of a MaxPool2d(2,2)(ReLU(.)) output,
-   * [n][64][ho][wo]) is not stored; y receives, at full resolution [n][64][2ho][2wo],
+  /* unpool_out = 1 (split path, raw-input 3x3 stride-1 data gradient, cout C = 64 or 128,
+   * wo % 32 == 0, ho % 4 == 0): the conv's result d (the gradient of a MaxPool2d(2,2)(ReLU
+   * (.)) output, [n][C][ho][wo]) is not stored; y receives, at full resolution
+   * [n][C][2ho][2wo],
    *   y[co][Y][X] = d[co][Y/2][X/2] * [(Y, X) is the first max of its 2x2 window of relu(z)]
    *                 * [z[co][Y][X] > 0]  +  s * sum_c A[n][c][co] z[c][Y][X]
-   * with z = up_z, A = p2_wt (p2_wt_batch_stride, pitch cout_pad), p2_c = 64, s = *p2_scale
-   * (or 1), p2_amax >= max|z| and p2_wt_amax >= max|A| -- the ReLU+MaxPool backward and
-   * the Gram backward of the pooled VGG tap (stransfer/network.py:110-123 through
-   * :264-275) in the producing conv's epilogue, so d never reaches HBM.  out_amax receives
-   * max|y|; no bias / mask / aux / accumulate / relu_out / pool / Gram outputs. */
+   *                 (+ aux_scale * aux[co][Y][X] with aux, full resolution)
+   * with z = up_z, A = p2_wt (p2_wt_batch_stride, pitch cout_pad = C), p2_c = C, s =
+   * *p2_scale (or 1), p2_amax >= max|z| and p2_wt_amax >= max|A| -- the ReLU+MaxPool
+   * backward and the Gram backward (+ the folded content term) of the pooled VGG tap
+   * (stransfer/network.py:110-164 through :264-275) in the producing conv's epilogue, so d
+   * never reaches HBM.  out_amax receives max|y|; no bias / mask / accumulate / relu_out /
+   * pool / Gram outputs. */
   int unpool_out;
 } stx_conv_params;
 

@@ -716,15 +716,15 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   }
   if (p.unpool_out &&
       (!p.wt16 || p.wt16 == (const void*)1 || !p.w_amax || !p.in_amax || p.wt16_up || p.ks != 3 ||
-       p.pad != 1 || p.stride != 1 || p.in_mode != STX_IN_RAW || p.cin < 16 || p.cout != 64 ||
-       p.cout_pad != 64 || p.p2_c != 64 || !p.up_z || !p.p2_wt || !p.p2_amax || !p.p2_wt_amax ||
-       p.p2_z || p.up_dp || p.mask || p.aux || p.accumulate || p.acc_scale || p.relu_out ||
-       p.bias || p.pool_out || p.pool_sum || p.gram_part || p.gram_cnt || p.mse_ref ||
-       p.wt_batch_stride || p.wo % 32 || p.ho % 4 ||
-       4LL * 64 * 4 * p.ho * p.wo >= (long long)BUF_OOB / 2)) {
+       p.pad != 1 || p.stride != 1 || p.in_mode != STX_IN_RAW || p.cin < 16 ||
+       (p.cout != 64 && p.cout != 128) || p.cout_pad != p.cout || p.p2_c != p.cout || !p.up_z ||
+       !p.p2_wt || !p.p2_amax || !p.p2_wt_amax || p.p2_z || p.up_dp || p.mask || p.accumulate ||
+       p.acc_scale || p.relu_out || p.bias || p.pool_out || p.pool_sum || p.gram_part ||
+       p.gram_cnt || p.mse_ref || p.wt_batch_stride || p.wo % 32 || p.ho % 4 ||
+       4LL * p.cout * 4 * p.ho * p.wo >= (long long)BUF_OOB / 2)) {
     set_error("stx_conv2d: unpool_out needs a raw-input split 3x3 stride-1 data gradient with "
-              "cout 64, wo %% 32 == 0, ho %% 4 == 0, up_z / p2_wt / p2_amax / p2_wt_amax, p2_c "
-              "64, and no other epilogue term");
+              "cout 64 or 128 (= p2_c = cout_pad), wo %% 32 == 0, ho %% 4 == 0, up_z / p2_wt / "
+              "p2_amax / p2_wt_amax, and no epilogue term but aux");
     return STX_E_INVALID;
   }
   if ((p.mse_ref || p.mse_parts) && (!p.mse_ref || !p.mse_parts || !p.gram_part || p.cout != 128)) {

@@ -372,10 +372,14 @@ __device__ __forceinline__ void epi_unpool_gram(f32x16 (&acc)[2][1], const stx_c
   static_assert(TW == 32, "32 x 4 tiles of d");
   constexpr int UNITS = 2 * 2 * 2 * 128;  // [P][cg][dx][4 rows x 32]: one 16 KB buffer
   const int tid = threadIdx.x, h = t.h, l32 = t.l32, wn = t.wn;
+  const int C = p.cout, nch = C / 16;     // z channels (= cout: 64 or 128), K chunks
   const int H2 = 2 * p.ho, W2 = 2 * p.wo;
   const uint32_t pb2 = (uint32_t)H2 * (uint32_t)W2 * 4u;
-  const auto rz = make_srd(p.up_z + (size_t)t.n * 64 * H2 * W2, 64u * pb2);
-  const auto ry = make_srd(p.y + (size_t)t.n * 64 * H2 * W2, 64u * pb2);
+  const size_t img = (size_t)t.n * C * H2 * W2, blk = img + (size_t)t.co0 * H2 * W2;
+  const auto rz = make_srd(p.up_z + img, (uint32_t)C * pb2);   // all channels (A . z)
+  const auto rw = make_srd(p.up_z + blk, 64u * pb2);           // this block's 64 (windows)
+  const auto ry = make_srd(p.y + blk, 64u * pb2);
+  const auto rx = make_srd(p.aux ? p.aux + blk : p.y + blk, p.aux ? 64u * pb2 : 0u);
   const int Y0 = 2 * (t.ty0 + wn), X0 = 2 * (t.tx0 + l32);
   const uint32_t win = (uint32_t)(Y0 * W2 + X0) * 4u, wrow = (uint32_t)W2 * 4u;
   auto corow = [&](int i, int r) { return i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
@@ -387,8 +391,8 @@ __device__ __forceinline__ void epi_unpool_gram(f32x16 (&acc)[2][1], const stx_c
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const uint32_t o = (uint32_t)corow(i, r) * pb2 + win;
-      top[r] = buf_ld2(rz, o);
-      bot[r] = buf_ld2(rz, o + wrow);
+      top[r] = buf_ld2(rw, o);
+      bot[r] = buf_ld2(rw, o + wrow);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -413,15 +417,14 @@ __device__ __forceinline__ void epi_unpool_gram(f32x16 (&acc)[2][1], const stx_c
   const int ez = amax_exp(read_amax(p.p2_amax));
   const float sa = __builtin_ldexpf(s2, 15 - ea), sz = __builtin_ldexpf(1.f, 15 - ez);
   const float down = __builtin_ldexpf(1.f, ea + ez - 30);
-  // A' (64 x 64, both passes) split once into LDS after the z buffers: [chunk][P][cg][co]
-  // 16-B units (8 channels of one cout), 16 KB; thread t -> (chunk, cg, co) = the 512
-  // units' first / second half
+  // A'[c][co0 .. co0 + 63] (C x 64, both passes) split once into LDS after the z buffers:
+  // [chunk][P][cg][co] 16-B units (8 channels of one cout), C x 256 B; thread t -> the
+  // units (channel group of 8, cout) t, t + 256, ...
   char* la = smem + 2 * UNITS * 16;
   {
-    const float* __restrict__ A = p.p2_wt + (size_t)t.n * p.p2_wt_batch_stride;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int u = tid + 256 * k, co = u & 63, cg8 = u >> 6;  // channel group of 8 (0..7)
+    const float* __restrict__ A = p.p2_wt + (size_t)t.n * p.p2_wt_batch_stride + t.co0;
+    for (int u = tid; u < C * 8; u += 256) {
+      const int co = u & 63, cg8 = u >> 6;  // channel group of 8
       float av[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) av[e] = A[(size_t)(8 * cg8 + e) * p.cout_pad + co];
@@ -477,8 +480,7 @@ __device__ __forceinline__ void epi_unpool_gram(f32x16 (&acc)[2][1], const stx_c
     __syncthreads();  // the LDS is free (main loop / the previous pass's reads done)
     stage(g, 0);
     fetch(dy, 16, g);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < nch; ++c) {
       const int b = c & 1;
       __syncthreads();  // buffer b (and A') complete; buffer b ^ 1's reads (chunk c - 1) done
       const char* lz = smem + b * UNITS * 16;
@@ -500,21 +502,34 @@ __device__ __forceinline__ void epi_unpool_gram(f32x16 (&acc)[2][1], const stx_c
           acc2[dx][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i][1], bh, acc2[dx][i], 0, 0, 0);
         }
       }
-      if (c + 1 < 4) {
+      if (c + 1 < nch) {
         stage(g, b ^ 1);
-        if (c + 2 < 4) fetch(dy, 16 * (c + 2), g);
+        if (c + 2 < nch) fetch(dy, 16 * (c + 2), g);
       }
     }
-    // 3. y = A.z + the routed d (8-B stores of the dx pair)
+    // 3. y = A.z (+ aux_scale aux) + the routed d (8-B stores of the dx pair); the aux
+    // loads all go out before the first store (vmcnt counts stores too)
     const uint32_t sel0 = dy ? sel[2] : sel[0], sel1 = dy ? sel[3] : sel[1];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+    for (int rh = 0; rh < 16; rh += 8) {
+      f32x2_t xv[16];
+      if (p.aux) {
+#pragma unroll
+        for (int r = rh; r < rh + 8; ++r)
+          xv[r] = buf_ld2(rx, (uint32_t)corow(i, r) * pb2 + win + (uint32_t)dy * wrow);
+      }
+#pragma unroll
+      for (int r = rh; r < rh + 8; ++r) {
         const float d = acc[i][0][r] * descale;
         const uint32_t bit = 1u << (16 * i + r);
-        const float v0 = acc2[0][i][r] * down + ((sel0 & bit) ? d : 0.f);
-        const float v1 = acc2[1][i][r] * down + ((sel1 & bit) ? d : 0.f);
+        float v0 = acc2[0][i][r] * down + ((sel0 & bit) ? d : 0.f);
+        float v1 = acc2[1][i][r] * down + ((sel1 & bit) ? d : 0.f);
+        if (p.aux) {
+          v0 = fmaf(p.aux_scale, xv[r].x, v0);
+          v1 = fmaf(p.aux_scale, xv[r].y, v1);
+        }
         vmax_u = max(vmax_u, max(__float_as_uint(v0) & 0x7fffffffu,
                                  __float_as_uint(v1) & 0x7fffffffu));
         typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
@@ -522,6 +537,7 @@ __device__ __forceinline__ void epi_unpool_gram(f32x16 (&acc)[2][1], const stx_c
         __builtin_amdgcn_raw_buffer_store_b64(
             dv, ry, (uint32_t)corow(i, r) * pb2 + win + (uint32_t)dy * wrow, 0, 0);
       }
+    }
   }
   if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
 }
@@ -792,7 +808,7 @@ conv3x3_f16x3_kernel(stx_conv_params p, int tiles_x) {
 // cin >= 16 only.
 // WM = 2: one 8-wave block for 128 couts (waves 4..7 the second 64), the halo of the
 // pixel tile staged once for both cout halves (the 128-channel layers)
-template <int TW, int NI, int WM = 1>
+template <int TW, int NI, int WM = 1, int MINLDS = 0>
 struct C16v2 {
   static constexpr int NT = 256 * WM;
   static constexpr int BM = 64 * WM, NPIX = 128 * NI, TH = NPIX / TW;
@@ -805,9 +821,11 @@ struct C16v2 {
   static constexpr int WB = WU * 16;                   // one weight buffer
   static constexpr int LOOP_BYTES = 2 * HB + 2 * WB;
   // (the 128-channel fused Gram planes of a WM = 2, 64 x 4 tile: 135 KB, one block per CU)
-  static constexpr int LDS_BYTES =
+  static constexpr int LDS_BYTES0 =
       WM == 2 && TW == 64 && NI == 2 && LOOP_BYTES < GramPlanes128::BYTES ? GramPlanes128::BYTES
                                                                            : LOOP_BYTES;
+  // (MINLDS: the unpool epilogue's z buffers and A' for 128 channels, 64 KB)
+  static constexpr int LDS_BYTES = LDS_BYTES0 < MINLDS ? MINLDS : LDS_BYTES0;
   static_assert(WU % NT == 0, "weight units per thread");
   static_assert(16 * NPIX * 4 + 16 * BM * 4 <= LDS_BYTES, "phase-2 staging fits");
   static_assert(TW != 64 || NI != 2 || GramPlanes<256>::BYTES <= LDS_BYTES, "Gram planes fit");
@@ -838,7 +856,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   constexpr bool PAR = LM == STX_IN_DILATE2 && TW == 64 && NI == 2 && WM == 1 && P2 == 0;
   // UPP: the nearest-x2 upsampled input as four output-parity 2x2 convs (C16up)
   constexpr bool UPP = LM == STX_IN_UPSAMPLE2 && TW == 64 && NI == 2 && WM == 1 && P2 == 0;
-  using C = std::conditional_t<UPP, C16up, C16v2<TW, NI, WM>>;
+  using C = std::conditional_t<UPP, C16up, C16v2<TW, NI, WM, P2 == 4 ? 65536 : 0>>;
   constexpr int NT = C::NT;
   constexpr int KS = UPP ? 2 : 3;  // K steps per 16-channel chunk
   constexpr bool RP = TW == 64 && NI == 2 && !PAR && !UPP;  // row-pair tiles (pool / unpool)
@@ -1222,7 +1240,8 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
       conv_epilogue_plain<TW, NI, RP, false, WM>(acc, p, et, descale, smem);
     } else if constexpr (P2 == 4) {
       // (eligibility: stx_conv2d -- stx_conv_params.unpool_out)
-      static_assert(2 * 2 * 2 * 2 * 128 * 16 + 16384 <= C::LDS_BYTES, "unpool epilogue buffers fit");
+      static_assert(2 * 2 * 2 * 2 * 128 * 16 + 128 * 256 <= C::LDS_BYTES,
+                    "unpool epilogue buffers fit");
       epi_unpool_gram<TW>(acc, p, et, descale, smem);
     } else if constexpr (P2 == 3) {
       // (eligibility: launch16v2 -- data gradient + mask + the phase, bias / out_amax only)
@@ -1770,7 +1789,7 @@ weight_compose16_kernel(const float* __restrict__ A, int pitch, const float* __r
 // stx_conv_params.unpool_out (validated by stx_conv2d): 32 x 4 tiles of d, 64 couts
 static int launch16_unpool(const stx_conv_params& p, hipStream_t st) {
   const int tiles_x = p.wo / 32, ntiles = tiles_x * (p.ho / 4);
-  hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<32, STX_IN_RAW, 4, 1>), dim3(ntiles, 1, p.n),
+  hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<32, STX_IN_RAW, 4, 1>), dim3(ntiles, p.cout / 64, p.n),
                      dim3(256), 0, st, p, tiles_x, ntiles);
   return check_launch("stx_conv2d(f16x3 v2 + unpool / Gram-backward epilogue)");
 }

@@ -225,7 +225,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         st = LossState()
     dev = x.device
     if st.amax is None:
-        st.amax = torch.zeros(16 * N.STX_AMAX_SLOTS, device=dev, dtype=torch.float32)
+        st.amax = torch.zeros(17 * N.STX_AMAX_SLOTS, device=dev, dtype=torch.float32)
     elif not st.amax_cleared:
         st.amax.zero_()
     st.amax_cleared = False  # (the Gatys engine's Adam launch clears it for the next pass)
@@ -321,7 +321,7 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         if l == CONTENT_CONV and not fused_mse:  # content, feature, feature-mse: one pass
             ops.mse(z, c4, mode=2, out=st.losses[5:8])
 
-    st.coef_amax = [None] * 5
+    st.coef_amax = [None] * 5  # (per style tap)
 
     def on_layer(l, z):
         # the style loss of layer l (and the content/feature losses at conv2_2) run on
@@ -380,8 +380,8 @@ _SIDE = {}
 
 # amax groups of LossState.amax: 0..5 forward, 6..10 backward split-conv inputs, 11 / 12
 # max|A| of the taps whose Gram backward is a data-gradient conv's second phase
-COEF_AMAX_SLOT = {0: 11, 1: 15, 2: 12, 4: 14}  # max|A| per tap (split phase / composed
-# weights / conv2_1^T's unpool epilogue)
+COEF_AMAX_SLOT = {0: 11, 1: 15, 2: 12, 3: 16, 4: 14}  # max|A| per tap (split phase /
+# composed weights / the unpool epilogues of conv2_1^T and conv3_1^T)
 COMPOSE_AMAX_SLOT = 13  # max|A5 W| of the composed conv3_1 data-gradient weights
 
 
@@ -430,8 +430,17 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
     # COMPOSE_AMAX_SLOT
     sp = feat.wt16[1] is not None  # split kernels in use
     n4 = (B, 128, z[3].shape[2] // 2, z[3].shape[3] // 2)
-    # (STX_COMPOSE=0: the Gram backward of conv3_1 as its own 1x1 pass, dZ5 = A5 Z5; A/B)
     ca = st.coef_amax if st.coef_amax else [None] * 5
+    # dZ4 = unpool(dP2)[Z4 > 0] + A4 Z4 (+ the folded content term) in the epilogue of the
+    # conv that produces dP2 (stx_conv_params.unpool_out): dP2 never reaches HBM
+    dz4 = None
+    up4 = None
+    if sp and ca[3] is not None and n4[3] % 32 == 0 and n4[2] % 4 == 0 and \
+            N.knob("STX_UNPOOL_FUSE", "1") != "0":
+        up4 = dict(unpool_out=(z[3], st.coef[3], ca[3], slot(am, 4), s(3)),
+                   aux=st.c4 if folded else None, aux_scale=-st.alpha,
+                   out_amax=slot(am, 7) if folded else None)
+    # (STX_COMPOSE=0: the Gram backward of conv3_1 as its own 1x1 pass, dZ5 = A5 Z5; A/B)
     if sp and B == 1 and feat.wtT16[4] is not None and ca[4] is not None and \
             N.knob("STX_COMPOSE", "1") != "0":
         # conv3_1's output feeds only its style loss, so dP2 = conv3_1^T(A5 Z5) =
@@ -442,19 +451,29 @@ def loss_backward(feat: VGGFeatures, st: LossState, g=None, dx=None, feature_gra
             st.coef[4], ca[4], feat.w[4], feat.wtT16[4][1], slot(am, COMPOSE_AMAX_SLOT),
             scale=s(4), out=sc.get("compose5"))
         cout, cin = VGG_CONV_SHAPES[4]
-        dp2 = ops.conv2d(z[4], None, cout, cin, 3, out=buf("dp2", n4),
-                         wt16=(sc["compose5"], slot(am, COMPOSE_AMAX_SLOT)), in_amax=slot(am, 5))
+        if up4:
+            dz4 = ops.conv2d(z[4], None, cout, cin, 3, out=buf("dz4", z[3].shape),
+                             wt16=(sc["compose5"], slot(am, COMPOSE_AMAX_SLOT)),
+                             in_amax=slot(am, 5), **up4)
+        else:
+            dp2 = ops.conv2d(z[4], None, cout, cin, 3, out=buf("dp2", n4),
+                             wt16=(sc["compose5"], slot(am, COMPOSE_AMAX_SLOT)),
+                             in_amax=slot(am, 5))
     else:
         # conv3_1 output: dZ5 = A5 Z5
         dz5 = ops.gram_bwd_fused(st.coef[4], z[4], out=buf("dz5", z[4].shape), acc_scale=s(4),
                                  out_amax=slot(am, 6), z_amax=slot(am, 5) if sp else None)
         # -> grad wrt pool(relu Z4)
-        dp2 = feat.dgrad(4, dz5, buf("dp2", n4), in_amax=slot(am, 6))
+        if up4:
+            dz4 = feat.dgrad(4, dz5, buf("dz4", z[3].shape), in_amax=slot(am, 6), **up4)
+        else:
+            dp2 = feat.dgrad(4, dz5, buf("dp2", n4), in_amax=slot(am, 6))
     # dZ4 = unpool(dP2)*[Z4>0] + A4 Z4 (+ content)
-    dz4 = ops.gram_bwd_fused(st.coef[3], z[3], out=buf("dz4", z[3].shape), acc_scale=s(3),
-                             up_dp=dp2, aux=st.c4 if folded else None, aux_scale=-st.alpha,
-                             out_amax=slot(am, 7) if folded else None,
-                             z_amax=slot(am, 4) if sp else None)
+    if dz4 is None:
+        dz4 = ops.gram_bwd_fused(st.coef[3], z[3], out=buf("dz4", z[3].shape), acc_scale=s(3),
+                                 up_dp=dp2, aux=st.c4 if folded else None, aux_scale=-st.alpha,
+                                 out_amax=slot(am, 7) if folded else None,
+                                 z_amax=slot(am, 4) if sp else None)
     n = z[3].numel()
     dz4_amax = slot(am, 7) if folded else None
     if not folded:

@@ -769,20 +769,25 @@ def test_composed_dgrad_weights(dev, hw, scale):
     print(f"composed {rel(y, ref):.2e}, unfused {rel(y2, ref):.2e}")
 
 
-@pytest.mark.parametrize("shape", [(1, 32, 32), (2, 64, 32), (1, 256, 256)])
+@pytest.mark.parametrize("shape", [(1, 32, 32, 64, False), (2, 64, 32, 64, False),
+                                   (1, 256, 256, 64, False), (1, 32, 32, 128, True),
+                                   (1, 128, 128, 128, True), (2, 64, 32, 128, False)])
 def test_unpool_gram_epilogue(dev, shape):
     """stx_conv_params.unpool_out: the pooled tap's ReLU+MaxPool backward and Gram backward
     in the epilogue of the data gradient that produces the pooled gradient (conv2_1^T in
     the Gatys iteration): dZ2 = unpool(d)[Z2 > 0] + s A Z2 with d never stored.  Against
     the unfused launches (conv2_1^T, then the streaming Gram backward) and fp64; ties in the
     2x2 windows (quantised z) exercise the first-maximum rule; out_amax is max|y|."""
-    b, h, w = shape                       # d is h x w, z is 2h x 2w
-    z = rnd(b, 64, 2 * h, 2 * w, dev=dev, seed=301, scale=2, shift=-1)
+    b, h, w, c, with_aux = shape          # d is h x w, z is 2h x 2w (c channels)
+    z = rnd(b, c, 2 * h, 2 * w, dev=dev, seed=301, scale=2, shift=-1)
     z = (z * 8).round() / 8               # quantised: equal values inside many windows
-    dz3 = rnd(b, 128, h, w, dev=dev, seed=302, scale=2e-3, shift=-1e-3)
-    wgt = rnd(128, 64, 3, 3, dev=dev, seed=303, scale=0.2, shift=-0.1)  # conv2_1: 64 -> 128
-    t = rnd(b, 64, 64, dev=dev, seed=304, scale=1e-2)
-    ws = torch.empty(N.lib().stx_gram_ws(b, 64, 4 * h * w), device=dev, dtype=torch.uint8)
+    # the producing conv: conv2_1^T (128 -> 64) or conv3_1^T (256 -> 128)
+    dz3 = rnd(b, 2 * c, h, w, dev=dev, seed=302, scale=2e-3, shift=-1e-3)
+    wgt = rnd(2 * c, c, 3, 3, dev=dev, seed=303, scale=0.2, shift=-0.1)
+    t = rnd(b, c, c, dev=dev, seed=304, scale=1e-2)
+    aux = rnd(b, c, 2 * h, 2 * w, dev=dev, seed=305) if with_aux else None
+    asc = -0.37 if with_aux else 0.0
+    ws = torch.empty(N.lib().stx_gram_ws(b, c, 4 * h * w), device=dev, dtype=torch.uint8)
     fin = ops.FinalizeBatch()
     _, coef = ops.style_loss(z, t[0], weight=2.0, defer_ws=ws, fin=fin)
     ca = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
@@ -793,10 +798,11 @@ def test_unpool_gram_epilogue(dev, shape):
     w16 = ops.conv_weight_prep16(wgt, transpose=True)
     zam = ops.amax(z)
     am = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
-    y = ops.conv2d(dz3, wtT, 128, 64, 3, wt16=w16, out_amax=am,
+    y = ops.conv2d(dz3, wtT, 2 * c, c, 3, wt16=w16, out_amax=am, aux=aux, aux_scale=asc,
                    unpool_out=(z, coef, ca, zam, s2))
-    d = ops.conv2d(dz3, wtT, 128, 64, 3, wt16=w16)
-    ref = ops.gram_bwd_fused(coef, z, up_dp=d, acc_scale=s2, z_amax=zam)
+    d = ops.conv2d(dz3, wtT, 2 * c, c, 3, wt16=w16)
+    ref = ops.gram_bwd_fused(coef, z, up_dp=d, acc_scale=s2, z_amax=zam, aux=aux,
+                             aux_scale=asc)
     torch.cuda.synchronize()
     assert y.shape == z.shape
     assert rel(y, ref) < 2e-6, rel(y, ref)
@@ -804,10 +810,12 @@ def test_unpool_gram_epilogue(dev, shape):
     if b * h * w <= 4096:  # fp64 of the same math
         z64, d64 = z.double().cpu(), d.double().cpu()
         rz = z64.clamp_min(0)
-        win = rz.reshape(b, 64, h, 2, w, 2).permute(0, 1, 2, 4, 3, 5).reshape(b, 64, h, w, 4)
+        win = rz.reshape(b, c, h, 2, w, 2).permute(0, 1, 2, 4, 3, 5).reshape(b, c, h, w, 4)
         first = torch.nn.functional.one_hot(win.argmax(-1), 4).double()  # first max
-        routed = (first * d64.unsqueeze(-1)).reshape(b, 64, h, w, 2, 2)
-        up = routed.permute(0, 1, 2, 4, 3, 5).reshape(b, 64, 2 * h, 2 * w) * (z64 > 0)
-        A = coef.double().cpu()[:, :64, :64]
+        routed = (first * d64.unsqueeze(-1)).reshape(b, c, h, w, 2, 2)
+        up = routed.permute(0, 1, 2, 4, 3, 5).reshape(b, c, 2 * h, 2 * w) * (z64 > 0)
+        A = coef.double().cpu()[:, :c, :c]
         gz = float(s2) * torch.einsum("bcd,bchw->bdhw", A, z64)
+        if with_aux:
+            gz = gz + asc * aux.double().cpu()
         assert rel(y, up + gz) < 2e-6, rel(y, up + gz)
