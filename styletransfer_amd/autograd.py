@@ -427,6 +427,10 @@ class FastStLossFn(torch.autograd.Function):
         y = _c(y)
         dev = y.device
         st = V.LossState()
+        # the amax groups of the loss network from the training step's arena (zeroed by its
+        # one fill at the step's start) instead of a fill of their own
+        st.amax = ops.ARENA.take_span(V.LOSS_AMAX_GROUPS, dev)
+        st.amax_cleared = st.amax is not None
         st.losses = torch.empty(V.N_LOSSES + 2, device=dev, dtype=torch.float32)
         st.fmean = st.losses[6:8]
         tvg = torch.empty_like(y)  # MINUS the TV gradient (see backward)

@@ -69,6 +69,9 @@ class FastStTrainer:
             dist.broadcast(self.flat, src=self._src(), group=self.pg)
             bump_versions(self.params)
         self.opt = FlatAdam(self.flat, self.flat_grad, lr=lr, params=self.params)
+        # the backward's seed gradient d total / d total = 1, allocated once (autograd's
+        # default seed is a fill launch per step)
+        self._one = torch.ones((), device=self.device, dtype=torch.float32)
         self.vgg_weights = vgg_weights
         self._graph = None  # (replay, static batch, static loss) of train_step
         from .layers import Conv2d
@@ -116,7 +119,7 @@ class FastStTrainer:
         try:
             y = self.itn(batch)
             total = self._total(batch, y)
-            total.backward()
+            total.backward(self._one)
             ops.PGRADS.flush()
         finally:
             ops.SIDE.end()
@@ -263,7 +266,7 @@ class VideoTrainer(FastStTrainer):
         try:
             y = self.itn(x6)
             total = self._video_total(batch, y, old_c, old_s)
-            total.backward()
+            total.backward(self._one)
             ops.PGRADS.flush()
         finally:
             ops.SIDE.end()

@@ -225,7 +225,8 @@ def loss_forward(feat: VGGFeatures, targets, x, c4, st: LossState | None = None,
         st = LossState()
     dev = x.device
     if st.amax is None:
-        st.amax = torch.zeros(17 * N.STX_AMAX_SLOTS, device=dev, dtype=torch.float32)
+        st.amax = torch.zeros(LOSS_AMAX_GROUPS * N.STX_AMAX_SLOTS, device=dev,
+                              dtype=torch.float32)
     elif not st.amax_cleared:
         st.amax.zero_()
     st.amax_cleared = False  # (the Gatys engine's Adam launch clears it for the next pass)
@@ -380,6 +381,7 @@ _SIDE = {}
 
 # amax groups of LossState.amax: 0..5 forward, 6..10 backward split-conv inputs, 11 / 12
 # max|A| of the taps whose Gram backward is a data-gradient conv's second phase
+LOSS_AMAX_GROUPS = 17  # LossState.amax: the groups below
 COEF_AMAX_SLOT = {0: 11, 1: 15, 2: 12, 3: 16, 4: 14}  # max|A| per tap (split phase /
 # composed weights / the unpool epilogues of conv2_1^T and conv3_1^T)
 COMPOSE_AMAX_SLOT = 13  # max|A5 W| of the composed conv3_1 data-gradient weights
