@@ -54,7 +54,8 @@ typedef struct stx_conv_params {
   const float* wt;    /* prepped weights [cin_pad*ks*ks][cout_pad] (stx_conv_weight_prep);
                          may be NULL when wt16 selects the split path */
   const float* bias;  /* [cout] or NULL */
-  float* y;           /* output [n][cout][ho][wo] */
+  float* y;           /* output [n][cout][ho][wo]; NULL with pool_out (split path, plain
+                         epilogue): only pool_out is written */
   const float* mask;  /* NULL or [n][cout][ho][wo]: value *= (mask > 0)   (ReLU backward) */
   const float* aux;   /* NULL or [n][cout][ho][wo]: value += aux_scale*aux */
   float aux_scale;

@@ -631,7 +631,7 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
   int cinp, coutp;
   if (stx_conv_weight_dims(p.cin, p.cout, p.ks, &cinp, &coutp)) return STX_E_INVALID;
   if (p.cin_pad != cinp || p.cout_pad != coutp || p.n <= 0 || p.ho <= 0 || p.wo <= 0 ||
-      p.pad < 0 || p.in_mode < 0 || p.in_mode > 4 || !p.x || !p.y ||
+      p.pad < 0 || p.in_mode < 0 || p.in_mode > 4 || !p.x || (!p.y && !p.pool_out) ||
       (!p.wt && (!p.wt16 || p.wt16 == (const void*)1))) {
     set_error("stx_conv2d: invalid params (cin_pad %d/%d cout_pad %d/%d n %d ho %d wo %d)",
               p.cin_pad, cinp, p.cout_pad, coutp, p.n, p.ho, p.wo);
@@ -712,6 +712,14 @@ extern "C" int stx_conv2d(const stx_conv_params* pp, void* stream) {
        p.p2_z || p.pool_out || p.pool_sum || p.gram_part)) {
     set_error("stx_conv2d: wt16_up needs an upsampled-input split conv (3x3 stride 1, wo > 32, "
               "virtual size exactly 2h x 2w) with the plain epilogue (bias / relu_out / out_amax)");
+    return STX_E_INVALID;
+  }
+  // y = NULL with pool_out: only the pooled output is written (the VGG content target's
+  // conv1_2: nothing reads Z2 there) -- the split path's plain epilogue only
+  if (!p.y && (!p.wt16 || p.wt16 == (const void*)1 || p.pool_sum || p.mask || p.aux ||
+               p.accumulate || p.acc_scale || p.up_dp || p.p2_z || p.gram_part || p.mse_ref ||
+               p.unpool_out || p.stride != 1)) {
+    set_error("stx_conv2d: y = NULL (pool_out only) needs the split path's plain epilogue");
     return STX_E_INVALID;
   }
   if (p.unpool_out &&

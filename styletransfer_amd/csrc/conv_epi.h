@@ -514,7 +514,9 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
   const int co_w = t.co0 + t.wm * 64;
   const int rows = max(0, p.cout - co_w);
   const uint32_t pb = (uint32_t)plane * 4u;
-  const auto ry = make_srd(p.y + ((size_t)t.n * p.cout + co_w) * plane, (uint32_t)rows * pb);
+  // (y = NULL: pool_out only -- a zero-size descriptor drops every full-resolution store)
+  const auto ry = make_srd(p.y ? p.y + ((size_t)t.n * p.cout + co_w) * plane : p.pool_out,
+                           p.y ? (uint32_t)rows * pb : 0u);
   const auto raux = make_srd(AUX ? p.aux + ((size_t)t.n * p.cout + co_w) * plane : p.y,
                              AUX ? (uint32_t)rows * pb : 0u);
   uint32_t vo[NI];

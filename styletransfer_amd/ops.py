@@ -449,7 +449,7 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
            p2_scale=None, up_dp=None, up_z=None, wt16=None, in_amax=None, out_amax=None,
            pool_out=None, p2_amax=None, split_1x1=False, gram_part=None, pool_sum=False,
            gram_cnt=None, p2_wt_amax=None, mse_ref=None, mse_parts=None, wt16_up=None,
-           unpool_out=None):
+           unpool_out=None, pool_only=False):
     """stx_conv2d on x [n][cin][h][w] with a prepped slab `wt`.
     p2_z/p2_coef: fused Gram-backward phase (value += s2 * A[n] . p2_z[n]);
     up_dp/up_z: fused ReLU+MaxPool2d backward epilogue.
@@ -470,7 +470,9 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
     unpool_out=(z, coef, coef_amax, z_amax, scale): the result d is the gradient of
     maxpool2x2(relu(z)) and `out` [n][cout][2 ho][2 wo] receives unpool(d) [z > 0] +
     scale * A[n] . z (stx_conv_params.unpool_out: a pooled tap's ReLU+MaxPool and Gram
-    backward in this data gradient's epilogue)."""
+    backward in this data gradient's epilogue).
+    pool_only (with pool_out, split path): the full-resolution output is not written
+    (stx_conv_params.y = NULL); returns pool_out."""
     _req(x, "x")
     n, c, h, w = x.shape
     assert c == cin, (c, cin)
@@ -564,6 +566,10 @@ def conv2d(x, wt, cin, cout, ks, stride=1, pad=None, in_mode=N.STX_IN_RAW, bias=
             assert gram_cnt.is_cuda and gram_cnt.dtype == torch.int32 and \
                 gram_cnt.numel() >= n * ng, (gram_cnt.dtype, gram_cnt.numel(), n * ng)
             p.gram_cnt = gram_cnt.data_ptr()
+    if pool_only:
+        assert pool_out is not None and not pool_sum and gram_part is None, "pool_only"
+        p.y = None
+        out = pool_out
     check(lib().stx_conv2d(C.byref(p), _stream()), "stx_conv2d")
     return out
 

@@ -138,7 +138,7 @@ class VGGFeatures:
         return ops.conv_gram_groups(cin, cout, ho, wo, n=n, in_mode=self._run_mode(l, wo))
 
     def forward(self, x, upto=5, outs=None, amax=None, pools=None, on_layer=None, grams=None,
-                content=None):
+                content=None, keep=None):
         """[Z1..Z_upto] (pre-ReLU conv outputs).  amax: device [>=5] slots, zeroed by
         the caller; slot l+1 receives max|Z_l| (the next split conv's input scale);
         each slot is an amax group of N.STX_AMAX_SLOTS floats (slot(amax, k)).
@@ -147,7 +147,10 @@ class VGGFeatures:
         None): conv l writes its fused Gram partials there (gram_tiles); a (slab,
         counters) pair instead: the in-kernel group sums (gram_groups) after the per-tile
         scratch.  content=(c4, parts): the content tap's conv (fused Gram, 128 channels)
-        also writes its content / feature MSE sums against c4 into parts."""
+        also writes its content / feature MSE sums against c4 into parts.  keep (a set of
+        layer indices, or None = all): the layers whose full output is needed; a layer
+        outside it that writes a fused pooled output writes that alone (its entry in the
+        returned list is the pooled tensor)."""
         zs, cur, pin = [], x, None
         for l in range(upto):
             cout, cin = VGG_CONV_SHAPES[l]
@@ -166,6 +169,9 @@ class VGGFeatures:
                 if pools is not None:
                     pools[l] = pin
                 kw["pool_out"] = pin
+                if keep is not None and l not in keep and outs is None and grams is None \
+                        and on_layer is None and self.wt16[l] is not None:
+                    kw["pool_only"] = True
             if grams is not None and grams[l] is not None:
                 if isinstance(grams[l], tuple):
                     kw["gram_part"], kw["gram_cnt"] = grams[l]
@@ -515,7 +521,8 @@ def content_target(feat: VGGFeatures, content, out=None, amax=None):
     """C4 = conv2_2 output of the content image (ContentLoss target, pre-ReLU).
     amax: optional zeroed slot vector (>= 5 groups): each conv then emits its output's
     max|.| for the next split conv instead of that conv re-reading its input."""
-    return feat.forward(content.contiguous(), 4, amax=amax)[3] if out is None else \
+    # (conv1_2's Z2 is read by nothing here: only its pooled output is written)
+    return feat.forward(content.contiguous(), 4, amax=amax, keep={3})[3] if out is None else \
         feat.forward(content.contiguous(), 4, [None, None, None, out], amax=amax)[3]
 
 

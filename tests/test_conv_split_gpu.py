@@ -819,3 +819,27 @@ def test_unpool_gram_epilogue(dev, shape):
         if with_aux:
             gz = gz + asc * aux.double().cpu()
         assert rel(y, up + gz) < 2e-6, rel(y, up + gz)
+
+
+@pytest.mark.parametrize("case", [(1, 64, 64, 256, 256), (8, 64, 64, 64, 96)])
+def test_pool_only_output(dev, case):
+    """stx_conv_params.y = NULL with pool_out (the VGG content target's conv1_2): the pooled
+    output equals the one the full launch writes, bit for bit, and no full-resolution
+    output is written (a sentinel buffer stays untouched)."""
+    n, cin, cout, h, w = case
+    x = rnd(n, cin, h, w, dev=dev, seed=311, scale=2, shift=-1)
+    wgt = rnd(cout, cin, 3, 3, dev=dev, seed=312, scale=0.2, shift=-0.1)
+    b = rnd(cout, dev=dev, seed=313)
+    wt, w16 = ops.conv_weight_prep(wgt), ops.conv_weight_prep16(wgt)
+    am1 = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    am2 = torch.zeros(N.STX_AMAX_SLOTS, device=dev)
+    p1 = torch.empty(n, cout, h // 2, w // 2, device=dev)
+    p2 = torch.full_like(p1, 7.0)
+    y = ops.conv2d(x, wt, cin, cout, 3, in_mode=N.STX_IN_RELU, bias=b, wt16=w16, pool_out=p1,
+                   out_amax=am1)
+    r = ops.conv2d(x, wt, cin, cout, 3, in_mode=N.STX_IN_RELU, bias=b, wt16=w16, pool_out=p2,
+                   out_amax=am2, pool_only=True)
+    torch.cuda.synchronize()
+    assert r is p2
+    assert torch.equal(p1, p2)
+    assert float(am1.max()) == float(am2.max()) == float(y.abs().max())
