@@ -195,13 +195,45 @@ def test_adam(dev):
     m = torch.zeros_like(p)
     v = torch.zeros_like(p)
     step = torch.zeros(1, dtype=torch.int32, device=dev)
-    ws = torch.empty(16, dtype=torch.float32, device=dev)
+    ws = torch.zeros(16, dtype=torch.float32, device=dev)
     for it in range(3):
         gi = g * (it + 1)
         pr.grad = gi.cpu()
         opt.step()
         ops.adam_step(p, gi, m, v, step, ws)
     assert int(step.item()) == 3
+    assert rel(p, pr.detach().to(dev)) < 1e-6
+
+
+@pytest.mark.parametrize("n", [4096 * 1024 + 5, 3 * 512 * 512])
+def test_adam_multiblock_graph(dev, n):
+    """stx_adam_step_clear with many blocks and a grid-stride tail (n above the 4096-block
+    cap, and not a multiple of 4), replayed from a captured hipGraph: torch.optim.Adam's
+    update on every step, the device counter after each, the clear buffer zeroed."""
+    p = rnd(n, dev=dev, seed=65)
+    g = rnd(n, dev=dev, seed=66, scale=2, shift=-1)
+    pr = p.clone().cpu().requires_grad_()
+    opt = torch.optim.Adam([pr], lr=0.01)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    step = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = torch.zeros(16, dtype=torch.float32, device=dev)
+    clear = torch.full((300,), 2.0, device=dev)
+    ops.adam_step(p, g, m, v, step, ws, lr=0.01, clear=clear)  # eager first step
+    pr.grad = g.cpu()
+    opt.step()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        ops.adam_step(p, g, m, v, step, ws, lr=0.01, clear=clear)
+    for it in range(4):
+        clear.fill_(1.0)
+        graph.replay()
+        pr.grad = g.cpu()
+        opt.step()
+        torch.cuda.synchronize()
+        assert int(step.item()) == it + 2
+        assert float(clear.abs().max()) == 0.0
     assert rel(p, pr.detach().to(dev)) < 1e-6
 
 
@@ -215,7 +247,7 @@ def test_adam_step_clear(dev):
         g = rnd(n, dev=dev, seed=64, scale=2, shift=-1)
         st = [(p.clone(), torch.zeros_like(p), torch.zeros_like(p),
                torch.zeros(1, dtype=torch.int32, device=dev),
-               torch.empty(16, dtype=torch.float32, device=dev)) for _ in range(2)]
+               torch.zeros(16, dtype=torch.float32, device=dev)) for _ in range(2)]
         clear = torch.full((nclear,), 3.0, device=dev)
         for it in range(2):
             ops.adam_step(st[0][0], g * (it + 1), *st[0][1:])
