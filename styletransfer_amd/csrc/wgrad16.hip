@@ -43,7 +43,7 @@ struct Wg16 {
   int ncot, ncit, nsplit, steps, steps_per_split;
   int cout32, cin32;
   int ci2;  // cout <= 32: a wave takes 32 couts x 64 cins (two cin tiles), not 64 x 32
-  int lds;  // wgrad16_lds_kernel geometry (cout 64/128, 64-cin tiles, 1 block per CU)
+  int lds;  // wgrad16_lds_kernel geometry (cout 64/128, 64-cin tiles, 1 block per CU; 2: K2)
 };
 
 // Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one L2): renumber
@@ -691,15 +691,27 @@ wgrad16up_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dw, Wg
 // CIB = cins per block (64; 128 for cout = 64, so each wave still owns two 32 x 32
 // (co, ci) tiles: 18 MFMAs per barrier instead of 9)
 // RL: ReLU input (compile time: no per-element select)
-template <int WCO, bool UP, int PF, int CIB = 64, bool RL = false>  // WCO = couts / 32; UP:
-__global__ void __launch_bounds__(256, 1)  // nearest x2 upsampled input; PF + 1 steps in flight
-wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                   float* __restrict__ ws, const float* __restrict__ x_amax,
-                   const float* __restrict__ dy_amax, Wg16 g) {
+// K2: two groups of four waves per block (512 threads) take alternate 16-pixel steps of the
+// block's K range, each with its own double-buffered V images and accumulators, so two waves
+// per SIMD share the MFMA pipe (the 4-wave block has one: its staging, barrier and operand
+// latency leave the pipe idle); group 1's sums are added to group 0's through LDS at the
+// end (fixed order), the partial slab and the split count stay those of the 4-wave block.
+template <int WCO, bool UP, int PF, int CIB = 64, bool RL = false, bool K2 = false>
+__global__ void __launch_bounds__(K2 ? 512 : 256, 1)  // WCO = couts / 32; UP: nearest x2
+wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,  // upsampled
+                   float* __restrict__ ws, const float* __restrict__ x_amax,   // input; PF + 1
+                   const float* __restrict__ dy_amax, Wg16 g) {               // steps in flight
   constexpr int NCI = CIB / 64;            // staged cin rows per thread
   constexpr int NPAIR = WCO * 2 * NCI / 4;  // (co tile, ci tile) pairs per wave
-  __shared__ __attribute__((aligned(16))) char vimg[2][3 * 2 * 2 * CIB * 16];  // 2 x 12|24 KB
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NG = K2 ? 2 : 1;           // step groups
+  static_assert((PF + 1) % 2 == 0, "ring slot k stages into V image k & 1");
+  constexpr int IMG = 3 * 2 * 2 * CIB * 16;  // one V image: 12|24 KB
+  constexpr int RED = K2 ? 4 * NPAIR * 3 * 16 * 64 * 4 : 0;  // group 1's accumulators
+  constexpr int LDSB = 2 * NG * IMG > RED ? 2 * NG * IMG : RED;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int gk = K2 ? (int)(threadIdx.x >> 8) : 0;  // this thread's step group
+  auto vimg = [&](int b) { return smem + (b * NG + gk) * IMG; };
   const int h = lane >> 5, l32 = lane & 31;
   int unit = xcd_block(blockIdx.x, gridDim.x);
   const int cit = unit % g.ncit;           // CIB-cin tile
@@ -740,11 +752,14 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   auto load = [&](Ld& t) {
     const int n = ln, y = ly, x0 = lxs * 16;
     const bool live = lleft-- > 0;
-    if (++lxs == wsteps) {
-      lxs = 0;
-      if (++ly == H) {
-        ly = 0;
-        ++ln;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {  // (this group's next step: NG steps on)
+      if (++lxs == wsteps) {
+        lxs = 0;
+        if (++ly == H) {
+          ly = 0;
+          ++ln;
+        }
       }
     }
     const uint32_t oa = (uint32_t)(((n * g.cout) * H + y) * W + x0) * 4u + la;
@@ -840,27 +855,52 @@ wgrad16_lds_kernel(const float* __restrict__ x, const float* __restrict__ dy,
   const int s0 = split * g.steps_per_split;
   const int nst = min(g.steps, s0 + g.steps_per_split) - s0;  // >= 1
   {
-    const int r0 = s0 / wsteps;
-    lxs = s0 - r0 * wsteps;
+    const int sg = s0 + gk;  // this group's first step (K2: steps sg, sg + 2, ...)
+    const int r0 = sg / wsteps;
+    lxs = sg - r0 * wsteps;
     ln = r0 / H;
     ly = r0 - ln * H;
-    lleft = nst;
+    lleft = (nst - gk + NG - 1) / NG;
   }
+  const int nit = (nst + NG - 1) / NG;  // steps per group (both groups: the same barriers)
   // steps run in groups of PF + 1 (a ring slot per step); a ragged last group computes
   // on zeros
   Ld ring[PF + 1];
 #pragma unroll
   for (int k = 0; k <= PF; ++k) load(ring[k]);
-  stage(ring[0], vimg[0]);
+  stage(ring[0], vimg(0));
   __syncthreads();
-  for (int s = 0; s < nst; s += PF + 1) {
+  for (int s = 0; s < nit; s += PF + 1) {
 #pragma unroll
     for (int k = 0; k <= PF; ++k) {
-      stage(ring[(k + 1) % (PF + 1)], vimg[(k + 1) & 1]);  // the next step's V image
-      compute(ring[k], vimg[k & 1]);
+      stage(ring[(k + 1) % (PF + 1)], vimg((k + 1) & 1));  // the next step's V image
+      compute(ring[k], vimg(k & 1));
       load(ring[k]);  // step s + k + PF + 1
       __syncthreads();  // lgkmcnt(0) + s_barrier: the global loads stay in flight
     }
+  }
+  if constexpr (K2) {
+    // group 1's accumulators -> LDS (the images are dead after the loop's last barrier);
+    // group 0 adds them (acc0 + acc1) and writes the partial
+    float* red = reinterpret_cast<float*>(smem);
+    if (gk == 1) {
+#pragma unroll
+      for (int pi = 0; pi < NPAIR; ++pi)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            red[(((wave * NPAIR + pi) * 3 + kw) * 16 + r) * 64 + lane] = acc[pi][kw][r];
+    }
+    __syncthreads();
+    if (gk == 1) return;
+#pragma unroll
+    for (int pi = 0; pi < NPAIR; ++pi)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          acc[pi][kw][r] += red[(((wave * NPAIR + pi) * 3 + kw) * 16 + r) * 64 + lane];
   }
   // partial [split][kh*3+kw][co (cout32)][ci (cin32)], descaled (exact)
 #pragma unroll
@@ -894,6 +934,10 @@ static bool lds_on_64() {
 
 typedef void (*Wg16Kernel)(const float*, const float*, float*, const float*, const float*, Wg16);
 
+constexpr int WG16_K2_PF = 3;  // the K2 blocks' load ring
+
+static int wg16_threads(const Wg16& g) { return g.lds == 2 ? 512 : 256; }
+
 static int wg16_pf() {
   static const int pf = STX_KNOB("STX_WG16_PF", 4);
   return pf;
@@ -915,6 +959,9 @@ static Wg16Kernel wg16_kernel(const Wg16& g) {
       return up ? wgrad16_lds_kernel<2, true, 3> : wgrad16_lds_kernel<2, false, 3>;
     }
 #endif
+    if (g.lds == 2)  // (K2: cout 128, not upsampled -- wg16_plan)
+      return g.mode == STX_IN_RELU ? wgrad16_lds_kernel<4, false, WG16_K2_PF, 64, true, true>
+                                   : wgrad16_lds_kernel<4, false, WG16_K2_PF, 64, false, true>;
     if (g.mode == STX_IN_RELU) return wgrad16_lds_kernel<4, false, 3, 64, true>;
     return up ? wgrad16_lds_kernel<4, true, 3> : wgrad16_lds_kernel<4, false, 3>;
   }
@@ -928,13 +975,13 @@ static Wg16Kernel wg16_kernel(const Wg16& g) {
   return wgrad16_kernel<4, false>;
 }
 
-// resident blocks of `k` over the whole device (CUs x blocks per CU at 256 threads);
+// resident blocks of `k` over the whole device (CUs x blocks per CU at `threads`);
 // 256 x 1 when no device answers (the CPU-only build host sizing a workspace)
-static int wg16_slots_query(Wg16Kernel k) {
+static int wg16_slots_query(Wg16Kernel k, int threads) {
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k), 256,
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k), threads,
                                                    0) != hipSuccess ||
       cus <= 0 || per <= 0) {
     (void)hipGetLastError();
@@ -943,13 +990,13 @@ static int wg16_slots_query(Wg16Kernel k) {
   return cus * per;
 }
 
-static int wg16_slots(Wg16Kernel k) {  // cached per kernel (plans run at every launch)
+static int wg16_slots(Wg16Kernel k, int threads) {  // cached per kernel (plans run at every launch)
   static std::mutex mu;
   static std::unordered_map<const void*, int> cache;
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache.find(reinterpret_cast<const void*>(k));
   if (it != cache.end()) return it->second;
-  const int v = wg16_slots_query(k);
+  const int v = wg16_slots_query(k, threads);
   cache.emplace(reinterpret_cast<const void*>(k), v);
   return v;
 }
@@ -985,6 +1032,9 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   g.steps = n * hv * (wv / 16);
   g.lds = wg16_lds_on() && (cout == 128 || (cout == 64 && lds_on_64())) && cin % 64 == 0 &&
           (in_mode == STX_IN_RAW || in_mode == STX_IN_RELU || in_mode == STX_IN_UPSAMPLE2);
+  // (read per plan: A/B in one process; both forms run one block per CU, so the split
+  // count and the workspace are the same)
+  if (g.lds && cout == 128 && in_mode != STX_IN_UPSAMPLE2 && STX_KNOB("STX_WG16_K2", 1)) g.lds = 2;
   // the upsampled input as parity classes (4 instead of 9 MACs per output; STX_WG16_UPP=0:
   // the upsampled-row kernels): 32-column steps over the output rows of one row parity
   static const bool upp_on = STX_KNOB("STX_WG16_UPP", 1) != 0;
@@ -1002,7 +1052,7 @@ static bool wg16_plan(int n, int cin, int cout, int in_mode, int hv, int wv, Wg1
   // K splits: as many as fill whole rounds of resident blocks (a ragged last round of a
   // few blocks costs a full block duration: 513 blocks at 256 slots ran 3 rounds)
   static const int rounds = std::max(1, STX_KNOB("STX_WG16_ROUNDS", 1));
-  const int slots = rounds * wg16_slots(wg16_kernel(g));
+  const int slots = rounds * wg16_slots(wg16_kernel(g), wg16_threads(g));
   // blocks per split: (kh x cin tiles) for the LDS kernel; 4 units (waves) per block
   // (parity classes: 4 (ry, a) units per cout / cin tile pair instead of 3 kh)
   const int kq = g.mode == WG16_UPP ? 4 : 3;
@@ -1052,8 +1102,8 @@ extern "C" int stx_conv2d_wgrad16(const float* x, const float* dy, float* dw, in
   hipStream_t st = (hipStream_t)stream;
   const int units = g.nsplit * (g.mode == WG16_UPP ? 4 : 3) * g.ncot * g.ncit;
   const int blocks = g.lds ? g.nsplit * 3 * g.ncit : cdiv(units, 4);
-  hipLaunchKernelGGL(wg16_kernel(g), dim3(blocks), dim3(256), 0, st, x, dy, (float*)ws, x_amax,
-                     dy_amax, g);
+  hipLaunchKernelGGL(wg16_kernel(g), dim3(blocks), dim3(wg16_threads(g)), 0, st, x, dy,
+                     (float*)ws, x_amax, dy_amax, g);
   const long long total = (long long)cout * cin * 9;
   if (g.mode == WG16_UPP) {
     hipLaunchKernelGGL(wgrad16up_reduce_kernel, dim3((int)((total + 63) / 64)), dim3(256), 0, st,

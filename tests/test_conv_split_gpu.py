@@ -645,6 +645,11 @@ def test_split_gram_bwd_window_ties(dev, c):
                                   (1, 128, 128, 1, 16, N.STX_IN_RAW),
                                   (3, 192, 64, 10, 24, N.STX_IN_UPSAMPLE2),
                                   (1, 64, 128, 3, 16, N.STX_IN_RAW),
+                                  # cout 128: two step groups per block (K2), ReLU input,
+                                  # an odd step count (the second group's last step empty)
+                                  (2, 128, 128, 6, 32, N.STX_IN_RELU),
+                                  (3, 64, 128, 5, 48, N.STX_IN_RELU),
+                                  (1, 128, 128, 3, 16, N.STX_IN_RAW),
                                   # cout 64, cin % 128 == 0: 128 cins per block
                                   (2, 256, 64, 6, 16, N.STX_IN_RAW),
                                   (1, 128, 64, 5, 32, N.STX_IN_RELU),

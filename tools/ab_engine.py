@@ -6,12 +6,19 @@ bit against the first variant.
     python tools/ab_engine.py "STX_FIN_BATCH=0" "STX_FIN_BATCH=1" [--rounds 7] [--no-fast] [--no-gatys]
 
 A variant is a comma-separated list of NAME=VALUE settings applied while that variant's
-engine is built and captured (the library reads its switches at launch/capture time)."""
+engine is built and captured (the library reads its switches at launch/capture time).
+The process runs the A/B build of the library (`make AB=1`: libstx_ab.so, whose STX_KNOB
+switches read the environment; the product build compiles them to their defaults) unless
+STX_LIB names another."""
 import os
 import statistics
 import sys
 
 import torch
+
+# the library's own switches (STX_KNOB) read the environment only in the A/B build
+os.environ.setdefault("STX_LIB", os.path.join(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__))), "styletransfer_amd", "libstx_ab.so"))
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from styletransfer_amd import vgg as V  # noqa: E402
