@@ -37,6 +37,10 @@ constexpr int W9_SC = W9_TW + 8;        // staged S columns (4-column zero halo)
 constexpr int W9_SCP = W9_SC + 1;       // LDS row pitch (dwords)
 constexpr int W9_NS = 3;                // small-side channels (27 of 32 tile rows)
 constexpr int W9_PART = 9 * 32 * 32;    // floats per block partial [kh][row][l]
+constexpr int W9_LPF = 3;               // L steps in flight ahead of the MFMAs
+constexpr int W9_SB = 10;               // S staging: loads per thread per batch
+constexpr int W9_STG = (W9_NS * W9_SR * W9_SC + 255) / 256 + (W9_SB - 1) -
+                       ((W9_NS * W9_SR * W9_SC + 255) / 256 + W9_SB - 1) % W9_SB;  // 40
 
 struct Wf9 {
   const float* S;       // [n][ns][h][w]
@@ -88,13 +92,32 @@ __global__ void __launch_bounds__(256, 2) wgrad9_kernel(Wf9 p) {
     const int y0 = ry * W9_ROWS, x0 = tx * W9_TW;
     __syncthreads();  // previous unit's LDS reads are done
     {
-      const float* Sn = p.S + (size_t)n * p.ns * plane;
-      for (int idx = tid; idx < p.ns * W9_SR * W9_SC; idx += 256) {
-        const int s = idx / (W9_SR * W9_SC), rem = idx - s * (W9_SR * W9_SC);
-        const int rr = rem / W9_SC, cc = rem - rr * W9_SC;
-        const int y = y0 - 4 + rr, x = x0 - 4 + cc;
-        const float v = (y >= 0 && y < p.h && x >= 0 && x < p.w) ? Sn[(size_t)s * plane + y * p.w + x] : 0.f;
-        st[(s * W9_SR + rr) * W9_SCP + cc] = w9_pack(v * sS);
+      // the S window in batches of W9_SB elements per thread: every load of a batch issued
+      // before the first use (unconditional descriptor loads: outside the image or past
+      // ns channels read 0), then split and stored
+      const auto rs = make_srd(p.S + (size_t)n * p.ns * plane, (uint32_t)(p.ns * plane) * 4u);
+      const int nel = p.ns * W9_SR * W9_SC;
+#pragma unroll 1
+      for (int b0 = 0; b0 < W9_STG; b0 += W9_SB) {
+        float v[W9_SB];
+#pragma unroll
+        for (int j = 0; j < W9_SB; ++j) {
+          const int idx = tid + 256 * (b0 + j);
+          const int s = idx / (W9_SR * W9_SC), rem = idx - s * (W9_SR * W9_SC);
+          const int rr = rem / W9_SC, cc = rem - rr * W9_SC;
+          const int y = y0 - 4 + rr, x = x0 - 4 + cc;
+          const bool ok = idx < nel && y >= 0 && y < p.h && x >= 0 && x < p.w;
+          v[j] = buf_ld(rs, ok ? (uint32_t)(s * plane + y * p.w + x) * 4u : BUF_OOB);
+        }
+#pragma unroll
+        for (int j = 0; j < W9_SB; ++j) {
+          const int idx = tid + 256 * (b0 + j);
+          if (idx < nel) {
+            const int s = idx / (W9_SR * W9_SC), rem = idx - s * (W9_SR * W9_SC);
+            const int rr = rem / W9_SC, cc = rem - rr * W9_SC;
+            st[(s * W9_SR + rr) * W9_SCP + cc] = w9_pack(v[j] * sS);
+          }
+        }
       }
     }
     __syncthreads();
@@ -102,10 +125,27 @@ __global__ void __launch_bounds__(256, 2) wgrad9_kernel(Wf9 p) {
     if (y < p.h) {
       const float* Lrow = p.L + ((size_t)n * 32 + l32) * plane + (size_t)y * p.w;
       const int xend = min(W9_TW, p.w - x0);
-      for (int xs = 0; xs < xend; xs += 16) {
-        // B: L[l32][y][x0 + xs + 8h .. +7], split in registers
-        const f32x4 v0 = *reinterpret_cast<const f32x4*>(Lrow + x0 + xs + 8 * h);
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(Lrow + x0 + xs + 8 * h + 4);
+      // the L row in 16-pixel steps with the next W9_LPF steps' loads in flight (one
+      // exposed HBM latency per row instead of one per step); loads past the row's end
+      // read the row start (valid memory, never used)
+      f32x4 lr[W9_LPF + 1][2];
+#pragma unroll
+      for (int k = 0; k < W9_LPF; ++k) {
+        const int xo = 16 * k < xend ? 16 * k : 0;
+        lr[k][0] = *reinterpret_cast<const f32x4*>(Lrow + x0 + xo + 8 * h);
+        lr[k][1] = *reinterpret_cast<const f32x4*>(Lrow + x0 + xo + 8 * h + 4);
+      }
+      for (int xs = 0; xs < xend; xs += 16 * (W9_LPF + 1)) {
+#pragma unroll
+      for (int k = 0; k <= W9_LPF; ++k) {
+        {
+          const int xn = xs + 16 * (k + W9_LPF), xo = xn < xend ? xn : 0;
+          lr[(k + W9_LPF) % (W9_LPF + 1)][0] = *reinterpret_cast<const f32x4*>(Lrow + x0 + xo + 8 * h);
+          lr[(k + W9_LPF) % (W9_LPF + 1)][1] = *reinterpret_cast<const f32x4*>(Lrow + x0 + xo + 8 * h + 4);
+        }
+        if (xs + 16 * k >= xend) break;
+        // B: L[l32][y][x0 + xs + 16k + 8h .. +7], split in registers
+        const f32x4 v0 = lr[k][0], v1 = lr[k][1];
         f16x8_w9 bh, bl;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -115,7 +155,7 @@ __global__ void __launch_bounds__(256, 2) wgrad9_kernel(Wf9 p) {
           bl[e] = (_Float16)(v - (float)vh);
         }
         // A rows (s, kw) for each tap row kh: S at pixel (y + sgn(kh-4), x + sgn(kw-4))
-        const int cbase = xs + 8 * h + 4 + sgn * (kw - 4);
+        const int cbase = xs + 16 * k + 8 * h + 4 + sgn * (kw - 4);
 #pragma unroll
         for (int kh = 0; kh < 9; ++kh) {
           const int rr = wave + 4 + sgn * (kh - 4);
@@ -136,6 +176,7 @@ __global__ void __launch_bounds__(256, 2) wgrad9_kernel(Wf9 p) {
           acc[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[kh], 0, 0, 0);
           acc[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[kh], 0, 0, 0);
         }
+      }
       }
     }
   }
