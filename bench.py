@@ -529,7 +529,7 @@ def convert_leg(args, world, rank, dev):
                 itn(x)
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with ops.graph_capture(g):
                 y = itn(x)
             warm(g.replay, 1, dev)
             dt = timed(g.replay, n, world, dev)

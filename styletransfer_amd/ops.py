@@ -7,7 +7,9 @@ missing library raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import gc
 
 import os
 
@@ -128,6 +130,23 @@ SIDE = SideStream()
 
 def _scratch():
     return WS_SIDE if SIDE.on_side() else WS
+
+
+@contextlib.contextmanager
+def graph_capture(graph, **kw):
+    """torch.cuda.graph(graph, **kw) with Python's cyclic garbage collector held off for
+    the capture (after one collection): a CUDAGraph left in a reference cycle by earlier
+    work (a finished engine) and collected while this stream captures would be destroyed
+    mid-capture, which HIP refuses (hipErrorStreamCaptureUnsupported -> abort)."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(graph, **kw):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class AmaxArena:

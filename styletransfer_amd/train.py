@@ -159,9 +159,9 @@ class FastStTrainer:
         torch.cuda.current_stream(self.device).wait_stream(side)
         g_fb, g_up = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         # thread_local: a process-group watchdog thread may query its events meanwhile
-        with torch.cuda.graph(g_fb, capture_error_mode="thread_local"):
+        with ops.graph_capture(g_fb, capture_error_mode="thread_local"):
             loss = self._fwd_bwd(static)
-        with torch.cuda.graph(g_up, pool=g_fb.pool(), capture_error_mode="thread_local"):
+        with ops.graph_capture(g_up, pool=g_fb.pool(), capture_error_mode="thread_local"):
             self.opt.step()
         ptrs = self._param_ptrs()
         # every older graph refuses to replay (pointer check below): the slabs of

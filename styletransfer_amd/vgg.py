@@ -581,7 +581,7 @@ class GatysEngine:
                 self._iteration()
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with ops.graph_capture(self.graph):
             self._iteration()
         return self
 
@@ -669,11 +669,11 @@ class GatysLBFGS:
         torch.cuda.current_stream().wait_stream(s)
         b = self.opt._buf
         self.g_eval = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_eval):
+        with ops.graph_capture(self.g_eval):
             self._closure()
             b["host"].copy_(b["scal"], non_blocking=True)  # the scalars torch tests
         self.g_iter = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_iter, pool=self.g_eval.pool()):
+        with ops.graph_capture(self.g_iter, pool=self.g_eval.pool()):
             self.opt.direction(self.grad.view(-1))
             self._closure()
             b["host"].copy_(b["scal"], non_blocking=True)

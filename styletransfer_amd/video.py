@@ -158,7 +158,7 @@ class FrameEngine:
             # the first frame ran eagerly (allocations, prepped-weight caches); capture
             # records without executing, then replay runs this frame
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with ops.graph_capture(self.graph):
                 self._forward()
             self.graph.replay()
         else:

@@ -224,7 +224,7 @@ def test_adam_multiblock_graph(dev, n):
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=s):
+    with ops.graph_capture(graph, stream=s):
         ops.adam_step(p, g, m, v, step, ws, lr=0.01, clear=clear)
     for it in range(4):
         clear.fill_(1.0)
