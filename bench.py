@@ -16,6 +16,7 @@ the same line under "fast_st".  Inputs are resident in HBM before timing.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import platform
@@ -655,8 +656,29 @@ def launch(n):
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env))
-    rcs = [p.wait() for p in procs]
-    return max(rcs, key=abs)
+    # a rank that fails leaves the others waiting in a rendezvous or collective: stop
+    # them (the processes started here, by PID) and report the failure
+    rc = 0
+    while procs:
+        for p in list(procs):
+            r = p.poll()
+            if r is None:
+                continue
+            procs.remove(p)
+            if r != 0:
+                rc = r
+                for q in procs:
+                    q.terminate()
+                for q in procs:
+                    try:
+                        q.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                procs = []
+                break
+        time.sleep(0.2)
+    return rc
 
 
 def main():
@@ -681,10 +703,12 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         backend = os.environ.get("STX_BENCH_BACKEND", "nccl")
+        # (a bounded wait: a rank that never arrives fails the run instead of hanging it)
+        pg_timeout = datetime.timedelta(seconds=300)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout)
     N.lib()
     if args.fast_only:
         fs = fast_st_leg(args, world, rank, dev)

@@ -24,8 +24,9 @@ def test_bench_two_ranks_same_device():
     cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2",
            "--warmup", "1", "--fast-steps", "2", "--gatys-run-iters", "10", "--skip-cpu",
            "--skip-infer"]
-    r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=540)
-    assert r.returncode == 0, r.stderr[-3000:]
+    # (the ranks' stderr goes to this test's own output: a hang or crash shows where)
+    r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, text=True, timeout=540)
+    assert r.returncode == 0, r.stdout[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 alone prints the line
     res = json.loads(lines[0])
