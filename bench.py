@@ -157,20 +157,25 @@ def timed(fn, k, world, dev):
 WARM_MS = 150.0
 
 
-def warm(fn, w, dev):
-    """W untimed calls, then more until WARM_MS of wall time; returns the number made."""
+def warm(fn, w, dev, world=1):
+    """W untimed calls, then more until WARM_MS of wall time; returns the number made.
+    With world > 1 every rank makes the same number of calls (fn may hold a collective --
+    the fast_st step's all-reduce -- so a rank that stopped early would leave the others
+    waiting in it): after each round the ranks agree whether any still needs time."""
     t0 = time.perf_counter()
     n = 0
-    for _ in range(max(1, w)):
-        fn()
-        n += 1
-    torch.cuda.synchronize(dev)
-    while (time.perf_counter() - t0) * 1e3 < WARM_MS:
+    while True:
         for _ in range(max(1, w)):
             fn()
             n += 1
         torch.cuda.synchronize(dev)
-    return n
+        more = (time.perf_counter() - t0) * 1e3 < WARM_MS
+        if world > 1:
+            t = torch.tensor([1.0 if more else 0.0], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            more = bool(t.item() > 0)
+        if not more:
+            return n
 
 
 def event_avg_ms(fn, reps=10):
@@ -233,7 +238,7 @@ def gatys_leg(args, world, rank, dev):
         eng.step()
         torch.cuda.synchronize(dev)
         first_replay_ms = (time.perf_counter() - t0) * 1e3
-    nwarm = warm(eng.step, args.warmup, dev)
+    nwarm = warm(eng.step, args.warmup, dev, world)
     dt = timed(eng.step, args.steps, world, dev)
     rate = world * args.steps / dt
     run = None
@@ -442,12 +447,12 @@ def fast_st_leg(args, world, rank, dev, B=None, steps=None):
     graph = not args.no_graph and N.knob("STX_FAST_GRAPH", "1") != "0"
     if graph:  # hipGraph replays per training step (FastStTrainer.capture)
         replay, static, _ = tr.capture(batch, warmup=max(1, min(args.warmup, 2)))
-        warm(replay, 1, dev)
+        warm(replay, 1, dev, world)
         dt = timed(replay, steps, world, dev)
         return dict(rate=world * B * steps / dt, dt=dt, steps=steps, batch=B, graph=True)
     for _ in range(max(1, min(args.warmup, 2))):
         tr.step(batch)
-    warm(lambda: tr.step(batch), 1, dev)
+    warm(lambda: tr.step(batch), 1, dev, world)
     dt = timed(lambda: tr.step(batch), steps, world, dev)
     ips = world * B * steps / dt
     return dict(rate=ips, dt=dt, steps=steps, batch=B, graph=False)
@@ -490,7 +495,7 @@ def video_leg(args, world, rank, dev):
             i[0] += 1
         for _ in range(3):
             step()
-        warm(step, 1, dev)
+        warm(step, 1, dev, world)
         dt = timed(step, n, world, dev)
         out[mode] = dict(rate=world * n / dt, dt=dt)
         if mode == "hbm":
@@ -521,7 +526,7 @@ def convert_leg(args, world, rank, dev):
     with torch.no_grad():
         for _ in range(2):
             itn(x)
-        warm(lambda: itn(x), 1, dev)
+        warm(lambda: itn(x), 1, dev, world)
         dt_eager = timed(lambda: itn(x), n, world, dev)
         try:
             s = torch.cuda.Stream()
@@ -532,7 +537,7 @@ def convert_leg(args, world, rank, dev):
             g = torch.cuda.CUDAGraph()
             with ops.graph_capture(g):
                 y = itn(x)
-            warm(g.replay, 1, dev)
+            warm(g.replay, 1, dev, world)
             dt = timed(g.replay, n, world, dev)
             ref = itn(x)
             torch.cuda.synchronize(dev)
