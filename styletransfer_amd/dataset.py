@@ -49,7 +49,10 @@ class CocoDataset(Dataset):
 
     def __getitem__(self, idx):
         try:
-            img = Image.open(os.path.join(self.path, self.images[idx])).convert("RGB")
+            img = Image.open(os.path.join(self.path, self.images[idx]))
+            # (convert("RGB") of an RGB image is a full copy: the same pixels without it)
+            if img.mode != "RGB":
+                img = img.convert("RGB")
             if self.decode_only:
                 return np.asarray(img, dtype=np.uint8)
             return img_utils.image_loader_transform(img).cpu()
