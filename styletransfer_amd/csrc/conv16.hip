@@ -539,7 +539,7 @@ __device__ __forceinline__ void epi_unpool_gram(f32x16 (&acc)[2][1], const stx_c
       }
     }
   }
-  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u));
+  if (p.out_amax) block_max_to(p.out_amax, __uint_as_float(vmax_u), 4);  // (4 waves: K2 too)
 }
 
 // S = 2: the stride-2 downsampling convs (raw input, loader mode LM_S2): the tile's
@@ -847,8 +847,14 @@ struct C16up {
   static_assert(16 * NPIX * 4 + 16 * BM * 4 <= LDS_BYTES, "phase-2 staging fits");
 };
 
-template <int TW, int LM, int P2, int NI, int WM = 1>
-__global__ void __launch_bounds__(256 * WM, WM == 2 ? 1 : ((NI == 1 && TW <= 32 && P2 == 0) ? 3 : 2))
+// K2: two groups of four waves per block (512 threads) walk alternate 16-channel chunks of
+// the same tile with their own double-buffered halo / weight images and accumulators --
+// two waves per SIMD in a grid of one block per CU (the unpool launch of conv3_1^T at
+// B = 1); group 1 hands its sums to group 0 through LDS (acc0 + acc1, fixed order) and
+// ends, group 0 runs the epilogue (waves that have ended are not counted at a barrier).
+template <int TW, int LM, int P2, int NI, int WM = 1, bool K2 = false>
+__global__ void __launch_bounds__(256 * WM * (K2 ? 2 : 1),
+                                  (WM == 2 || K2) ? 1 : ((NI == 1 && TW <= 32 && P2 == 0) ? 3 : 2))
 conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   // PAR: the zero-dilated data gradient (a stride-2 conv's input gradient) on 64 x 4 tiles
   // whose N-tiles are output parity classes: of the 9 taps x 3 kernel rows only those that
@@ -865,10 +871,15 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
                 "the unpool epilogue takes 32 x 4 tiles of a raw-input conv");
   static_assert(P2 != 2, "1x1 mode: v1 kernel");
   static_assert(WM == 1 || P2 == 0, "WM = 2: plain epilogue only");
+  static_assert(!K2 || (WM == 1 && !PAR && !UPP), "K2: the plain 4-wave loop");
   constexpr int BM = C::BM;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  constexpr int NG = K2 ? 2 : 1;  // chunk groups
+  constexpr int LDSB = NG * C::LOOP_BYTES > C::LDS_BYTES ? NG * C::LOOP_BYTES : C::LDS_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
 
-  const int tid = threadIdx.x;
+  const int tid = K2 ? (int)(threadIdx.x & 255) : (int)threadIdx.x;
+  const int gk = K2 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8) : 0;
+  char* const sg = smem + gk * C::LOOP_BYTES;  // this group's loop buffers
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;  // cout half, pixel column of the wave
   const int h = lane >> 5, l32 = lane & 31;
@@ -886,8 +897,10 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   // apart instead of issuing their epilogue stores together (same-process A/B:
   // Gatys 679.6 -> 674.5 us per iteration, fast_st within noise)
   if ((blockIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
-  const int nchunks = cdiv(p.cin, 16);
+  // (K2: this group's chunks gch(c) = 2c + gk of an even count -- launch16_unpool)
+  const int nchunks = cdiv(p.cin, 16) / NG;
   const int nsteps = KS * nchunks;
+  auto gch = [&](int c) { return NG * c + gk; };  // global chunk of local chunk c
   // the parity-class forms with cout <= 32 in this block (the ITN's 32-channel layers:
   // the up conv to 32 channels, the first down conv's data gradient): the second 32-row
   // MFMA tile would only multiply the slab's zero padding
@@ -966,7 +979,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   float hv[C::NIT][8];
   f32x4 wreg[C::NWU];
   auto ld_halo = [&](int chunk, int r) {
-    const int c0 = chunk * 16;
+    const int c0 = gch(chunk) * 16;
     const auto rs = make_srd(xn + (size_t)c0 * plane_in, (uint32_t)(p.cin - c0) * pb);
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -981,7 +994,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
   auto st_halo = [&](int buf, int r) {
     const int idx = tid + r * NT;
     if (r + 1 < C::NIT || C::NITEM % NT == 0 || idx < C::NITEM) {
-      char* hb = smem + buf * C::HB;
+      char* hb = sg + buf * C::HB;
 #ifdef STX_DIAG_NOSPLIT
       // timing-only diagnostic build (make DIAG=1, numerically meaningless): the loader's
       // values stored as raw fp32 bits in the two planes -- no scale, no fp16 conversion
@@ -1017,7 +1030,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     }
   };
   auto ld_w = [&](int step) {  // step = chunk * KS + kh (UPP: ry)
-    const int chunk = step / KS, kh = step - KS * chunk;
+    const int chunk = gch(step / KS), kh = step - KS * (step / KS);
     const size_t base = UPP ? (size_t)upa * nchunks * chunk_bytes : 0;  // (UPP: parity a)
     const auto rw = make_srd(reinterpret_cast<const float*>(wt16 + base +
                                                             (size_t)chunk * chunk_bytes +
@@ -1027,7 +1040,7 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
     for (int q = 0; q < C::NWU; ++q) wreg[q] = buf_ld4(rw, woff[q]);
   };
   auto st_w = [&](int buf) {
-    char* wbp = smem + 2 * C::HB + buf * C::WB;
+    char* wbp = sg + 2 * C::HB + buf * C::WB;
 #pragma unroll
     for (int q = 0; q < C::NWU; ++q)
       *reinterpret_cast<f32x4*>(wbp + (tid + q * NT) * 16) = wreg[q];
@@ -1077,10 +1090,10 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
       for (int k = 0; k < KS; ++k) {
         const int s = KS * c + k;
         const int wbo = (s & 1) * C::WB;
-        const char* abase = smem + aoff + wbo;
+        const char* abase = sg + aoff + wbo;
         const char* bbase[NI];
 #pragma unroll
-        for (int j = 0; j < NI; ++j) bbase[j] = smem + boff[j] + hbo;
+        for (int j = 0; j < NI; ++j) bbase[j] = sg + boff[j] + hbo;
         auto rdA = [&](int tl, int P, f16x8 (&a)[2]) {
 #pragma unroll
           for (int i = 0; i < 2; ++i)
@@ -1223,6 +1236,28 @@ conv3x3_f16x3_v2_kernel(stx_conv_params p, int tiles_x, int ntiles) {
         }
         __syncthreads();  // this step's reads done; the staged buffers are complete
       }
+    }
+    if constexpr (K2) {
+      // group 1's accumulators -> LDS (the loop buffers are dead after its last barrier),
+      // group 0 adds them; group 1 ends here
+      float* red = reinterpret_cast<float*>(smem);
+      if (gk == 1) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[(((wave * 2 + i) * NI + j) * 16 + r) * 64 + lane] = acc[i][j][r];
+      }
+      __syncthreads();
+      if (gk == 1) return;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] += red[(((wave * 2 + i) * NI + j) * 16 + r) * 64 + lane];
+      __syncthreads();  // (the epilogue reuses this LDS)
     }
 
     EpiTile et{n, co0, ty0, tx0, wm, wn, h, l32};
@@ -1787,10 +1822,19 @@ weight_compose16_kernel(const float* __restrict__ A, int pitch, const float* __r
 }
 
 // stx_conv_params.unpool_out (validated by stx_conv2d): 32 x 4 tiles of d, 64 couts
+// (K2 -- two chunk groups per block -- when the grid is at most one block per CU and
+// the chunk count is even)
 static int launch16_unpool(const stx_conv_params& p, hipStream_t st) {
   const int tiles_x = p.wo / 32, ntiles = tiles_x * (p.ho / 4);
-  hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<32, STX_IN_RAW, 4, 1>), dim3(ntiles, p.cout / 64, p.n),
-                     dim3(256), 0, st, p, tiles_x, ntiles);
+  const dim3 grid(ntiles, p.cout / 64, p.n);
+  const bool k2 = STX_KNOB("STX_CONV_K2", 1) != 0 && cdiv(p.cin, 16) % 2 == 0 &&
+                  (long long)ntiles * (p.cout / 64) * p.n <= cus16();
+  if (k2)
+    hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<32, STX_IN_RAW, 4, 1, 1, true>), grid, dim3(512),
+                       0, st, p, tiles_x, ntiles);
+  else
+    hipLaunchKernelGGL((conv3x3_f16x3_v2_kernel<32, STX_IN_RAW, 4, 1>), grid, dim3(256), 0, st, p,
+                       tiles_x, ntiles);
   return check_launch("stx_conv2d(f16x3 v2 + unpool / Gram-backward epilogue)");
 }
 

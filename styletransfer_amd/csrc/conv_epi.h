@@ -57,7 +57,8 @@ __device__ __forceinline__ void atomic_max_abs(float* slot, float m) {
 // one of the group's STX_AMAX_SLOTS slots: same-address atomics serialise at
 // ~12-15 ns each chip-wide (8192 of them stalled a 64 MB pass for 100 us; 1024 at a
 // conv's tail cost ~15 us)
-__device__ __forceinline__ void block_max_to(float* group, float m) {
+// nwaves: the waves taking part (0: the whole block; a K2 block's epilogue runs on 4)
+__device__ __forceinline__ void block_max_to(float* group, float m, int nwaves = 0) {
   __shared__ float red[16];  // up to 1024-thread blocks
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -69,7 +70,8 @@ __device__ __forceinline__ void block_max_to(float* group, float m) {
   lds_sync();  // (not a __syncthreads: the caller's output stores need not drain first)
   if (tid == 0) {
     float r = red[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
+    const int nw = nwaves > 0 ? nwaves : (int)(blockDim.x >> 6);
+    for (int i = 1; i < nw; ++i) r = (red[i] != red[i]) ? red[i] : fmaxf(r, red[i]);
     const int bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
     atomic_max_abs(group + (bid & (STX_AMAX_SLOTS - 1)), fabsf(r));
   }
