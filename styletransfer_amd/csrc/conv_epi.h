@@ -558,6 +558,9 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
           auxv[j][i][r] = buf_ld(raux, vo[j] + (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * pb);
   }
   const bool rows_full = rows >= 64;
+  // (a tile with cout <= 32 in it -- the ITN's 32-channel layers: its second 32-row MFMA
+  // tile holds only padding, whose stores fall outside the descriptor anyway)
+  const bool half = rows <= 32;
   uint32_t lmask[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) lmask[j] = lane_ok[j] ? 0x7fffffffu : 0u;
@@ -566,6 +569,7 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
   for (int j = 0; j < NI; ++j) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (i == 1 && half && !ROWPAIR) break;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = i * 32 + (r & 3) + 8 * (r >> 2);
@@ -584,7 +588,8 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
     // the lane's two N-tiles are the neighbouring pixels 2 l32 and 2 l32 + 1: one 8-B store
     // per row (a 4-B store where the odd pixel is past a ragged right edge)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
+      if (i == 1 && half) break;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const uint32_t o = vo[0] + (uint32_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * pb;
@@ -596,6 +601,7 @@ __device__ __forceinline__ void conv_epilogue_plain_body(f32x16 (&acc)[2][NI],
           buf_st(ry, o, acc[i][0][r]);
         }
       }
+    }
   }
   if constexpr (ROWPAIR) if (p.pool_out) {
     // relu(maxpool2x2(y)) = maxpool2x2(relu(y)) -> pool_out [n][cout][ho/2][wo/2]
