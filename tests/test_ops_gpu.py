@@ -237,6 +237,48 @@ def test_adam_multiblock_graph(dev, n):
     assert rel(p, pr.detach().to(dev)) < 1e-6
 
 
+def test_graph_capture_with_cyclic_garbage(dev):
+    """ops.graph_capture: a CUDAGraph left in a reference cycle (a finished engine) must not
+    be collected while another stream captures -- HIP refuses the destruction mid-capture
+    (hipErrorStreamCaptureUnsupported, an abort).  The capture body here allocates enough
+    Python objects to cross the collector's thresholds; the helper collected before and
+    holds the collector off until the capture ends."""
+    import gc
+
+    class Engine:
+        pass
+
+    x = torch.ones(1024, device=dev)  # (captured work runs only on replay)
+    for _ in range(3):
+        e = Engine()
+        e.me = e  # a cycle: only the cyclic collector frees it
+        e.graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with ops.graph_capture(e.graph):
+                x.add_(1.0)
+        torch.cuda.current_stream().wait_stream(s)
+        del e
+    assert gc.isenabled()
+    g2 = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with ops.graph_capture(g2):
+            junk = []
+            for i in range(20000):  # well past gc's generation-0 threshold
+                d = {"i": i}
+                d["self"] = d
+                junk.append(d)
+            x.mul_(2.0)
+    torch.cuda.current_stream().wait_stream(s)
+    assert gc.isenabled()
+    g2.replay()
+    torch.cuda.synchronize()
+    assert float(x[0]) == 2.0  # only g2 replayed
+
+
 def test_adam_step_clear(dev):
     """stx_adam_step_clear (the Gatys engine's Adam launch that also zeroes its amax
     groups for the next iteration): the same update bits as stx_adam_step, and the clear
